@@ -1,0 +1,265 @@
+#!/usr/bin/env python3
+"""Headline benchmark (BASELINE.json): device-resident GiB/s of LZ4 block
+decompression, 4 MiB blocks, 4096 blocks in HBM per GPU (configs[1]).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
+
+A step = one launch of the LZ4 decode kernel over the rank's whole batch.
+Blocks are independent, so ranks shard them with no data-path collective
+(weak scaling: every rank decodes its own 4096 blocks); torch.distributed is
+used only for the barrier and the max-over-ranks time.  Inputs are synthetic
+text-like blocks generated on the GPU and compressed by the GPU
+encoder (byte-identical to LZ4_compress_default) before timing; the decoded
+output is checked against the original on the device after timing.
+
+Extra fields: roofline (HIP-event timed kernel, algorithmic bytes C+U per
+launch vs 8 TB/s), cpu_baseline (the CPU oracle on this host's cores, bounded
+sample), host_path (PCIe-inclusive rate through the C ABI's batch API).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--blocks", type=int, default=4096)
+    p.add_argument("--block-bytes", type=int, default=4 << 20)
+    p.add_argument("--cls", default="T")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-host-path", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=6.0, help="wall budget per CPU baseline leg")
+    p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    return p.parse_args()
+
+
+def host_threads() -> int:
+    try:
+        n = len(os.sched_getaffinity(0))
+    except Exception:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))  # the GPU box's CPU share is 16
+
+
+def cpu_baseline(comp_blocks, U, seconds):
+    """Time the CPU oracle (test infrastructure, kind "port") decompressing a
+    bounded sample of the same compressed blocks on this host's cores."""
+    from tests.oracle_ctypes import Oracle
+    so = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
+    if not os.path.exists(so):
+        return None
+    orc = Oracle(so)
+    T = host_threads()
+    bufs = [ctypes.create_string_buffer(c, len(c)) for c in comp_blocks]
+    counts = [0] * T
+    stop = [False]
+
+    def work(t):
+        out = ctypes.create_string_buffer(U)
+        k = t
+        while not stop[0]:
+            c = bufs[k % len(bufs)]
+            r = orc.lib.oracle_lz4_decompress_safe(c, out, len(c) - 0, U)
+            assert r == U
+            counts[t] += 1
+            k += T
+
+    # size the run: each thread loops over the sample until the time budget ends
+    th = [threading.Thread(target=work, args=(t,)) for t in range(T)]
+    t0 = time.perf_counter()
+    [x.start() for x in th]
+    time.sleep(seconds)
+    stop[0] = True
+    [x.join() for x in th]
+    dt = time.perf_counter() - t0
+    nb = sum(counts)
+    return {"value": nb * U / dt / 2**30, "unit": "GiB/s", "cores": T, "kind": "port",
+            "sample": f"{nb} decodes of {len(bufs)} distinct 4 MiB text blocks (oracle/lz4_oracle.c, -O2), "
+                      f"{T} threads, {dt:.1f} s wall"}
+
+
+def liblz4_baseline(comp_blocks, U, seconds):
+    """The C library pkg/compress reaches through cgo (LZ4_decompress_safe), if
+    the host has one; reported beside the oracle."""
+    for path in ("/opt/conda/lib/liblz4.so.1", "/usr/lib/x86_64-linux-gnu/liblz4.so.1"):
+        if os.path.exists(path):
+            break
+    else:
+        return None
+    lz = ctypes.CDLL(path)
+    T = host_threads()
+    bufs = [ctypes.create_string_buffer(c, len(c)) for c in comp_blocks]
+    counts = [0] * T
+    stop = [False]
+
+    def work(t):
+        out = ctypes.create_string_buffer(U)
+        k = t
+        while not stop[0]:
+            c = bufs[k % len(bufs)]
+            r = lz.LZ4_decompress_safe(c, out, len(c), U)
+            assert r == U
+            counts[t] += 1
+            k += T
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(T)]
+    t0 = time.perf_counter()
+    [x.start() for x in th]
+    time.sleep(seconds)
+    stop[0] = True
+    [x.join() for x in th]
+    dt = time.perf_counter() - t0
+    return {"value": sum(counts) * U / dt / 2**30, "unit": "GiB/s", "cores": T,
+            "library": f"{path} v{lz.LZ4_versionNumber()}"}
+
+
+def host_path_rate(comp_blocks, U, reps=3):
+    """PCIe-inclusive: host buffers -> pinned -> HBM -> kernel -> host, via the
+    C ABI batch entry point (what the cgo drop-in calls)."""
+    from juicefs_amd import compress as C
+    c = C.LZ4()
+    pairs = [(bytearray(U), cb) for cb in comp_blocks]
+    c.DecompressBatch(pairs[:4])
+    best = 0.0
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        res = c.DecompressBatch(pairs)
+        dt = time.perf_counter() - t0
+        assert all(n == U and e is None for n, e in res)
+        best = max(best, len(pairs) * U / dt / 2**30)
+    return {"value": best, "unit": "GiB/s", "blocks": len(pairs),
+            "path": "jfs_decompress_batch: host memcpy -> pinned -> H2D -> kernel -> D2H -> host (1 GPU)"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from juicefs_amd import device as D
+
+    U, nblk = a.block_bytes, a.blocks
+    t_setup = time.perf_counter()
+    batch = D.Lz4Batch(nblk, U, a.cls, seed_base=1 + rank * nblk, device=dev)
+    C = batch.comp_bytes
+    setup_s = time.perf_counter() - t_setup
+
+    stream = torch.cuda.current_stream()
+    for _ in range(a.warmup):
+        batch.decompress(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        ev[i][0].record(stream)
+        batch.decompress(stream)
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+    kms = [s.elapsed_time(e) for s, e in ev]
+    kern_s = float(np.mean(kms)) / 1e3
+    ok = batch.verify()
+    okt = torch.tensor([1 if ok else 0], device=dev)
+    if world > 1:
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+    if int(okt.item()) != 1:
+        raise SystemExit("decoded output mismatch: benchmark invalid")
+
+    ms_per_step = elapsed / a.steps * 1e3
+    value = world * nblk * U * a.steps / elapsed / 2**30
+    achieved = (C + nblk * U) / kern_s / 1e9
+    traffic = None
+    if os.path.exists(a.traffic_file):
+        try:
+            tj = json.load(open(a.traffic_file))
+            if tj.get("blocks") == nblk and tj.get("block_bytes") == U:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    out = {
+        "metric": "device-resident GiB/s (de)compress, 4 MiB blocks, LZ4+Zstd, 1/2/4/8 MI355X",
+        "value": value,
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (text-like blocks generated on GPU, SURVEY.md 8d; LZ4-compressed on GPU)",
+        "config": {
+            "workload": "LZ4 decompress, 4096x4MiB blocks already in HBM (BASELINE configs[1])",
+            "blocks_per_gpu": nblk, "block_bytes": U, "class": a.cls,
+            "compressed_bytes_per_gpu": C, "ratio": nblk * U / C,
+            "parallelism": f"{world} process(es), one per GPU, blocks sharded, no collective",
+        },
+        "roofline": {
+            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            "kernel": "jfs::lz4d::lz4_decode_kernel", "kernel_ms": kern_s * 1e3,
+            "algorithmic_bytes_per_launch": C + nblk * U,
+            "u_only_TBps": nblk * U / kern_s / 1e12,
+        },
+        "setup_s": setup_s,
+    }
+    if rank == 0 and world == 1:
+        comp_np = batch.comp.cpu().numpy() if False else None
+        # bounded sample for the CPU legs: 32 distinct blocks
+        ns = min(32, nblk)
+        comp_blocks = []
+        for i in range(ns):
+            s0 = i * batch.slot
+            comp_blocks.append(batch.comp[s0:s0 + int(batch.csize[i])].cpu().numpy().tobytes())
+        if not a.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(comp_blocks, U, a.cpu_seconds)
+            lb = liblz4_baseline(comp_blocks, U, a.cpu_seconds / 2)
+            if lb:
+                out["cpu_liblz4"] = lb
+        if not a.no_host_path:
+            try:
+                out["host_path"] = host_path_rate(comp_blocks * 8, U)
+            except Exception as e:  # report, never fake
+                out["host_path"] = {"error": str(e)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,123 @@
+/*
+ * jfs_gpucodec.h -- C ABI of libjfsgpu.so, the MI355X block-compression engine
+ * that drops in under JuiceFS's pkg/compress.
+ *
+ * Plain C types only (pointers + sizes); no torch / HIP types in signatures.
+ * A stream argument is a hipStream_t passed as void* (0 = the library's own
+ * per-device stream).
+ *
+ * Reference interface replaced (file:line in /root/reference):
+ *   pkg/compress/compress.go:31-36   type Compressor interface {Name, CompressBound, Compress, Decompress}
+ *   pkg/compress/compress.go:39-49   func NewCompressor(algr string) Compressor
+ *   pkg/compress/compress.go:51-68   noOp            (Name "Noop")
+ *   pkg/compress/compress.go:70-103  ZStandard{1}    (Name "Zstd", level ZSTD_LEVEL=1 :28)
+ *   pkg/compress/compress.go:105-125 LZ4             (Name "LZ4")
+ * Callers: pkg/chunk/cached_store.go:359,372 (upload), :764,814 (load),
+ *          :827,846 (NewCachedStore), cmd/format.go:445 (validation).
+ * The cgo binding a maintainer adds on the Go side is shown in INTEGRATION.md.
+ */
+#ifndef JFS_GPUCODEC_H
+#define JFS_GPUCODEC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Codec ids (the three values NewCompressor can return). */
+#define JFS_ALGO_NONE 0 /* noOp       compress.go:51  */
+#define JFS_ALGO_LZ4 1  /* LZ4{}      compress.go:106 */
+#define JFS_ALGO_ZSTD 2 /* ZStandard  compress.go:71  */
+
+/* Status codes returned by the library (<0).  LZ4 decompression failures
+ * return the raw LZ4_decompress_safe value instead (also negative), because
+ * lz4.DecompressSafe passes it through to the Go caller (compress.go:124). */
+#define JFS_OK 0
+#define JFS_ERR_SHORT_BUFFER (-1000001)  /* "buffer too short: %d < %d"   compress.go:57,64,88,100 */
+#define JFS_ERR_EMPTY_INPUT (-1000002)   /* "decompress an empty input"   compress.go:122 / zstd ErrEmptySlice */
+#define JFS_ERR_CORRUPT (-1000003)       /* malformed Zstd frame (ZSTD_decompress error) */
+#define JFS_ERR_COMPRESS_FAIL (-1000004) /* LZ4_compress_default returned 0 */
+#define JFS_ERR_UNSUPPORTED (-1000005)   /* operation not available (e.g. Zstd encode on GPU) */
+#define JFS_ERR_NO_DEVICE (-1000006)     /* no usable gfx950 device; the library never falls back to CPU */
+#define JFS_ERR_INVALID (-1000007)       /* bad argument (unknown algo, negative size, ...) */
+#define JFS_ERR_HIP (-1000008)           /* HIP runtime failure */
+
+/* ---- Compressor surface (one synchronous call per block) ---------------- */
+
+/* NewCompressor(algr): case-insensitive "zstd" | "lz4" | "none" | "" -> algo id,
+ * anything else -> -1 (the Go factory's nil).                 compress.go:39-49 */
+int jfs_codec_from_name(const char *name);
+
+/* Name(): "Noop" / "LZ4" / "Zstd"; NULL for an unknown id.
+ *                                                compress.go:53,76,109 */
+const char *jfs_codec_name(int algo);
+
+/* CompressBound(n).  LZ4: n>0x7E000000 ? 0 : n + n/255 + 16 (compress.go:112);
+ * Zstd: n + n>>8 + (n < 128K ? (128K-n)>>11 : 0) (compress.go:79); none: n. */
+int64_t jfs_compress_bound(int algo, int64_t n);
+
+/* Compress(dst, src) -> bytes written (>=0) or a JFS_ERR_* code.
+ * dst_cap is len(dst) for LZ4/none and cap(dst) for Zstd (DataDog/zstd writes
+ * into dst[:cap]; compress.go:83-89).  LZ4 output is byte-identical to
+ * LZ4_compress_default; a dst smaller than the compressed size fails
+ * (JFS_ERR_COMPRESS_FAIL), like lz4.CompressDefault returning 0. */
+int64_t jfs_compress(int algo, uint8_t *dst, int64_t dst_cap, const uint8_t *src, int64_t n);
+
+/* Decompress(dst, src) -> bytes written (>=0) or <0.
+ * LZ4: empty src -> JFS_ERR_EMPTY_INPUT (compress.go:121-123); otherwise the
+ * exact LZ4_decompress_safe(src, dst, n, dst_cap) result.
+ * Zstd: empty src -> JFS_ERR_EMPTY_INPUT; frame(s) larger than dst_cap ->
+ * JFS_ERR_SHORT_BUFFER (compress.go:99-101); malformed -> JFS_ERR_CORRUPT. */
+int64_t jfs_decompress(int algo, uint8_t *dst, int64_t dst_cap, const uint8_t *src, int64_t n);
+
+/* ---- Batch surface (host buffers; FillCache / compaction / aggregator) ----
+ * Blocks are independent; they are dealt round-robin over the devices in
+ * device_mask (bit d = device d; 0 = all visible devices) and staged through
+ * pinned host memory with async copies.  out_n[i] receives what the
+ * single-block call would have returned for block i.  Returns JFS_OK or a
+ * JFS_ERR_* code for failures that are not per-block. */
+typedef struct jfs_iov {
+    const uint8_t *src;
+    int64_t src_len;
+    uint8_t *dst;
+    int64_t dst_cap;
+} jfs_iov;
+
+int jfs_compress_batch(int algo, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t device_mask);
+int jfs_decompress_batch(int algo, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t device_mask);
+
+/* ---- Device-resident surface (inputs/outputs already in HBM) ------------
+ * One descriptor per block; all pointers are device pointers on the current
+ * device.  ret[i] is written with the single-block result.  Asynchronous on
+ * `stream`.  `scratch`/`scratch_bytes` as returned by jfs_*_scratch_size (may
+ * be 0 when that returns 0). */
+typedef struct jfs_dev_block {
+    const uint8_t *src;
+    uint8_t *dst;
+    int32_t src_len;
+    int32_t dst_cap;
+} jfs_dev_block;
+
+int jfs_lz4_decompress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream);
+int jfs_lz4_compress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream);
+int jfs_zstd_decompress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream);
+
+/* ---- Runtime / utilities ------------------------------------------------- */
+
+/* Number of usable gfx950 devices (0 when none; never an error). */
+int jfs_device_count(void);
+/* Library version string. */
+const char *jfs_version(void);
+
+/* Synthetic benchmark input: block i of class cls
+ * ('T','Z','R') with seed base+i, each `block_bytes` long, written
+ * back-to-back at d_dst (device pointer) on `stream`.  Host twin below. */
+int jfs_gen_blocks_device(uint8_t *d_dst, int nblk, int64_t block_bytes, char cls, uint64_t seed_base,
+                          void *stream);
+void jfs_gen_block_host(uint8_t *dst, int64_t n, char cls, uint64_t seed);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* JFS_GPUCODEC_H */

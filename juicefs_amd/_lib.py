@@ -1,0 +1,81 @@
+"""Loader for libjfsgpu.so (the HIP kernels + C ABI in include/jfs_gpucodec.h).
+
+The library is built in-tree (``juicefs_amd/lib/libjfsgpu.so``) by
+``__graft_entry__.build()`` / ``make -C juicefs_amd/csrc``.  There is no
+fallback: if the library is missing, importing the codec raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libjfsgpu.so")
+
+ALGO_NONE, ALGO_LZ4, ALGO_ZSTD = 0, 1, 2
+JFS_OK = 0
+JFS_ERR_SHORT_BUFFER = -1000001
+JFS_ERR_EMPTY_INPUT = -1000002
+JFS_ERR_CORRUPT = -1000003
+JFS_ERR_COMPRESS_FAIL = -1000004
+JFS_ERR_UNSUPPORTED = -1000005
+JFS_ERR_NO_DEVICE = -1000006
+JFS_ERR_INVALID = -1000007
+JFS_ERR_HIP = -1000008
+
+# every symbol include/jfs_gpucodec.h declares
+EXPORTS = [
+    "jfs_codec_from_name", "jfs_codec_name", "jfs_compress_bound", "jfs_compress", "jfs_decompress",
+    "jfs_compress_batch", "jfs_decompress_batch", "jfs_lz4_decompress_device", "jfs_lz4_compress_device",
+    "jfs_zstd_decompress_device", "jfs_device_count", "jfs_version", "jfs_gen_blocks_device",
+    "jfs_gen_block_host",
+]
+
+
+class JfsIov(ctypes.Structure):
+    _fields_ = [("src", ctypes.c_void_p), ("src_len", ctypes.c_int64),
+                ("dst", ctypes.c_void_p), ("dst_cap", ctypes.c_int64)]
+
+
+class JfsDevBlock(ctypes.Structure):
+    _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p),
+                ("src_len", ctypes.c_int32), ("dst_cap", ctypes.c_int32)]
+
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libjfsgpu.so; raises if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} not built: run `make -C juicefs_amd/csrc` (or __graft_entry__.build())")
+    lib = ctypes.CDLL(LIB_PATH)
+    i64, i32, vp, u32 = ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p, ctypes.c_uint32
+    lib.jfs_codec_from_name.argtypes = [ctypes.c_char_p]
+    lib.jfs_codec_from_name.restype = ctypes.c_int
+    lib.jfs_codec_name.argtypes = [ctypes.c_int]
+    lib.jfs_codec_name.restype = ctypes.c_char_p
+    lib.jfs_compress_bound.argtypes = [ctypes.c_int, i64]
+    lib.jfs_compress_bound.restype = i64
+    for f in (lib.jfs_compress, lib.jfs_decompress):
+        f.argtypes = [ctypes.c_int, vp, i64, vp, i64]
+        f.restype = i64
+    for f in (lib.jfs_compress_batch, lib.jfs_decompress_batch):
+        f.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(JfsIov), ctypes.POINTER(i64), u32]
+        f.restype = ctypes.c_int
+    for f in (lib.jfs_lz4_decompress_device, lib.jfs_lz4_compress_device, lib.jfs_zstd_decompress_device):
+        f.argtypes = [vp, ctypes.c_int, vp, vp]
+        f.restype = ctypes.c_int
+    lib.jfs_device_count.argtypes = []
+    lib.jfs_device_count.restype = ctypes.c_int
+    lib.jfs_version.argtypes = []
+    lib.jfs_version.restype = ctypes.c_char_p
+    lib.jfs_gen_blocks_device.argtypes = [vp, ctypes.c_int, i64, ctypes.c_char, ctypes.c_uint64, vp]
+    lib.jfs_gen_blocks_device.restype = ctypes.c_int
+    lib.jfs_gen_block_host.argtypes = [vp, i64, ctypes.c_char, ctypes.c_uint64]
+    lib.jfs_gen_block_host.restype = None
+    _lib = lib
+    return lib

@@ -1,0 +1,169 @@
+"""Python mirror of JuiceFS pkg/compress over libjfsgpu.so.
+
+Same names, argument meaning and error behaviour as
+/root/reference/pkg/compress/compress.go so the parity tests read like the
+reference's own compress_test.go:
+
+    ZSTD_LEVEL = 1                                   compress.go:28
+    class Compressor (Name / CompressBound / Compress / Decompress)   :31-36
+    NewCompressor(algr) -> Compressor | None        :39-49
+    noOp / ZStandard / LZ4                           :51-125
+
+Go's ``(int, error)`` results become ``(n, err)`` tuples with ``err`` either
+``None`` or a :class:`CompressError`.  ``dst`` must be a writable buffer
+(bytearray / memoryview / numpy array); ``src`` any bytes-like object.  For
+Zstd the capacity is ``len(dst)`` (Go passes ``cap(dst)``).
+
+Every LZ4 byte is produced by the HIP kernels in libjfsgpu.so; there is no CPU
+fallback (the library returns ``JFS_ERR_NO_DEVICE`` without a gfx950 GPU).
+"""
+from __future__ import annotations
+
+import ctypes
+
+from . import _lib as L
+
+ZSTD_LEVEL = 1
+
+
+class CompressError(Exception):
+    def __init__(self, msg: str, code: int):
+        super().__init__(msg)
+        self.code = code
+
+
+def _addr(buf, writable: bool):
+    """Return (c_void_p, length, keepalive) for a buffer."""
+    if buf is None:
+        return None, 0, None
+    mv = memoryview(buf)
+    if not mv.contiguous:
+        raise ValueError("buffer must be contiguous")
+    mv = mv.cast("B")
+    n = mv.nbytes
+    if n == 0:
+        return None, 0, mv
+    if writable:
+        if mv.readonly:
+            raise ValueError("dst must be writable")
+        c = (ctypes.c_char * n).from_buffer(mv)
+    else:
+        if mv.readonly:
+            c = ctypes.create_string_buffer(bytes(mv), n)  # copy of read-only input
+        else:
+            c = (ctypes.c_char * n).from_buffer(mv)
+    return ctypes.cast(c, ctypes.c_void_p), n, (mv, c)
+
+
+def _err(code: int, dst_len: int, src_len: int, op: str) -> CompressError:
+    if code == L.JFS_ERR_SHORT_BUFFER:
+        return CompressError(f"buffer too short: {dst_len} < {src_len}", code)
+    if code == L.JFS_ERR_EMPTY_INPUT:
+        return CompressError("decompress an empty input", code)
+    if code == L.JFS_ERR_COMPRESS_FAIL:
+        return CompressError("lz4: compression failed (destination too small)", code)
+    if code == L.JFS_ERR_CORRUPT:
+        return CompressError("zstd: corrupted frame", code)
+    if code == L.JFS_ERR_UNSUPPORTED:
+        return CompressError(f"{op}: not supported by the GPU engine", code)
+    if code == L.JFS_ERR_NO_DEVICE:
+        return CompressError("no usable gfx950 device", code)
+    if code <= -1000000:
+        return CompressError(f"{op}: error {code}", code)
+    return CompressError(f"lz4: decompress failed ({code})", code)
+
+
+class Compressor:
+    """compress.go:31-36"""
+
+    algo: int = -1
+
+    def Name(self) -> str:
+        return L.load().jfs_codec_name(self.algo).decode()
+
+    def CompressBound(self, n: int) -> int:
+        return int(L.load().jfs_compress_bound(self.algo, n))
+
+    def Compress(self, dst, src):
+        d, dn, kd = _addr(dst, True)
+        s, sn, ks = _addr(src, False)
+        r = int(L.load().jfs_compress(self.algo, d, dn, s, sn))
+        if r < 0:
+            return 0, _err(r, dn, sn, "compress")
+        return r, None
+
+    def Decompress(self, dst, src):
+        d, dn, kd = _addr(dst, True)
+        s, sn, ks = _addr(src, False)
+        r = int(L.load().jfs_decompress(self.algo, d, dn, s, sn))
+        if r < 0:
+            # LZ4 passes LZ4_decompress_safe's negative value through (compress.go:124);
+            # the other adapters return 0 with the error (compress.go:57-100).
+            n = r if (self.algo == L.ALGO_LZ4 and r > -1000000) else 0
+            return n, _err(r, dn, sn, "decompress")
+        return r, None
+
+    # batch helpers (host buffers) -------------------------------------------
+    def CompressBatch(self, pairs, device_mask: int = 0):
+        return _batch(self.algo, pairs, device_mask, compress=True)
+
+    def DecompressBatch(self, pairs, device_mask: int = 0):
+        return _batch(self.algo, pairs, device_mask, compress=False)
+
+
+class noOp(Compressor):  # noqa: N801  (reference name, compress.go:51)
+    algo = L.ALGO_NONE
+
+
+class ZStandard(Compressor):
+    """compress.go:70-103; level is fixed at ZSTD_LEVEL (1)."""
+
+    algo = L.ALGO_ZSTD
+
+    def __init__(self, level: int = ZSTD_LEVEL):
+        self.level = level
+
+
+class LZ4(Compressor):
+    """compress.go:105-125"""
+
+    algo = L.ALGO_LZ4
+
+
+def NewCompressor(algr: str):
+    """compress.go:39-49: case-insensitive "zstd" / "lz4" / "none" / ""; else None."""
+    a = L.load().jfs_codec_from_name(algr.encode())
+    if a == L.ALGO_ZSTD:
+        return ZStandard(ZSTD_LEVEL)
+    if a == L.ALGO_LZ4:
+        return LZ4()
+    if a == L.ALGO_NONE:
+        return noOp()
+    return None
+
+
+def _batch(algo: int, pairs, device_mask: int, compress: bool):
+    """pairs: list of (dst, src).  Returns list of (n, err)."""
+    lib = L.load()
+    nb = len(pairs)
+    iov = (L.JfsIov * max(nb, 1))()
+    keep = []
+    for i, (dst, src) in enumerate(pairs):
+        d, dn, kd = _addr(dst, True)
+        s, sn, ks = _addr(src, False)
+        keep.append((kd, ks))
+        iov[i].src, iov[i].src_len, iov[i].dst, iov[i].dst_cap = s, sn, d, dn
+    out = (ctypes.c_int64 * max(nb, 1))()
+    fn = lib.jfs_compress_batch if compress else lib.jfs_decompress_batch
+    rc = fn(algo, nb, iov, out, device_mask)
+    if rc != 0:
+        raise _err(rc, 0, 0, "batch")
+    res = []
+    for i in range(nb):
+        r = int(out[i])
+        if r < 0:
+            n = r if (algo == L.ALGO_LZ4 and not compress and r > -1000000) else 0
+            res.append((n, _err(r, iov[i].dst_cap, iov[i].src_len, "compress" if compress else "decompress")))
+        else:
+            res.append((r, None))
+    return res

@@ -1,0 +1,110 @@
+"""Device-resident batch helpers (torch tensors in HBM -> libjfsgpu device API).
+
+PyTorch is only plumbing here: it owns the HBM allocations and the stream; the
+byte work is the HIP kernels behind ``jfs_lz4_decompress_device`` /
+``jfs_lz4_compress_device`` / ``jfs_zstd_decompress_device``.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib as L
+
+DESC_DTYPE = np.dtype([("src", "<u8"), ("dst", "<u8"), ("src_len", "<i4"), ("dst_cap", "<i4")])
+assert DESC_DTYPE.itemsize == ctypes.sizeof(L.JfsDevBlock)
+
+
+def make_desc(src: torch.Tensor, src_offs, src_lens, dst: torch.Tensor, dst_offs, dst_caps) -> torch.Tensor:
+    """Build a device tensor of jfs_dev_block descriptors (24 bytes each)."""
+    n = len(src_offs)
+    a = np.zeros(n, dtype=DESC_DTYPE)
+    a["src"] = src.data_ptr() + np.asarray(src_offs, dtype=np.uint64)
+    a["dst"] = dst.data_ptr() + np.asarray(dst_offs, dtype=np.uint64)
+    a["src_len"] = np.asarray(src_lens, dtype=np.int32)
+    a["dst_cap"] = np.asarray(dst_caps, dtype=np.int32)
+    t = torch.from_numpy(a.view(np.uint8).copy())
+    return t.to(src.device)
+
+
+def _stream_ptr(stream) -> int:
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return stream.cuda_stream
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed: {rc}")
+
+
+def lz4_decompress(desc: torch.Tensor, ret: torch.Tensor, stream=None):
+    n = desc.numel() // DESC_DTYPE.itemsize
+    _check(L.load().jfs_lz4_decompress_device(desc.data_ptr(), n, ret.data_ptr(), _stream_ptr(stream)),
+           "jfs_lz4_decompress_device")
+
+
+def lz4_compress(desc: torch.Tensor, ret: torch.Tensor, stream=None):
+    n = desc.numel() // DESC_DTYPE.itemsize
+    _check(L.load().jfs_lz4_compress_device(desc.data_ptr(), n, ret.data_ptr(), _stream_ptr(stream)),
+           "jfs_lz4_compress_device")
+
+
+def zstd_decompress(desc: torch.Tensor, ret: torch.Tensor, stream=None):
+    n = desc.numel() // DESC_DTYPE.itemsize
+    _check(L.load().jfs_zstd_decompress_device(desc.data_ptr(), n, ret.data_ptr(), _stream_ptr(stream)),
+           "jfs_zstd_decompress_device")
+
+
+def gen_blocks(out: torch.Tensor, nblk: int, block_bytes: int, cls: str, seed_base: int, stream=None):
+    """Fill out[0 : nblk*block_bytes] with synthetic blocks."""
+    assert out.numel() >= nblk * block_bytes
+    _check(L.load().jfs_gen_blocks_device(out.data_ptr(), nblk, block_bytes, cls.encode(), seed_base,
+                                          _stream_ptr(stream)), "jfs_gen_blocks_device")
+
+
+def lz4_bound(n: int) -> int:
+    return n + n // 255 + 16
+
+
+class Lz4Batch:
+    """A batch of equal-size blocks resident in HBM: raw, compressed, decoded.
+
+    Compressed block i lives at comp[i*slot : i*slot + csize[i]] with
+    slot = bound rounded up to 256 bytes (16-byte aligned slots).
+    """
+
+    def __init__(self, nblk: int, block_bytes: int, cls: str = "T", seed_base: int = 1, device="cuda"):
+        self.nblk, self.U = nblk, block_bytes
+        self.slot = (lz4_bound(block_bytes) + 255) // 256 * 256
+        self.device = torch.device(device)
+        self.raw = torch.empty(nblk * block_bytes, dtype=torch.uint8, device=self.device)
+        gen_blocks(self.raw, nblk, block_bytes, cls, seed_base)
+        self.comp = torch.empty(nblk * self.slot, dtype=torch.uint8, device=self.device)
+        self.ret = torch.empty(nblk, dtype=torch.int32, device=self.device)
+        offs = np.arange(nblk, dtype=np.int64)
+        self.enc_desc = make_desc(self.raw, offs * block_bytes, [block_bytes] * nblk, self.comp, offs * self.slot,
+                                  [self.slot] * nblk)
+        lz4_compress(self.enc_desc, self.ret)
+        torch.cuda.synchronize()
+        self.csize = self.ret.cpu().numpy().astype(np.int64)
+        if (self.csize <= 0).any():
+            raise RuntimeError("device LZ4 compression failed")
+        self.out = torch.empty(nblk * block_bytes, dtype=torch.uint8, device=self.device)
+        self.dec_desc = make_desc(self.comp, offs * self.slot, self.csize, self.out, offs * block_bytes,
+                                  [block_bytes] * nblk)
+        self.dec_ret = torch.empty(nblk, dtype=torch.int32, device=self.device)
+
+    def decompress(self, stream=None):
+        lz4_decompress(self.dec_desc, self.dec_ret, stream)
+
+    @property
+    def comp_bytes(self) -> int:
+        return int(self.csize.sum())
+
+    def verify(self) -> bool:
+        torch.cuda.synchronize()
+        ok = bool((self.dec_ret == self.U).all().item())
+        return ok and bool(torch.equal(self.out, self.raw))

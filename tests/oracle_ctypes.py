@@ -1,0 +1,40 @@
+"""ctypes binding of the CPU oracle (oracle/_build/liboracle.so) -- test infra only."""
+from __future__ import annotations
+
+import ctypes
+
+
+class Oracle:
+    def __init__(self, path: str):
+        self.lib = lib = ctypes.CDLL(path)
+        vp, i32, i64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
+        lib.oracle_lz4_bound.argtypes = [i64]
+        lib.oracle_lz4_bound.restype = i64
+        lib.oracle_lz4_compress_default.argtypes = [vp, vp, i32, i32]
+        lib.oracle_lz4_compress_default.restype = i32
+        lib.oracle_lz4_decompress_safe.argtypes = [vp, vp, i32, i32]
+        lib.oracle_lz4_decompress_safe.restype = i32
+        self.has_zstd = hasattr(lib, "oracle_zstd_decompress")
+        if self.has_zstd:
+            lib.oracle_zstd_decompress.argtypes = [vp, i64, vp, i64]
+            lib.oracle_zstd_decompress.restype = i64
+
+    def lz4_bound(self, n: int) -> int:
+        return self.lib.oracle_lz4_bound(n)
+
+    def lz4_compress(self, src: bytes, cap: int | None = None):
+        if cap is None:
+            cap = self.lz4_bound(len(src))
+        dst = ctypes.create_string_buffer(max(cap, 1))
+        n = self.lib.oracle_lz4_compress_default(src, dst, len(src), cap)
+        return n, dst.raw[: max(n, 0)]
+
+    def lz4_decompress(self, src: bytes, cap: int):
+        dst = ctypes.create_string_buffer(max(cap, 1))
+        n = self.lib.oracle_lz4_decompress_safe(src, dst, len(src), cap)
+        return n, dst.raw[: max(n, 0)]
+
+    def zstd_decompress(self, src: bytes, cap: int):
+        dst = ctypes.create_string_buffer(max(cap, 1))
+        n = self.lib.oracle_zstd_decompress(src, len(src), dst, cap)
+        return n, dst.raw[: max(n, 0)]

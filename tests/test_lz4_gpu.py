@@ -1,0 +1,204 @@
+"""GPU parity: the HIP LZ4 kernels (through the C ABI) vs the CPU oracle and the
+liblz4 1.9.3 golden vectors.  Bar: bit-exact bytes and exact return values."""
+import hashlib
+import random
+
+import numpy as np
+import pytest
+
+from juicefs_amd import compress as C
+from juicefs_amd.blockgen import gen_block
+
+pytestmark = pytest.mark.gpu
+
+
+def sha(b):
+    return hashlib.sha256(b).hexdigest()
+
+
+def test_compressor_contract_lz4_and_none(gpu):
+    """compress_test.go:25-64 (testCompress) for "lz4" and "none"."""
+    for name in ("lz4", "none"):
+        c = C.NewCompressor(name)
+        src0 = c.Name().encode()
+        for src in (src0, b""):
+            if len(src) > 1:
+                _, err = c.Compress(bytearray(1), src)
+                assert err is not None, "expect short buffer error"
+            dst = bytearray(c.CompressBound(len(src)))
+            n, err = c.Compress(dst, src)
+            assert err is None, err
+            if len(src) > 1:
+                _, err = c.Decompress(bytearray(1), bytes(dst[:n]))
+                assert err is not None, "expect short buffer error"
+            src2 = bytearray(len(src))
+            n2, err = c.Decompress(src2, bytes(dst[:n]))
+            assert err is None, err
+            assert bytes(src2[:n2]) == src
+        if c.CompressBound(0) > 0:
+            n, err = c.Decompress(bytearray(100), src0[:0])
+            assert err is not None and n <= 0
+
+
+def test_lz4_kats_on_gpu(gpu, golden):
+    c = C.LZ4()
+    for k in golden["lz4"]["kat"]:
+        src = bytes.fromhex(k["src"])
+        dst = bytearray(k["bound"])
+        n, err = c.Compress(dst, src)
+        assert err is None and bytes(dst[:n]).hex() == k["comp"]
+        out = bytearray(len(src))
+        if n:
+            m, err = c.Decompress(out, bytes(dst[:n]))
+            assert err is None and m == len(src) and bytes(out) == src
+
+
+BLOCK_CASES = [(cls, n) for cls in "TZR" for n in (1, 12, 13, 100, 4096, 65535, 65547, 131072, 1 << 20)] + [
+    ("T", 4 << 20), ("Z", 4 << 20), ("R", 4 << 20)]
+
+
+def test_lz4_decode_blocks_vs_oracle(gpu, oracle):
+    c = C.LZ4()
+    pairs, want = [], []
+    for i, (cls, n) in enumerate(BLOCK_CASES):
+        src = gen_block(cls, 900 + i, n)
+        _, comp = oracle.lz4_compress(src)
+        for cap in (n, n + 77):
+            pairs.append((bytearray(cap), comp))
+            want.append((n, src))
+        if n > 1:  # short destination: exact negative value from the oracle
+            r, _ = oracle.lz4_decompress(comp, n - 1)
+            pairs.append((bytearray(n - 1), comp))
+            want.append((r, None))
+    res = c.DecompressBatch(pairs)
+    for (dst, comp), (n_exp, src), (n, err) in zip(pairs, want, res):
+        if n_exp >= 0:
+            assert err is None and n == n_exp
+            assert bytes(dst[:n]) == src
+        else:
+            assert err is not None and n == n_exp
+
+
+def test_lz4_decode_corpus_exact(gpu, golden):
+    """Every case of the liblz4 1.9.3 acceptance corpus: same return value
+    (success size or negative error position), same bytes on success."""
+    c = C.LZ4()
+    cases = golden["lz4"]["decode_corpus"]
+    pairs = [(bytearray(max(e["cap"], 0)), bytes.fromhex(e["src"])) for e in cases]
+    res = c.DecompressBatch(pairs)
+    bad = []
+    for e, (dst, _), (n, err) in zip(cases, pairs, res):
+        if e["ret"] >= 0:
+            if not (err is None and n == e["ret"] and sha(bytes(dst[:n])) == e["out_sha"]):
+                bad.append((e, n))
+        else:
+            if not (err is not None and n == e["ret"]):
+                bad.append((e, n))
+    assert not bad, f"{len(bad)} mismatches, first: {bad[:3]}"
+
+
+def test_lz4_encode_golden(gpu, golden):
+    """Byte-identical LZ4_compress_default output (sha256 of liblz4 1.9.3 output),
+    including 4 MiB text blocks and the byU16/byU32 table switch at 65547."""
+    c = C.LZ4()
+    pairs, ents = [], []
+    for b in golden["lz4"]["blocks"]:
+        src = gen_block(b["cls"], b["seed"], b["size"])
+        pairs.append((bytearray(c.CompressBound(len(src))), src))
+        ents.append(b)
+    res = c.CompressBatch(pairs)
+    for (dst, _), b, (n, err) in zip(pairs, ents, res):
+        assert err is None, b
+        assert n == b["csize"] and sha(bytes(dst[:n])) == b["comp_sha"], (b["cls"], b["size"], b["seed"])
+
+
+def test_lz4_encode_limited_output(gpu, golden):
+    c = C.LZ4()
+    cache, pairs, ents = {}, [], []
+    for e in golden["lz4"]["limited"]:
+        key = (e["cls"], e["seed"], e["size"])
+        if key not in cache:
+            cache[key] = gen_block(*key)
+        pairs.append((bytearray(e["cap"]), cache[key]))
+        ents.append(e)
+    res = c.CompressBatch(pairs)
+    for e, (n, err) in zip(ents, res):
+        if e["ret"] == 0:
+            assert err is not None
+        else:
+            assert err is None and n == e["ret"]
+
+
+def test_lz4_encode_vs_oracle_random_sizes(gpu, oracle):
+    rng = random.Random(7)
+    c = C.LZ4()
+    pairs, srcs = [], []
+    for i in range(48):
+        n = rng.choice([rng.randrange(0, 300), rng.randrange(300, 70000), rng.randrange(70000, 600000)])
+        cls = rng.choice("TTTRZ")
+        src = gen_block(cls, 5000 + i, n)
+        if rng.random() < 0.3 and n > 100:  # mixed content
+            k = rng.randrange(n)
+            src = src[:k] + gen_block("R", i, min(5000, n - k)) + src[k + min(5000, n - k):]
+        srcs.append(src)
+        pairs.append((bytearray(c.CompressBound(n)), src))
+    res = c.CompressBatch(pairs)
+    for src, (dst, _), (n, err) in zip(srcs, pairs, res):
+        m, ref = oracle.lz4_compress(src)
+        assert err is None and n == m and bytes(dst[:n]) == ref
+
+
+def test_lz4_single_block_calls_concurrent(gpu, oracle):
+    """One call per block from many threads (pkg/chunk's 200 concurrent
+    downloads); the coalescer batches them."""
+    import threading
+    c = C.LZ4()
+    srcs = [gen_block("T", 70 + i, 65536 + 1000 * i) for i in range(32)]
+    comps = [oracle.lz4_compress(s)[1] for s in srcs]
+    errs = []
+
+    def work(i):
+        out = bytearray(len(srcs[i]))
+        n, err = c.Decompress(out, comps[i])
+        if err is not None or n != len(srcs[i]) or bytes(out) != srcs[i]:
+            errs.append(i)
+        dst = bytearray(c.CompressBound(len(srcs[i])))
+        n, err = c.Compress(dst, srcs[i])
+        if err is not None or bytes(dst[:n]) != comps[i]:
+            errs.append(100 + i)
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(32)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    assert not errs
+
+
+def test_lz4_device_resident_roundtrip(gpu, oracle):
+    """HBM-resident batch (the bench path): generate -> GPU compress -> GPU
+    decompress; compressed bytes checked against the oracle on a sample."""
+    import torch
+    from juicefs_amd import device as D
+    b = D.Lz4Batch(24, 4 << 20, "T", seed_base=11)
+    b.decompress()
+    assert b.verify()
+    raw = b.raw.cpu().numpy()
+    comp = b.comp.cpu().numpy()
+    for i in (0, 7, 23):
+        src = raw[i * b.U:(i + 1) * b.U].tobytes()
+        m, ref = oracle.lz4_compress(src)
+        assert m == b.csize[i]
+        assert comp[i * b.slot:i * b.slot + m].tobytes() == ref
+    # a different output placement: unaligned destinations and sources
+    out = torch.zeros(24 * (b.U + 32), dtype=torch.uint8, device=gpu)
+    src_copy = torch.zeros(24 * (b.slot + 32), dtype=torch.uint8, device=gpu)
+    offs_s = np.array([i * (b.slot + 32) + (i % 13) for i in range(24)])
+    for i in range(24):
+        src_copy[offs_s[i]:offs_s[i] + b.csize[i]] = b.comp[i * b.slot:i * b.slot + b.csize[i]]
+    offs_d = np.array([i * (b.U + 32) + (i * 7) % 16 for i in range(24)])
+    desc = D.make_desc(src_copy, offs_s, b.csize, out, offs_d, [b.U] * 24)
+    ret = torch.empty(24, dtype=torch.int32, device=gpu)
+    D.lz4_decompress(desc, ret)
+    torch.cuda.synchronize()
+    assert (ret == b.U).all()
+    for i in range(24):
+        assert torch.equal(out[offs_d[i]:offs_d[i] + b.U], b.raw[i * b.U:(i + 1) * b.U])
