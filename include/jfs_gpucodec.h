@@ -30,18 +30,20 @@ extern "C" {
 #define JFS_ALGO_LZ4 1  /* LZ4{}      compress.go:106 */
 #define JFS_ALGO_ZSTD 2 /* ZStandard  compress.go:71  */
 
-/* Status codes returned by the library (<0).  LZ4 decompression failures
- * return the raw LZ4_decompress_safe value instead (also negative), because
- * lz4.DecompressSafe passes it through to the Go caller (compress.go:124). */
+/* Status codes returned by the library (int64, all <= JFS_ERR_BASE).  LZ4
+ * decompression failures return the raw LZ4_decompress_safe value instead (a
+ * negative int32), because lz4.DecompressSafe passes it through to the Go
+ * caller (compress.go:124); the two ranges never overlap. */
 #define JFS_OK 0
-#define JFS_ERR_SHORT_BUFFER (-1000001)  /* "buffer too short: %d < %d"   compress.go:57,64,88,100 */
-#define JFS_ERR_EMPTY_INPUT (-1000002)   /* "decompress an empty input"   compress.go:122 / zstd ErrEmptySlice */
-#define JFS_ERR_CORRUPT (-1000003)       /* malformed Zstd frame (ZSTD_decompress error) */
-#define JFS_ERR_COMPRESS_FAIL (-1000004) /* LZ4_compress_default returned 0 */
-#define JFS_ERR_UNSUPPORTED (-1000005)   /* operation not available (e.g. Zstd encode on GPU) */
-#define JFS_ERR_NO_DEVICE (-1000006)     /* no usable gfx950 device; the library never falls back to CPU */
-#define JFS_ERR_INVALID (-1000007)       /* bad argument (unknown algo, negative size, ...) */
-#define JFS_ERR_HIP (-1000008)           /* HIP runtime failure */
+#define JFS_ERR_BASE (-(1LL << 40))
+#define JFS_ERR_SHORT_BUFFER (JFS_ERR_BASE - 1)  /* "buffer too short: %d < %d"   compress.go:57,64,88,100 */
+#define JFS_ERR_EMPTY_INPUT (JFS_ERR_BASE - 2)   /* "decompress an empty input"   compress.go:122 / zstd ErrEmptySlice */
+#define JFS_ERR_CORRUPT (JFS_ERR_BASE - 3)       /* malformed Zstd frame (ZSTD_decompress error) */
+#define JFS_ERR_COMPRESS_FAIL (JFS_ERR_BASE - 4) /* LZ4_compress_default returned 0 */
+#define JFS_ERR_UNSUPPORTED (JFS_ERR_BASE - 5)   /* operation not available (e.g. Zstd encode on GPU) */
+#define JFS_ERR_NO_DEVICE (JFS_ERR_BASE - 6)     /* no usable gfx950 device; the library never falls back to CPU */
+#define JFS_ERR_INVALID (JFS_ERR_BASE - 7)       /* bad argument (unknown algo, negative size, ...) */
+#define JFS_ERR_HIP (JFS_ERR_BASE - 8)           /* HIP runtime failure */
 
 /* ---- Compressor surface (one synchronous call per block) ---------------- */
 
@@ -84,8 +86,8 @@ typedef struct jfs_iov {
     int64_t dst_cap;
 } jfs_iov;
 
-int jfs_compress_batch(int algo, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t device_mask);
-int jfs_decompress_batch(int algo, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t device_mask);
+int64_t jfs_compress_batch(int algo, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t device_mask);
+int64_t jfs_decompress_batch(int algo, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t device_mask);
 
 /* ---- Device-resident surface (inputs/outputs already in HBM) ------------
  * One descriptor per block; all pointers are device pointers on the current
@@ -99,9 +101,9 @@ typedef struct jfs_dev_block {
     int32_t dst_cap;
 } jfs_dev_block;
 
-int jfs_lz4_decompress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream);
-int jfs_lz4_compress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream);
-int jfs_zstd_decompress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream);
+int64_t jfs_lz4_decompress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream);
+int64_t jfs_lz4_compress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream);
+int64_t jfs_zstd_decompress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream);
 
 /* ---- Runtime / utilities ------------------------------------------------- */
 
@@ -113,8 +115,8 @@ const char *jfs_version(void);
 /* Synthetic benchmark input: block i of class cls
  * ('T','Z','R') with seed base+i, each `block_bytes` long, written
  * back-to-back at d_dst (device pointer) on `stream`.  Host twin below. */
-int jfs_gen_blocks_device(uint8_t *d_dst, int nblk, int64_t block_bytes, char cls, uint64_t seed_base,
-                          void *stream);
+int64_t jfs_gen_blocks_device(uint8_t *d_dst, int nblk, int64_t block_bytes, char cls, uint64_t seed_base,
+                              void *stream);
 void jfs_gen_block_host(uint8_t *dst, int64_t n, char cls, uint64_t seed);
 
 #ifdef __cplusplus

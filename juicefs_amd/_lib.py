@@ -10,18 +10,19 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libjfsgpu.so")
+LIB_PATH = os.environ.get("JFS_GPU_LIB") or os.path.join(_HERE, "lib", "libjfsgpu.so")
 
 ALGO_NONE, ALGO_LZ4, ALGO_ZSTD = 0, 1, 2
 JFS_OK = 0
-JFS_ERR_SHORT_BUFFER = -1000001
-JFS_ERR_EMPTY_INPUT = -1000002
-JFS_ERR_CORRUPT = -1000003
-JFS_ERR_COMPRESS_FAIL = -1000004
-JFS_ERR_UNSUPPORTED = -1000005
-JFS_ERR_NO_DEVICE = -1000006
-JFS_ERR_INVALID = -1000007
-JFS_ERR_HIP = -1000008
+JFS_ERR_BASE = -(1 << 40)  # library codes are <= this; LZ4 decode errors are int32
+JFS_ERR_SHORT_BUFFER = JFS_ERR_BASE - 1
+JFS_ERR_EMPTY_INPUT = JFS_ERR_BASE - 2
+JFS_ERR_CORRUPT = JFS_ERR_BASE - 3
+JFS_ERR_COMPRESS_FAIL = JFS_ERR_BASE - 4
+JFS_ERR_UNSUPPORTED = JFS_ERR_BASE - 5
+JFS_ERR_NO_DEVICE = JFS_ERR_BASE - 6
+JFS_ERR_INVALID = JFS_ERR_BASE - 7
+JFS_ERR_HIP = JFS_ERR_BASE - 8
 
 # every symbol include/jfs_gpucodec.h declares
 EXPORTS = [
@@ -65,17 +66,19 @@ def load() -> ctypes.CDLL:
         f.restype = i64
     for f in (lib.jfs_compress_batch, lib.jfs_decompress_batch):
         f.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(JfsIov), ctypes.POINTER(i64), u32]
-        f.restype = ctypes.c_int
+        f.restype = i64
     for f in (lib.jfs_lz4_decompress_device, lib.jfs_lz4_compress_device, lib.jfs_zstd_decompress_device):
         f.argtypes = [vp, ctypes.c_int, vp, vp]
-        f.restype = ctypes.c_int
+        f.restype = i64
     lib.jfs_device_count.argtypes = []
     lib.jfs_device_count.restype = ctypes.c_int
     lib.jfs_version.argtypes = []
     lib.jfs_version.restype = ctypes.c_char_p
     lib.jfs_gen_blocks_device.argtypes = [vp, ctypes.c_int, i64, ctypes.c_char, ctypes.c_uint64, vp]
-    lib.jfs_gen_blocks_device.restype = ctypes.c_int
+    lib.jfs_gen_blocks_device.restype = i64
     lib.jfs_gen_block_host.argtypes = [vp, i64, ctypes.c_char, ctypes.c_uint64]
     lib.jfs_gen_block_host.restype = None
+    lib.jfs_selftest_wave.argtypes = [vp, vp]
+    lib.jfs_selftest_wave.restype = ctypes.c_int
     _lib = lib
     return lib

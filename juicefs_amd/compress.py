@@ -68,7 +68,7 @@ def _err(code: int, dst_len: int, src_len: int, op: str) -> CompressError:
         return CompressError(f"{op}: not supported by the GPU engine", code)
     if code == L.JFS_ERR_NO_DEVICE:
         return CompressError("no usable gfx950 device", code)
-    if code <= -1000000:
+    if code <= L.JFS_ERR_BASE:
         return CompressError(f"{op}: error {code}", code)
     return CompressError(f"lz4: decompress failed ({code})", code)
 
@@ -99,7 +99,7 @@ class Compressor:
         if r < 0:
             # LZ4 passes LZ4_decompress_safe's negative value through (compress.go:124);
             # the other adapters return 0 with the error (compress.go:57-100).
-            n = r if (self.algo == L.ALGO_LZ4 and r > -1000000) else 0
+            n = r if (self.algo == L.ALGO_LZ4 and r > L.JFS_ERR_BASE) else 0
             return n, _err(r, dn, sn, "decompress")
         return r, None
 
@@ -162,7 +162,7 @@ def _batch(algo: int, pairs, device_mask: int, compress: bool):
     for i in range(nb):
         r = int(out[i])
         if r < 0:
-            n = r if (algo == L.ALGO_LZ4 and not compress and r > -1000000) else 0
+            n = r if (algo == L.ALGO_LZ4 and not compress and r > L.JFS_ERR_BASE) else 0
             res.append((n, _err(r, iov[i].dst_cap, iov[i].src_len, "compress" if compress else "decompress")))
         else:
             res.append((r, None))

@@ -115,7 +115,7 @@ int64_t finish_result(int algo, int dir, int32_t raw) {
 
 // Run blocks [0,nblk) of iov on one device, synchronously.  Blocks that the
 // C-ABI answers without a kernel (empty input, noOp) are handled by the caller.
-int run_batch(DevCtx *dev, int algo, int dir, int nblk, const jfs_iov *iov, int64_t *out) {
+int64_t run_batch(DevCtx *dev, int algo, int dir, int nblk, const jfs_iov *iov, int64_t *out) {
     if (nblk <= 0) return JFS_OK;
     std::lock_guard<std::mutex> lk(dev->mu);
     (void)hipSetDevice(dev->id);
@@ -243,7 +243,7 @@ class Coalescer {
             iov.resize(batch.size());
             out.assign(batch.size(), 0);
             for (size_t i = 0; i < batch.size(); i++) iov[i] = batch[i]->iov;
-            int rc = run_batch(dev, batch[0]->algo, batch[0]->dir, (int)batch.size(), iov.data(), out.data());
+            int64_t rc = run_batch(dev, batch[0]->algo, batch[0]->dir, (int)batch.size(), iov.data(), out.data());
             {
                 std::lock_guard<std::mutex> lk(mu_);
                 for (size_t i = 0; i < batch.size(); i++) {
@@ -271,7 +271,7 @@ bool pre_answer(int algo, int dir, const jfs_iov &v, int64_t *res) {
     return false;
 }
 
-int batch_common(int algo, int dir, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t mask) {
+int64_t batch_common(int algo, int dir, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t mask) {
     if (nblk < 0 || (nblk > 0 && (!iov || !out_n))) return JFS_ERR_INVALID;
     if (algo != JFS_ALGO_NONE && algo != JFS_ALGO_LZ4 && algo != JFS_ALGO_ZSTD) return JFS_ERR_INVALID;
     std::vector<int> todo;
@@ -292,7 +292,7 @@ int batch_common(int algo, int dir, int nblk, const jfs_iov *iov, int64_t *out_n
         part[k % G].push_back(iov[todo[k]]);
         idx[k % G].push_back(todo[k]);
     }
-    std::vector<int> rc(G, JFS_OK);
+    std::vector<int64_t> rc(G, JFS_OK);
     std::vector<std::vector<int64_t>> res(G);
     auto work = [&](size_t g) {
         res[g].assign(part[g].size(), 0);
@@ -378,25 +378,25 @@ int64_t jfs_decompress(int algo, uint8_t *dst, int64_t dst_cap, const uint8_t *s
     return Coalescer::get().submit(algo, DECOMPRESS, v);
 }
 
-int jfs_compress_batch(int algo, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t device_mask) {
+int64_t jfs_compress_batch(int algo, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t device_mask) {
     return batch_common(algo, COMPRESS, nblk, iov, out_n, device_mask);
 }
 
-int jfs_decompress_batch(int algo, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t device_mask) {
+int64_t jfs_decompress_batch(int algo, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t device_mask) {
     return batch_common(algo, DECOMPRESS, nblk, iov, out_n, device_mask);
 }
 
-int jfs_lz4_decompress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream) {
+int64_t jfs_lz4_decompress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream) {
     if (devices().empty()) return JFS_ERR_NO_DEVICE;
     return jfs_launch_lz4_decode(d_blocks, nblk, d_ret, (hipStream_t)stream) == 0 ? JFS_OK : JFS_ERR_HIP;
 }
 
-int jfs_lz4_compress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream) {
+int64_t jfs_lz4_compress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream) {
     if (devices().empty()) return JFS_ERR_NO_DEVICE;
     return jfs_launch_lz4_encode(d_blocks, nblk, d_ret, (hipStream_t)stream) == 0 ? JFS_OK : JFS_ERR_HIP;
 }
 
-int jfs_zstd_decompress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream) {
+int64_t jfs_zstd_decompress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream) {
     if (devices().empty()) return JFS_ERR_NO_DEVICE;
     return jfs_launch_zstd_decode(d_blocks, nblk, d_ret, nullptr, (hipStream_t)stream) == 0 ? JFS_OK : JFS_ERR_HIP;
 }
@@ -405,7 +405,7 @@ int jfs_device_count(void) { return (int)devices().size(); }
 
 const char *jfs_version(void) { return JFS_VERSION; }
 
-int jfs_gen_blocks_device(uint8_t *d_dst, int nblk, int64_t block_bytes, char cls, uint64_t seed_base,
+int64_t jfs_gen_blocks_device(uint8_t *d_dst, int nblk, int64_t block_bytes, char cls, uint64_t seed_base,
                           void *stream) {
     std::vector<DevCtx *> &ds = devices();
     if (ds.empty()) return JFS_ERR_NO_DEVICE;

@@ -5,6 +5,23 @@
 
 #include "../../include/jfs_gpucodec.h"
 
+// Explicit global (address space 1) pointer types: generic pointers compile to
+// flat_* instructions, which count on both vmcnt and lgkmcnt and force the
+// compiler to drain LDS traffic around every HBM access.
+// (The host compilation pass of the same source sees plain types.)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define JFS_GLOBAL __attribute__((address_space(1)))
+#else
+#define JFS_GLOBAL
+#endif
+typedef JFS_GLOBAL uint8_t g_u8;
+typedef JFS_GLOBAL const uint8_t gc_u8;
+typedef JFS_GLOBAL uint32_t g_u32;
+typedef JFS_GLOBAL const uint32_t gc_u32;
+typedef JFS_GLOBAL uint4 g_u4;
+typedef JFS_GLOBAL const uint4 gc_u4;
+typedef JFS_GLOBAL const jfs_dev_block gc_blk;
+
 extern "C" {
 int jfs_launch_lz4_decode(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, hipStream_t stream);
 int jfs_launch_lz4_encode(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, hipStream_t stream);

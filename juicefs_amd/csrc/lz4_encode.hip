@@ -32,17 +32,17 @@ struct Smem {
 };
 
 struct Enc {
-    const uint8_t *src;
-    uint8_t *dst;
+    const gc_u8 *src;
+    g_u8 *dst;
     int64_t n, cap;
     int64_t op;  // output bytes produced
     int64_t F;   // flushed up to
     uint32_t dmis;
 };
 
-__device__ __forceinline__ uint32_t ld32u(const uint8_t *p) {
+__device__ __forceinline__ uint32_t ld32u(const gc_u8 *p) {
     uintptr_t a = (uintptr_t)p;
-    const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
+    const gc_u32 *w = (const gc_u32 *)(a & ~(uintptr_t)3);
     uint32_t sh = (uint32_t)(a & 3);
     uint32_t w0 = w[0];
     if (sh == 0) return w0;
@@ -50,9 +50,9 @@ __device__ __forceinline__ uint32_t ld32u(const uint8_t *p) {
     return __builtin_amdgcn_alignbyte(w1, w0, sh);
 }
 
-__device__ __forceinline__ uint64_t ld64u(const uint8_t *p) {
+__device__ __forceinline__ uint64_t ld64u(const gc_u8 *p) {
     uintptr_t a = (uintptr_t)p;
-    const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
+    const gc_u32 *w = (const gc_u32 *)(a & ~(uintptr_t)3);
     uint32_t sh = (uint32_t)(a & 3);
     uint32_t w0 = w[0], w1 = w[1];
     if (sh == 0) return (uint64_t)w0 | ((uint64_t)w1 << 32);
@@ -62,7 +62,7 @@ __device__ __forceinline__ uint64_t ld64u(const uint8_t *p) {
     return (uint64_t)lo | ((uint64_t)hi << 32);
 }
 
-__device__ __forceinline__ uint32_t hpos(const uint8_t *p, bool u16) {
+__device__ __forceinline__ uint32_t hpos(const gc_u8 *p, bool u16) {
     if (u16) return (ld32u(p) * 2654435761u) >> 19;
     return (uint32_t)(((ld64u(p) << 24) * 889523592379ull) >> 52);
 }
@@ -78,7 +78,7 @@ __device__ __forceinline__ void tput(Smem &s, uint32_t h, uint32_t v, bool u16) 
 // staging slot of output position x (mirrors HBM 16-byte alignment)
 __device__ __forceinline__ uint32_t obidx(const Enc &e, int64_t x) { return (uint32_t)((x + e.dmis) & OBMASK); }
 
-__device__ void oflush2(Smem &s, Enc &e, int64_t to) {
+__device__ __forceinline__ void oflush2(Smem &s, Enc &e, int64_t to) {
     const int l = lane_id();
     if (to > e.cap) to = e.cap;
     int64_t F = e.F;
@@ -87,7 +87,7 @@ __device__ void oflush2(Smem &s, Enc &e, int64_t to) {
     if (a > to) a = to;
     if (l < a - F) e.dst[F + l] = s.ob[obidx(e, F + l)];
     int64_t b = a + ((to - a) & ~(int64_t)15);
-    for (int64_t x = a + 16 * l; x < b; x += 1024) *(uint4 *)(e.dst + x) = *(const uint4 *)(s.ob + obidx(e, x));
+    for (int64_t x = a + 16 * l; x < b; x += 1024) *(g_u4 *)(e.dst + x) = *(const uint4 *)(s.ob + obidx(e, x));
     if (l < to - b) e.dst[b + l] = s.ob[obidx(e, b + l)];
     e.F = to;
 }
@@ -112,7 +112,7 @@ __device__ __forceinline__ void put_len(Smem &s, Enc &e, uint32_t len) {
     const int l = lane_id();
     uint32_t runs = len / 255;
     for (uint32_t k = 0; k < runs; k += 64) {
-        if (k + l < runs) s.ob[obidx(e, e.op + k + l)] = 255;
+        if (k + l < runs) s.ob[obidx(e, e.op + l)] = 255;
         e.op += (runs - k < 64 ? runs - k : 64);
         maybe_flush(s, e, INT64_MAX);
     }
@@ -120,7 +120,7 @@ __device__ __forceinline__ void put_len(Smem &s, Enc &e, uint32_t len) {
 }
 
 // copy literals src[from, from+len) into the output
-__device__ void put_lits(Smem &s, Enc &e, int64_t from, int64_t len, int64_t keep_from) {
+__device__ __forceinline__ void put_lits(Smem &s, Enc &e, int64_t from, int64_t len, int64_t keep_from) {
     const int l = lane_id();
     for (int64_t k = 0; k < len; k += 64) {
         maybe_flush(s, e, keep_from);
@@ -149,16 +149,16 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(const jfs_dev_block *__r
     const int b = blockIdx.x;
     if (b >= nblk) return;
     const int l = lane_id();
-    const jfs_dev_block d = blocks[b];
+    const jfs_dev_block d = ((const gc_blk *)blocks)[b];
     Enc e;
-    e.src = d.src;
-    e.dst = d.dst;
+    e.src = (const gc_u8 *)d.src;
+    e.dst = (g_u8 *)d.dst;
     e.n = d.src_len;
     e.cap = d.dst_cap;
     e.op = 0;
     e.F = 0;
     e.dmis = (uint32_t)((uintptr_t)d.dst & 15u);
-    const uint8_t *src = d.src;
+    const gc_u8 *src = e.src;
     const int64_t n = e.n;
     int32_t result;
     if (n < 0 || n > kMaxInput) {

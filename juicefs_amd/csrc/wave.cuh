@@ -55,3 +55,55 @@ __device__ __forceinline__ uint32_t lane_read(uint32_t v, int lane) {
 __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 }  // namespace jfs
+
+namespace jfs {
+// ---- DPP (no LDS round trip) wave64 scans / reductions ---------------------
+// row_shr:n = 0x110+n, row_bcast:15 = 0x142, row_bcast:31 = 0x143, wave_shr:1 = 0x138
+__device__ __forceinline__ uint32_t dpp_scan_add(uint32_t v) {  // inclusive
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xF, 0xF, true);
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xF, 0xF, true);
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xF, 0xF, true);
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xF, 0xF, true);
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xA, 0xF, false);
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xC, 0xF, false);
+    return v;
+}
+__device__ __forceinline__ uint32_t umax32(uint32_t a, uint32_t b) { return a > b ? a : b; }
+__device__ __forceinline__ uint32_t umin32(uint32_t a, uint32_t b) { return a < b ? a : b; }
+__device__ __forceinline__ uint32_t dpp_scan_max(uint32_t v) {  // inclusive, identity 0
+    v = umax32(v, __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xF, 0xF, true));
+    v = umax32(v, __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xF, 0xF, true));
+    v = umax32(v, __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xF, 0xF, true));
+    v = umax32(v, __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xF, 0xF, true));
+    v = umax32(v, __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xA, 0xF, false));
+    v = umax32(v, __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xC, 0xF, false));
+    return v;
+}
+__device__ __forceinline__ uint32_t dpp_scan_min(uint32_t v) {  // inclusive, identity ~0
+    v = umin32(v, __builtin_amdgcn_update_dpp(~0u, v, 0x111, 0xF, 0xF, false));
+    v = umin32(v, __builtin_amdgcn_update_dpp(~0u, v, 0x112, 0xF, 0xF, false));
+    v = umin32(v, __builtin_amdgcn_update_dpp(~0u, v, 0x114, 0xF, 0xF, false));
+    v = umin32(v, __builtin_amdgcn_update_dpp(~0u, v, 0x118, 0xF, 0xF, false));
+    v = umin32(v, __builtin_amdgcn_update_dpp(~0u, v, 0x142, 0xA, 0xF, false));
+    v = umin32(v, __builtin_amdgcn_update_dpp(~0u, v, 0x143, 0xC, 0xF, false));
+    return v;
+}
+// value of lane l-1 (lane 0 gets `first`): row_shr:1 within each 16-lane row,
+// then patch the three row heads with v_readlane/v_writelane
+__device__ __forceinline__ uint32_t dpp_shift_up(uint32_t v, uint32_t first) {
+    uint32_t t = __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xF, 0xF, true);
+    const int l = (int)__lane_id();
+    uint32_t r15 = (uint32_t)__builtin_amdgcn_readlane((int)v, 15);
+    uint32_t r31 = (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
+    uint32_t r47 = (uint32_t)__builtin_amdgcn_readlane((int)v, 47);
+    t = l == 16 ? r15 : t;
+    t = l == 32 ? r31 : t;
+    t = l == 48 ? r47 : t;
+    t = l == 0 ? first : t;
+    return t;
+}
+__device__ __forceinline__ uint32_t readlane(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
+__device__ __forceinline__ uint32_t dwave_min(uint32_t v) { return readlane(dpp_scan_min(v), 63); }
+__device__ __forceinline__ uint32_t dwave_max(uint32_t v) { return readlane(dpp_scan_max(v), 63); }
+__device__ __forceinline__ uint32_t dwave_sum(uint32_t v) { return readlane(dpp_scan_add(v), 63); }
+}  // namespace jfs
