@@ -200,22 +200,33 @@ __device__ __forceinline__ Tok parse_tok(const Smem &s, const Ctx &c, int32_t p)
     return t;
 }
 
+// rest of a 255-run of match-length extension bytes (rare): next position or STOP|p
+__device__ __forceinline__ uint32_t ext_tail(const Smem &s, const Ctx &c, int32_t p, int32_t q) {
+    const int32_t n = c.n;
+    int k = 1;
+    uint32_t sv;
+    do {
+        sv = cb(s, c, q);
+        q++;
+        if (q >= n - 4 || ++k > KEXT) return STOP | (uint32_t)p;
+    } while (sv == 255);
+    return (uint32_t)q;
+}
+
 // next-token position only (the DP's inner step); STOP|p when not a fast-path
-// token.  tb = the byte at p (from registers).
+// token.  tb = the byte at p (from registers).  The first match-length
+// extension byte is read unconditionally (no divergent loop in the common case).
 __device__ __forceinline__ uint32_t next_pos(const Smem &s, const Ctx &c, int32_t p, uint32_t tb) {
     const int32_t n = c.n;
     if (p > n - 18) return STOP | (uint32_t)p;
     uint32_t ll = tb >> 4;
     if (ll == 15) return (uint32_t)parse_tok(s, c, p).nxt;
-    int32_t q = p + 3 + (int32_t)ll;
+    int32_t q = p + 3 + (int32_t)ll;  // first byte after the offset (<= p + 17: staged)
+    uint32_t e1 = s.cwin[q - c.cbase];
     if ((tb & 15) == 15) {
-        int k = 0;
-        uint32_t sv;
-        do {
-            sv = cb(s, c, q);
-            q++;
-            if (q >= n - 4 || ++k > KEXT) return STOP | (uint32_t)p;
-        } while (sv == 255);
+        q++;
+        if (q >= n - 4) return STOP | (uint32_t)p;
+        if (e1 == 255) return ext_tail(s, c, p, q);
     }
     return (uint32_t)q;
 }
@@ -501,53 +512,37 @@ __device__ __forceinline__ uint32_t chunk_assign(Smem &s, Ctx &c, Chunk &ch, int
     uint32_t kind = 0, own = 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        int32_t pos = q + k;
-        bool use1 = (t1 != NONE) && pos >= o1;
-        int32_t o = use1 ? o1 : o0;
-        int32_t lit = use1 ? lit1 : lit0;
-        uint32_t lw = use1 ? lo1 : lo0;
-        int32_t ll = (int32_t)(lw & 0xFFFFu);
-        int32_t off = (int32_t)(lw >> 16);
-        int32_t ms = o + ll;
-        uint32_t kd, ad = 0, ow = 0, gv = 0;
-        if (pos < lo || pos >= hi) {
-            kd = K_LDS;  // outside this window's output: rewrite the ring byte unchanged
-            ad = slot(c, pos);
-        } else if (pos < ms) {
-            int32_t sp = lit + (pos - o);
-            int32_t r = sp - c.cbase;
-            if ((uint32_t)r < (uint32_t)CWIN) {
-                kd = K_LDS;
-                ad = R + (uint32_t)r;  // cwin follows ring in Smem
-            } else {
-                kd = K_GLB;
-                gv = c.src[sp];
-            }
-        } else if (off == 0) {
-            kd = K_ZERO;
-        } else {
-            uint32_t kk = (uint32_t)(pos - ms);
-            if (kk >= (uint32_t)off) kk = umod(kk, (uint32_t)off);
-            int32_t x = ms - off + (int32_t)kk;
-            if (x < rdy) {  // produced by an earlier chunk or window: final
-                if (x >= ringfloor) {
-                    kd = K_LDS;
-                    ad = slot(c, x);
-                } else {
-                    kd = K_GLB;
-                    gv = c.dst[x];
-                }
-            } else if (x >= q) {
-                kd = K_OWN;
-                ow = (uint32_t)(x - q);
-            } else {
-                kd = K_PEND;
-                ad = slot(c, x);
-                ow = (uint32_t)((x - c0) >> 2);
-            }
-        }
+        const int32_t pos = q + k;
+        const bool use1 = (t1 != NONE) && pos >= o1;
+        const int32_t o = use1 ? o1 : o0;
+        const int32_t lit = use1 ? lit1 : lit0;
+        const uint32_t lw = use1 ? lo1 : lo0;
+        const int32_t ll = (int32_t)(lw & 0xFFFFu);
+        const int32_t off = (int32_t)(lw >> 16);
+        const int32_t ms = o + ll;
+        const bool inwin = pos >= lo && pos < hi;
+        const bool islit = pos < ms;
+        const int32_t sp = lit + (pos - o);
+        const uint32_t rl = (uint32_t)(sp - c.cbase);
+        uint32_t kk = (uint32_t)(pos - ms);
+        if (inwin && !islit && off != 0 && kk >= (uint32_t)off) kk = umod(kk, (uint32_t)off);
+        const int32_t x = ms - off + (int32_t)kk;
+        // classify (selects, not branches)
+        const bool lit_lds = rl < (uint32_t)CWIN;
+        const bool m_ready = x < rdy;
+        const bool m_ring = x >= ringfloor;
+        const bool m_own = x >= q;
+        uint32_t kd = !inwin ? K_LDS
+                    : islit ? (lit_lds ? K_LDS : K_GLB)
+                    : off == 0 ? K_ZERO
+                    : m_ready ? (m_ring ? K_LDS : K_GLB)
+                    : m_own ? K_OWN : K_PEND;
+        uint32_t ad = !inwin ? slot(c, pos) : islit ? (uint32_t)R + rl : slot(c, x);
+        uint32_t ow = m_own ? (uint32_t)(x - q) : (uint32_t)((x - c0) >> 2);
+        uint32_t gv = 0;
+        if (kd == K_GLB) gv = islit ? (uint32_t)c.src[sp] : (uint32_t)c.dst[x];
         kind |= kd << (4 * k);
-        own |= ow << (8 * k);
+        own |= (ow & 0xFFu) << (8 * k);
         ch.addr[k] = ad;
         ch.g[k] = gv;
     }
@@ -637,16 +632,36 @@ __device__ __forceinline__ void window(Smem &s, Ctx &c, Ser &st, int *stopped PR
         pw[0] = a.x; pw[1] = a.y; pw[2] = a.z; pw[3] = a.w;
         pw[4] = b.x; pw[5] = b.y; pw[6] = b.z; pw[7] = b.w;
     }
+    // positions in groups of three: a token is >= 3 bytes, so every next
+    // position of the group lies above it and the three exit lookups are
+    // independent (one LDS round trip per group instead of per position)
 #pragma unroll
-    for (int i = P - 1; i >= 0; --i) {
-        int32_t p = plo + i;
-        uint32_t tb = (pw[i >> 2] >> ((i & 3) * 8)) & 0xFFu;
-        uint32_t nx = next_pos(s, c, p, tb);
-        uint32_t e;
-        if (nx & STOP) e = nx;
-        else if ((int32_t)nx >= phi) e = nx;
-        else e = s.u.ex[((uint32_t)((int32_t)nx - plo)) * 64 + (uint32_t)l];
-        s.u.ex[(uint32_t)i * 64 + (uint32_t)l] = e;
+    for (int g = P - 1; g >= 0; g -= 3) {
+        uint32_t nx[3];
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+            const int i = g - u;
+            if (i < 0) continue;
+            uint32_t tb = (pw[i >> 2] >> ((i & 3) * 8)) & 0xFFu;
+            nx[u] = next_pos(s, c, plo + i, tb);
+        }
+        uint32_t e[3];
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+            const int i = g - u;
+            if (i < 0) continue;
+            uint32_t x = nx[u];
+            bool direct = (x & STOP) || (int32_t)x >= phi;
+            uint32_t idx = direct ? (uint32_t)l : ((uint32_t)((int32_t)x - plo)) * 64 + (uint32_t)l;
+            uint32_t v = s.u.ex[idx];
+            e[u] = direct ? x : v;
+        }
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+            const int i = g - u;
+            if (i < 0) continue;
+            s.u.ex[(uint32_t)i * 64 + (uint32_t)l] = e[u];
+        }
     }
     __builtin_amdgcn_wave_barrier();
     PSTAMP(1);
@@ -683,8 +698,9 @@ __device__ __forceinline__ void window(Smem &s, Ctx &c, Ser &st, int *stopped PR
     }
     PSTAMP(2);
 
-    // 3a. walk the true chain of this piece, recording token positions
-    int32_t tp[TPMAX];
+    // 3a. walk the true chain of this piece, recording every token's fields
+    int32_t tpos[TPMAX], tlit[TPMAX];
+    uint32_t tlm[TPMAX], tof[TPMAX];  // ll | ml << 16 ; off | llx << 16
     uint32_t cnt = 0, olen = 0;
     int32_t stop_ip = -1;
     {
@@ -692,7 +708,10 @@ __device__ __forceinline__ void window(Smem &s, Ctx &c, Ser &st, int *stopped PR
         bool act = !(ent & STOP) && qq < phi;
 #pragma unroll
         for (int j = 0; j < TPMAX; ++j) {
-            tp[j] = qq;
+            tpos[j] = qq;
+            tlit[j] = 0;
+            tlm[j] = 0;
+            tof[j] = 0;
             if (act) {
                 Tok t = parse_tok(s, c, qq);
                 if ((uint32_t)t.nxt & STOP) {
@@ -701,6 +720,9 @@ __device__ __forceinline__ void window(Smem &s, Ctx &c, Ser &st, int *stopped PR
                 } else {
                     cnt++;
                     olen += (uint32_t)(t.ll + t.ml);
+                    tlit[j] = t.lit;
+                    tlm[j] = (uint32_t)t.ll | ((uint32_t)t.ml << 16);
+                    tof[j] = (uint32_t)t.off | ((uint32_t)t.llx << 16);
                     qq = t.nxt;
                     if (qq >= phi) act = false;
                 }
@@ -723,23 +745,26 @@ __device__ __forceinline__ void window(Smem &s, Ctx &c, Ser &st, int *stopped PR
     {
         int32_t o = op0 + (int32_t)obase;
         bool act = true;
+        const int32_t cap = c.cap;
 #pragma unroll
         for (int j = 0; j < TPMAX; ++j) {
             if (act && (uint32_t)j < cnt) {
-                Tok t = parse_tok(s, c, tp[j]);
-                int32_t om = o + t.ll;
-                bool bad = (t.llx && o + t.ll > c.cap - 32) || (om + t.ml >= c.cap - 64) || (t.off > om);
+                int32_t ll = (int32_t)(tlm[j] & 0xFFFFu), ml = (int32_t)(tlm[j] >> 16);
+                int32_t off = (int32_t)(tof[j] & 0xFFFFu);
+                bool llx = (tof[j] >> 16) != 0;
+                int32_t om = o + ll;
+                bool bad = (llx && om > cap - 32) || (om + ml >= cap - 64) || (off > om);
                 uint32_t idx = tbase + (uint32_t)j;
                 if (bad) {
                     bad_idx = idx;
-                    bad_ip = tp[j];
+                    bad_ip = tpos[j];
                     bad_op = o;
                     act = false;
                 } else {
                     s.u.tk.o[idx] = (uint32_t)o;
-                    s.u.tk.lit[idx] = (uint32_t)t.lit;
-                    s.u.tk.lo[idx] = (uint32_t)t.ll | ((uint32_t)t.off << 16);
-                    o = om + t.ml;
+                    s.u.tk.lit[idx] = (uint32_t)tlit[j];
+                    s.u.tk.lo[idx] = (uint32_t)ll | ((uint32_t)off << 16);
+                    o = om + ml;
                 }
             }
         }
