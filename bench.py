@@ -14,8 +14,11 @@ encoder (byte-identical to LZ4_compress_default) before timing; the decoded
 output is checked against the original on the device after timing.
 
 Extra fields: roofline (HIP-event timed kernel, algorithmic bytes C+U per
-launch vs 8 TB/s), cpu_baseline (the CPU oracle on this host's cores, bounded
-sample), host_path (PCIe-inclusive rate through the C ABI's batch API).
+launch vs 8 TB/s; traffic from profiles/traffic.json), cpu_baseline (the CPU
+oracle on this host's cores, bounded sample), cpu_liblz4 (the C library
+pkg/compress wraps, same sample), and with --host-path the PCIe-inclusive rate
+through the C ABI's batch API (kept out of the default run so that every
+decode launch in a default run is the headline launch).
 """
 from __future__ import annotations
 
@@ -46,7 +49,7 @@ def parse():
     p.add_argument("--block-bytes", type=int, default=4 << 20)
     p.add_argument("--cls", default="T")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--no-host-path", action="store_true")
+    p.add_argument("--host-path", action="store_true", help="also time the PCIe-inclusive batch path (extra launches)")
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="wall budget per CPU baseline leg")
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
     return p.parse_args()
@@ -250,7 +253,7 @@ def main():
             lb = liblz4_baseline(comp_blocks, U, a.cpu_seconds / 2)
             if lb:
                 out["cpu_liblz4"] = lb
-        if not a.no_host_path:
+        if a.host_path:
             try:
                 out["host_path"] = host_path_rate(comp_blocks * 8, U)
             except Exception as e:  # report, never fake
