@@ -18,6 +18,11 @@ class Oracle:
         if self.has_zstd:
             lib.oracle_zstd_decompress.argtypes = [vp, i64, vp, i64]
             lib.oracle_zstd_decompress.restype = i64
+            lib.oracle_zstd_set_strict_reserved.argtypes = [i32]
+            lib.oracle_zstd_frame_content_size.argtypes = [vp, i64]
+            lib.oracle_zstd_frame_content_size.restype = i64
+            lib.oracle_xxh64.argtypes = [vp, ctypes.c_size_t, ctypes.c_uint64]
+            lib.oracle_xxh64.restype = ctypes.c_uint64
 
     def lz4_bound(self, n: int) -> int:
         return self.lib.oracle_lz4_bound(n)
@@ -38,3 +43,9 @@ class Oracle:
         dst = ctypes.create_string_buffer(max(cap, 1))
         n = self.lib.oracle_zstd_decompress(src, len(src), dst, cap)
         return n, dst.raw[: max(n, 0)]
+
+    def zstd_strict_reserved(self, on: bool):
+        self.lib.oracle_zstd_set_strict_reserved(1 if on else 0)
+
+    def xxh64(self, b: bytes, seed: int = 0) -> int:
+        return self.lib.oracle_xxh64(b, len(b), seed)
