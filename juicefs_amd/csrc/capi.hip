@@ -100,6 +100,26 @@ std::vector<DevCtx *> &devices() {
 enum Dir { COMPRESS = 0, DECOMPRESS = 1 };
 
 // Per-block result conversion from the kernel's raw value to the C-ABI value.
+// DataDog/zstd v1.5.6 decompressSizeHint: the first frame's content size if
+// known and non-zero, else max(50*len(src), 1e6); capped at that bound.
+int64_t zstd_size_hint(const uint8_t *src, int64_t n) {
+    int64_t upper = std::max<int64_t>(50 * n, 1000000);
+    int64_t hint = upper;
+    if (n >= 5 && src[0] == 0x28 && src[1] == 0xB5 && src[2] == 0x2F && src[3] == 0xFD) {
+        int fhd = src[4];
+        int fcs_flag = fhd >> 6, single = (fhd >> 5) & 1, did = fhd & 3;
+        int64_t p = 5 + (single ? 0 : 1) + (did == 0 ? 0 : did == 1 ? 1 : did == 2 ? 2 : 4);
+        int fs = fcs_flag == 0 ? (single ? 1 : 0) : fcs_flag == 1 ? 2 : fcs_flag == 2 ? 4 : 8;
+        if (fs && p + fs <= n && !(fhd & 8)) {
+            uint64_t v = 0;
+            for (int i = 0; i < fs; i++) v |= (uint64_t)src[p + i] << (8 * i);
+            if (fs == 2) v += 256;
+            if (v > 0 && v < (uint64_t)INT64_MAX) hint = (int64_t)v;
+        }
+    }
+    return std::min(hint, upper);
+}
+
 int64_t finish_result(int algo, int dir, int32_t raw) {
     if (algo == JFS_ALGO_LZ4) {
         if (dir == COMPRESS) return raw > 0 ? raw : JFS_ERR_COMPRESS_FAIL;
@@ -132,6 +152,10 @@ int64_t run_batch(DevCtx *dev, int algo, int dir, int nblk, const jfs_iov *iov, 
             // result can be copied out exactly
             cap = std::min<int64_t>(cap, iov[i].src_len + iov[i].src_len / 255 + 16);
         }
+        if (algo == JFS_ALGO_ZSTD && dir == DECOMPRESS) {
+            // cap(dst) < hint: DataDog decodes into a new hint-sized buffer
+            cap = std::max<int64_t>(cap, zstd_size_hint(iov[i].src, iov[i].src_len));
+        }
         tout += align16(std::max<int64_t>(cap, 0));
     }
     int64_t desc_bytes = align16((int64_t)nblk * (int64_t)sizeof(jfs_dev_block));
@@ -153,6 +177,8 @@ int64_t run_batch(DevCtx *dev, int algo, int dir, int nblk, const jfs_iov *iov, 
         int64_t cap = iov[i].dst_cap;
         if (algo == JFS_ALGO_LZ4 && dir == COMPRESS)
             cap = std::min<int64_t>(cap, iov[i].src_len + iov[i].src_len / 255 + 16);
+        if (algo == JFS_ALGO_ZSTD && dir == DECOMPRESS)
+            cap = std::max<int64_t>(cap, zstd_size_hint(iov[i].src, iov[i].src_len));
         h_desc[i].dst_cap = (int32_t)std::min<int64_t>(cap, INT32_MAX);
     }
     hipStream_t st = dev->stream;
@@ -171,6 +197,11 @@ int64_t run_batch(DevCtx *dev, int algo, int dir, int nblk, const jfs_iov *iov, 
     if (hipStreamSynchronize(st) != hipSuccess) return JFS_ERR_HIP;
     for (int i = 0; i < nblk; i++) {
         int64_t r = finish_result(algo, dir, h_ret[i]);
+        if (algo == JFS_ALGO_ZSTD && dir == DECOMPRESS && r > 0 &&
+            iov[i].dst_cap < zstd_size_hint(iov[i].src, iov[i].src_len)) {
+            // decoded into DataDog's own buffer: compress.go:99-101 "buffer too short"
+            r = JFS_ERR_SHORT_BUFFER;
+        }
         if (r > 0) memcpy(iov[i].dst, h_out + out_off[i], (size_t)r);
         out[i] = r;
     }

@@ -1,0 +1,128 @@
+"""GPU parity: the HIP Zstd decoder (through the C ABI) vs the CPU oracle
+(oracle/zstd_oracle.c, pinned to libzstd 1.4.9 fixtures).  Bar: identical
+decoded bytes and identical result codes (size / -1 corrupt / -2 dst too
+small / -3 source size wrong) on every fixture and corpus case."""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from juicefs_amd import compress as C
+from juicefs_amd import device as D
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def sha(b):
+    return hashlib.sha256(b).hexdigest()
+
+
+@pytest.fixture(scope="module")
+def frames_bin(golden):
+    with open(os.path.join(GOLD, golden["zstd"]["bin"]), "rb") as f:
+        return f.read()
+
+
+def run_device(srcs, caps, dev, src_mis=0, dst_mis=0):
+    """Decode each src into its own dst (cap bytes) on the GPU; returns
+    (rets, outputs[:ret])."""
+    n = len(srcs)
+    so, do, off, doff = [], [], 0, 0
+    for i, s in enumerate(srcs):
+        m = (src_mis + 7 * i) % 16 if src_mis else 0
+        so.append(off + m)
+        off += m + len(s) + 64
+        off = (off + 15) & ~15
+        dm = (dst_mis + 5 * i) % 16 if dst_mis else 0
+        do.append(doff + dm)
+        doff += dm + caps[i] + 64
+        doff = (doff + 15) & ~15
+    host = np.zeros(off + 64, dtype=np.uint8)
+    for s, o in zip(srcs, so):
+        host[o:o + len(s)] = np.frombuffer(s, dtype=np.uint8)
+    src_t = torch.from_numpy(host).to(dev)
+    dst_t = torch.full((doff + 64,), 0xAB, dtype=torch.uint8, device=dev)
+    desc = D.make_desc(src_t, so, [len(s) for s in srcs], dst_t, do, caps)
+    ret = torch.zeros(n, dtype=torch.int32, device=dev)
+    D.zstd_decompress(desc, ret)
+    torch.cuda.synchronize()
+    r = ret.cpu().tolist()
+    dh = dst_t.cpu().numpy()
+    outs = [dh[o:o + max(x, 0)].tobytes() for o, x in zip(do, r)]
+    # nothing written at or past cap
+    for o, c in zip(do, caps):
+        assert (dh[o + c:o + c + 16] == 0xAB).all()
+    return r, outs
+
+
+def test_zstd_frames_vs_golden(gpu, golden, frames_bin):
+    ents = golden["zstd"]["frames"] + golden["zstd"]["special"]
+    srcs = [frames_bin[f["off"]:f["off"] + f["csize"]] for f in ents]
+    caps = [f["size"] for f in ents]
+    r, outs = run_device(srcs, caps, gpu)
+    for f, x, o in zip(ents, r, outs):
+        assert x == f["size"] and sha(o) == f["src_sha"], (f.get("name"), f["cls"], f.get("level"), f["size"], x)
+
+
+def test_zstd_frames_unaligned_and_short(gpu, golden, frames_bin, oracle):
+    ents = [f for f in golden["zstd"]["frames"] if f["size"] <= 300000]
+    srcs = [frames_bin[f["off"]:f["off"] + f["csize"]] for f in ents]
+    caps = [f["size"] for f in ents]
+    r, outs = run_device(srcs, caps, gpu, src_mis=3, dst_mis=9)
+    for f, x, o in zip(ents, r, outs):
+        assert x == f["size"] and sha(o) == f["src_sha"]
+    # one byte short -> dstSize_tooSmall, exactly like the oracle
+    caps2 = [max(c - 1, 0) for c in caps]
+    r2, _ = run_device(srcs, caps2, gpu)
+    for s, c, x in zip(srcs, caps2, r2):
+        assert x == oracle.zstd_decompress(s, c)[0]
+
+
+def test_zstd_accept_and_corpus_vs_oracle(gpu, golden, oracle):
+    cases = golden["zstd"]["accept"] + golden["zstd"]["corpus"]
+    srcs = [bytes.fromhex(a["src"]) for a in cases]
+    caps = [a["cap"] for a in cases]
+    r, outs = run_device(srcs, caps, gpu, src_mis=1, dst_mis=2)
+    bad = []
+    for s, c, x, o in zip(srcs, caps, r, outs):
+        want, wo = oracle.zstd_decompress(s, c)
+        if x != want or (x >= 0 and o != wo):
+            bad.append((s.hex(), c, want, x))
+    assert not bad, bad[:5]
+
+
+def test_zstd_baseline_block_batch(gpu, golden, frames_bin, oracle):
+    """configs[3] shape: 4 MiB level-3 frames, many per launch."""
+    f = [e for e in golden["zstd"]["frames"] if e["size"] == 4 << 20][0]
+    c = frames_bin[f["off"]:f["off"] + f["csize"]]
+    n, ref = oracle.zstd_decompress(c, f["size"])
+    assert n == f["size"]
+    nb = 96
+    r, outs = run_device([c] * nb, [f["size"]] * nb, gpu, dst_mis=0)
+    assert r == [f["size"]] * nb
+    assert all(o == ref for o in outs)
+
+
+def test_zstandard_decompress_contract(gpu, golden):
+    """compress.go:94-103 through DataDog v1.5.6 semantics (size hint)."""
+    z = C.ZStandard()
+    kat = {bytes.fromhex(k["src"]): bytes.fromhex(k["comp_l1"]) for k in golden["zstd"]["kat"]}
+    frame = kat[b"Zstd"]
+    out = bytearray(4)
+    n, err = z.Decompress(out, frame)
+    assert err is None and n == 4 and bytes(out) == b"Zstd"
+    n, err = z.Decompress(bytearray(1), frame)          # cap < hint -> "buffer too short"
+    assert err is not None
+    n, err = z.Decompress(bytearray(0), kat[b""])       # empty content -> (0, nil)
+    assert err is None and n == 0
+    n, err = z.Decompress(bytearray(100), b"")          # ErrEmptySlice
+    assert err is not None
+    big = kat[b"hello world" * 8]
+    out = bytearray(200)
+    n, err = z.Decompress(out, big)
+    assert err is None and bytes(out[:n]) == b"hello world" * 8
+    n, err = z.Decompress(bytearray(100), big[:-1])     # truncated frame
+    assert err is not None
