@@ -39,7 +39,9 @@ namespace zstdd {
 __device__ unsigned long long g_zprof[8];
 #define ZP_NOW() __builtin_amdgcn_s_memtime()
 #define ZP_ADD(i, v) do { if (lane_id() == 0) atomicAdd(&g_zprof[i], (unsigned long long)(v)); } while (0)
+#define XP_ADD(i, v) do { x.pacc[i] += (v); } while (0)
 #else
+#define XP_ADD(i, v) do { } while (0)
 #define ZP_NOW() 0ull
 #define ZP_ADD(i, v) do { } while (0)
 #endif
@@ -1269,6 +1271,9 @@ struct XSmem {
 };
 
 struct X {
+#ifdef JFS_PROF
+    uint64_t pacc[8];
+#endif
     int32_t bug;
     g_u8 *dst;
     const gc_u8 *lit;      // literal buffer of this input
@@ -1279,10 +1284,12 @@ struct X {
 
 __device__ __forceinline__ uint32_t slot(const X &x, int32_t pos) { return (uint32_t)(pos + (int32_t)x.dmis) & RMASK; }
 
-__device__ __forceinline__ void xflush(XSmem &s, X &x, int32_t to) {
+__device__ __forceinline__ void xflush(XSmem &s, X &x, int32_t to, bool wait = true) {
     const int l = lane_id();
-    wait_vm();
-    x.Fw = x.F;
+    if (wait) {
+        wait_vm();
+        x.Fw = x.F;
+    }
     int32_t F = x.F;
     if (to <= F) return;
     int32_t a = F + (int32_t)((16u - ((x.dmis + (uint32_t)F) & 15u)) & 15u);
@@ -1293,9 +1300,9 @@ __device__ __forceinline__ void xflush(XSmem &s, X &x, int32_t to) {
     if (l < to - bb) x.dst[bb + l] = s.ring[slot(x, bb + l)];
     x.F = to;
 }
-__device__ __forceinline__ void xflush_line(XSmem &s, X &x, int32_t hi) {
+__device__ __forceinline__ void xflush_line(XSmem &s, X &x, int32_t hi, bool wait = true) {
     int32_t to = (int32_t)(((uint32_t)hi + x.dmis) & ~127u) - (int32_t)x.dmis;
-    if (to > x.F) xflush(s, x, to);
+    if (to > x.F) xflush(s, x, to, wait);
 }
 
 // make lit[lp, lp+need) resident in the staging window
@@ -1379,7 +1386,126 @@ __device__ __forceinline__ uint64_t xxh64_dev(XSmem &s, const gc_u8 *p, int64_t 
 }
 
 // Execute a run of sequence items in parallel.  Lane j < r holds item j
-// (ll, ml, off); all checks were done by the caller.  Output [O0, O1).
+// (ll, ml, off); all checks were done by the caller.  Output [O0, O1) is
+// produced in 256-byte chunks (4 bytes per lane), software-pipelined: chunk
+// i+1 is classified and its far (HBM) source bytes are requested before chunk
+// i is written, so the HBM latency overlaps the LDS work of chunk i.
+struct Cls {
+    int32_t c, cp;                  // chunk start; sources >= cp are produced in this chunk
+    uint32_t live, lit, far, pend;  // 4-bit masks over the lane's bytes
+    int32_t src[4];                 // literal index or output position of the source
+    uint32_t fv[4];                 // far bytes (loads in flight)
+    int32_t litmin;                 // wave-uniform smallest literal index (INT_MAX: none)
+    int32_t fsnap;                  // F when the far loads were issued
+};
+
+__device__ __forceinline__ void x_classify(XSmem &s, const X &x, Cls &k, int32_t c, uint32_t *carry, uint32_t r,
+                                           uint32_t len, int32_t o, int32_t O0, int32_t O1) {
+    const int l = lane_id();
+    k.c = c;
+    k.cp = c > O0 ? c : O0;
+    const int32_t cend = c + CH, ringfloor = cend - R;
+    if ((uint32_t)l < r && len > 0 && o >= c && o < cend) s.mk[o - c] = (uint8_t)(l + 1);
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t w = *(const uint32_t *)(s.mk + 4 * l);
+    *(uint32_t *)(s.mk + 4 * l) = 0u;
+    const uint32_t m0 = w & 0xFF, m1 = (w >> 8) & 0xFF, m2 = (w >> 16) & 0xFF, m3 = w >> 24;
+    const uint32_t scan = dpp_scan_max(umax32(umax32(m0, m1), umax32(m2, m3)));
+    uint32_t own[4];
+    own[0] = umax32(umax32(dpp_shift_up(scan, 0u), *carry), m0);
+    own[1] = umax32(own[0], m1);
+    own[2] = umax32(own[1], m2);
+    own[3] = umax32(own[2], m3);
+    *carry = umax32(*carry, readlane(scan, 63));
+    k.live = k.lit = k.far = k.pend = 0;
+    int32_t litmin = 0x7FFFFFFF;
+    uint32_t needmod = 0;
+    uint32_t dd[4], oz[4];
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+        const int32_t xb = c + 4 * l + b;
+        k.src[b] = 0;
+        dd[b] = 0; oz[b] = 1;
+        if (own[b] == 0 || xb >= O1 || xb < O0) continue;
+        k.live |= 1u << b;
+        const uint4 e = s.run[own[b] - 1];
+        const int32_t rr = xb - (int32_t)e.x;
+        if (rr < (int32_t)e.y) {
+            k.src[b] = (int32_t)e.w + rr;
+            k.lit |= 1u << b;
+            litmin = litmin < k.src[b] ? litmin : k.src[b];
+        } else {
+            const uint32_t d = (uint32_t)(rr - (int32_t)e.y);
+            if (e.z > d) {
+                k.src[b] = xb - (int32_t)e.z;
+            } else {  // overlapping copy: the byte repeats with period `off`
+                k.src[b] = (int32_t)e.x + (int32_t)e.y - (int32_t)e.z;
+                dd[b] = d; oz[b] = e.z;
+                needmod |= 1u << b;
+            }
+        }
+    }
+    if (__ballot(needmod != 0)) {
+#pragma unroll
+        for (int b = 0; b < 4; b++)
+            if (needmod & (1u << b)) k.src[b] += (int32_t)(dd[b] % oz[b]);
+    }
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+        if ((k.live & ~k.lit) & (1u << b)) {
+            if (k.src[b] >= k.cp) k.pend |= 1u << b;
+            else if (k.src[b] < ringfloor) k.far |= 1u << b;
+        }
+    }
+    k.litmin = (int32_t)dwave_min((uint32_t)litmin);
+    k.fsnap = x.F;
+    // far source bytes: always 4 loads (dummy address when not far) so the
+    // compiler can count the outstanding loads across the pipeline
+#pragma unroll
+    for (int b = 0; b < 4; b++) k.fv[b] = x.dst[(k.far & (1u << b)) ? k.src[b] : 0];
+}
+
+__device__ __forceinline__ void x_write(XSmem &s, X &x, const Cls &k) {
+    const int l = lane_id();
+    if (k.litmin != 0x7FFFFFFF) lit_window(s, x, k.litmin, CH);
+    uint32_t val = 0;
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+        uint32_t v;
+        if (k.lit & (1u << b)) v = s.lw[k.src[b] - (int32_t)x.lw0];
+        else if (k.far & (1u << b)) v = k.fv[b];
+        else v = s.ring[slot(x, k.src[b])];
+        val |= (v & 0xFF) << (8 * b);
+    }
+    if (k.fsnap > x.Fw) x.Fw = k.fsnap;  // the far loads were waited for: earlier flush stores are complete
+    const uint32_t ready = k.live & ~k.pend;
+#pragma unroll
+    for (int b = 0; b < 4; b++)
+        if (ready & (1u << b)) s.ring[slot(x, k.c + 4 * l + b)] = (uint8_t)(val >> (8 * b));
+    uint32_t dw = 0;
+#pragma unroll
+    for (int b = 0; b < 4; b++) dw |= ((ready >> b) & 1u) << (8 * b);
+    *(uint32_t *)(s.done + 4 * l) = dw;
+    __builtin_amdgcn_wave_barrier();
+    uint32_t pend = k.pend;
+    int guard = 0;
+    while (__ballot(pend != 0)) {
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            if (pend & (1u << b)) {
+                if (s.done[k.src[b] - k.c]) {
+                    const int32_t xb = k.c + 4 * l + b;
+                    s.ring[slot(x, xb)] = s.ring[slot(x, k.src[b])];
+                    s.done[xb - k.c] = 1;
+                    pend &= ~(1u << b);
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (++guard > CH) { x.bug = 101; break; }
+    }
+}
+
 __device__ __forceinline__ void x_run(XSmem &s, X &x, uint32_t r, uint32_t ll, uint32_t ml, uint32_t off,
                                       int32_t O0, int32_t lit0) {
     const int l = lane_id();
@@ -1392,106 +1518,30 @@ __device__ __forceinline__ void x_run(XSmem &s, X &x, uint32_t r, uint32_t ll, u
     if (O1 == O0) return;
     if ((uint32_t)l < r) s.run[l] = make_uint4((uint32_t)o, ll, off, (uint32_t)lit);
     __builtin_amdgcn_wave_barrier();
-    int32_t c = O0 - (int32_t)((uint32_t)(O0 + (int32_t)x.dmis) & (CH - 1));
-    uint32_t carry = 0;  // 1-based owner of the byte before chunk c
-    for (; c < O1; c += CH) {
-        const int32_t cend = c + CH;
-        const int32_t ringfloor = cend - R;
-        const int32_t cp = c > O0 ? c : O0;  // sources at or above cp are produced in this chunk
-        if (cend - x.F >= FLUSH_T + CH) xflush_line(s, x, c);
-        // item-start markers
-        if ((uint32_t)l < r && len > 0 && o >= c && o < cend) s.mk[o - c] = (uint8_t)(l + 1);
-        __builtin_amdgcn_wave_barrier();
-        uint32_t w = *(const uint32_t *)(s.mk + 4 * l);
-        *(uint32_t *)(s.mk + 4 * l) = 0u;
-        uint32_t m0 = w & 0xFF, m1 = (w >> 8) & 0xFF, m2 = (w >> 16) & 0xFF, m3 = w >> 24;
-        uint32_t lmax = umax32(umax32(m0, m1), umax32(m2, m3));
-        uint32_t scan = dpp_scan_max(lmax);
-        uint32_t prev = umax32(dpp_shift_up(scan, 0u), carry);
-        uint32_t own[4];
-        own[0] = umax32(prev, m0);
-        own[1] = umax32(own[0], m1);
-        own[2] = umax32(own[1], m2);
-        own[3] = umax32(own[2], m3);
-        carry = umax32(carry, readlane(scan, 63));
-        // classify bytes
-        uint32_t val = 0, pend = 0, far = 0, isl = 0;
-        int32_t srcv[4];
-        int32_t litmin = 0x7FFFFFFF;
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-            const int32_t xb = c + 4 * l + b;
-            srcv[b] = 0;
-            if (own[b] == 0 || xb >= O1 || xb < O0) continue;
-            const uint4 e = s.run[own[b] - 1];
-            const int32_t rr = xb - (int32_t)e.x;
-            if (rr < (int32_t)e.y) {
-                srcv[b] = (int32_t)e.w + rr;  // literal index
-                isl |= 1u << b;
-                litmin = litmin < srcv[b] ? litmin : srcv[b];
-            } else {
-                const uint32_t d = (uint32_t)(rr - (int32_t)e.y);
-                const int32_t ms = (int32_t)e.x + (int32_t)e.y;
-                int32_t src = e.z > d ? xb - (int32_t)e.z : ms - (int32_t)e.z + (int32_t)(d % e.z);
-                srcv[b] = src;
-                if (src >= cp) pend |= 1u << b;
-                else if (src < ringfloor) far |= 1u << b;
-            }
+    const int32_t c0 = O0 - (int32_t)((uint32_t)(O0 + (int32_t)x.dmis) & (CH - 1));
+    uint32_t carry = 0;
+    if (c0 + CH - R > x.Fw) { wait_vm(); x.Fw = x.F; }
+    Cls cur, nxt;
+    uint64_t t0 = ZP_NOW();
+    x_classify(s, x, cur, c0, &carry, r, len, o, O0, O1);
+    uint64_t t1 = ZP_NOW();
+    XP_ADD(2, t1 - t0);
+    for (int32_t c = c0; c < O1; c += CH) {
+        const int32_t cn = c + CH;
+        if (cn - x.F >= FLUSH_T + CH) xflush_line(s, x, c, false);
+        const bool more = cn < O1;
+        if (more) {
+            if (cn + CH - R > x.Fw) { wait_vm(); x.Fw = x.F; }
+            x_classify(s, x, nxt, cn, &carry, r, len, o, O0, O1);
         }
-        // literal window covering this chunk's literals
-        int32_t lmin = (int32_t)dwave_min((uint32_t)litmin);
-        if (lmin != 0x7FFFFFFF) lit_window(s, x, lmin, CH);
-        if (__ballot(far != 0)) {
-            if (ringfloor > x.Fw) { wait_vm(); x.Fw = x.F; }
-        }
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-            uint32_t v = 0;
-            if (isl & (1u << b)) v = s.lw[srcv[b] - (int32_t)x.lw0];
-            else if (far & (1u << b)) v = x.dst[srcv[b]];
-            else if (!(pend & (1u << b)) && own[b] != 0) v = s.ring[slot(x, srcv[b])];
-            val |= v << (8 * b);
-        }
-        // write ready bytes, mark them done
-        uint32_t live = 0;
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-            const int32_t xb = c + 4 * l + b;
-            if (own[b] != 0 && xb >= O0 && xb < O1) live |= 1u << b;
-        }
-        uint32_t ready = live & ~pend;
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-            const int32_t xb = c + 4 * l + b;
-            if (ready & (1u << b)) s.ring[slot(x, xb)] = (uint8_t)(val >> (8 * b));
-        }
-        uint32_t dw = 0;
-#pragma unroll
-        for (int b = 0; b < 4; b++) dw |= ((ready >> b) & 1u) << (8 * b);
-        *(uint32_t *)(s.done + 4 * l) = dw;
-        __builtin_amdgcn_wave_barrier();
-        // in-chunk dependencies: resolve in rounds (sources always lie earlier)
-        int guard = 0;
-        while (__ballot(pend != 0)) {
-#pragma unroll
-            for (int b = 0; b < 4; b++) {
-                if (pend & (1u << b)) {
-                    const int32_t rel = srcv[b] - c;
-                    if (s.done[rel]) {
-                        const int32_t xb = c + 4 * l + b;
-                        uint8_t v = s.ring[slot(x, srcv[b])];
-                        s.ring[slot(x, xb)] = v;
-                        s.done[xb - c] = 1;
-                        pend &= ~(1u << b);
-                    }
-                }
-            }
-            __builtin_amdgcn_wave_barrier();
-            if (++guard > CH) {
-                x.bug = 101;
-                break;
-            }
-        }
+        uint64_t t2 = ZP_NOW();
+        x_write(s, x, cur);
+        uint64_t t3 = ZP_NOW();
+        XP_ADD(2, t2 - t1);
+        XP_ADD(3, t3 - t2);
+        XP_ADD(5, 1);
+        t1 = t3;
+        if (more) cur = nxt;
     }
 }
 
@@ -1510,7 +1560,11 @@ __global__ __launch_bounds__(64) void zexec_kernel(const jfs_dev_block *__restri
     x.lw0 = -(1LL << 40);
     x.cap = b.dst_cap;
     x.op = 0; x.F = 0; x.Fw = 0; x.fstart = 0; x.bug = 0;
+#ifdef JFS_PROF
+    for (int i = 0; i < 8; i++) x.pacc[i] = 0;
+#endif
     *(uint32_t *)(s.mk + 4 * l) = 0u;  // markers are cleared after each use; LDS starts undefined
+    const uint64_t tz0 = ZP_NOW();
     __builtin_amdgcn_wave_barrier();
     x.dmis = (uint32_t)((uintptr_t)b.dst & 15u);
     int32_t result = E_BUG;
@@ -1522,8 +1576,11 @@ __global__ __launch_bounds__(64) void zexec_kernel(const jfs_dev_block *__restri
     uint32_t rin0 = 1, rin1 = 4, rin2 = 8;  // repeat offsets at the start of the current block
     bool done = false;
     for (uint32_t base = 0; base < nit && !done; base += 64) {
+        uint64_t tb0 = ZP_NOW();
         uint4 mine = make_uint4(0, 0, 0, 0);
         if (base + l < nit) mine = it[base + l];
+        wait_vm();
+        XP_ADD(0, ZP_NOW() - tb0);
         uint32_t cnt = nit - base < 64 ? nit - base : 64;
         const uint64_t nonseq = __ballot((uint32_t)l >= cnt || (mine.w & 0xFF) != IT_SEQ);
         for (uint32_t k = 0; k < cnt; k++) {
@@ -1549,6 +1606,7 @@ __global__ __launch_bounds__(64) void zexec_kernel(const jfs_dev_block *__restri
                 const int32_t code = (int32_t)readlane(fdst ? (uint32_t)E_DSTSMALL : (uint32_t)E_CORRUPT, (int)(nexec & 63));
                 const uint32_t el = (uint32_t)l < nexec ? len : 0u, ell = (uint32_t)l < nexec ? lln : 0u;
                 const uint32_t tot = readlane(dpp_scan_add(el), 63), totll = readlane(dpp_scan_add(ell), 63);
+                XP_ADD(6, 1);
                 if (nexec) x_run(s, x, nexec, ll, ml, off, x.op, (int32_t)lp);
                 x.op += (int32_t)tot;
                 lp += totll;
@@ -1594,6 +1652,10 @@ __global__ __launch_bounds__(64) void zexec_kernel(const jfs_dev_block *__restri
     }
     if (!done) result = x.op;
     if (x.bug) result = -x.bug;
+    XP_ADD(7, ZP_NOW() - tz0);
+#ifdef JFS_PROF
+    for (int i = 0; i < 8; i++) ZP_ADD(i, x.pacc[i]);
+#endif
     xflush(s, x, x.op);
     wait_vm();
     if (l == 0) ret[bi] = result;

@@ -1,4 +1,4 @@
-"""Sequence-wave phase counters from libjfsgpu_prof.so (s_memtime, 100 MHz)."""
+"""zexec phase counters from libjfsgpu_prof.so (s_memtime ticks)."""
 import ctypes, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -13,8 +13,8 @@ lib.jfs_zprof_reset()
 b.decompress(); torch.cuda.synchronize()
 buf = (ctypes.c_ulonglong * 8)()
 lib.jfs_zprof_read(buf)
-t_tab, t_loop, t_tot, nblk, nseq = buf[0], buf[1], buf[2], buf[3], buf[4]
-print(f"frames {n} blocks {nblk} seqs {nseq} seq/frame {nseq / n:.0f}")
-print(f"memtime ticks per frame: tables {t_tab / n:.0f} loop {t_loop / n:.0f} total {t_tot / n:.0f}")
-print(f"ticks per sequence (loop) {t_loop / max(nseq, 1):.2f}; per block tables {t_tab / max(nblk, 1):.0f}")
+names = ["batch_load", "-", "classify", "write", "-", "chunks", "runs", "total"]
+for i, nm in enumerate(names):
+    print(f"{nm:12s} per frame {buf[i] / n:14.0f}")
+print(f"per chunk: classify {buf[2] / max(buf[5], 1):.0f} write {buf[3] / max(buf[5], 1):.0f}; per run batch_load {buf[0] / max(buf[6], 1):.0f}")
 print("ok" if b.verify() else "MISMATCH")
