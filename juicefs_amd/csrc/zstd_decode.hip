@@ -1254,19 +1254,22 @@ __global__ __launch_bounds__(64) void zseq_kernel(const jfs_dev_block *__restric
 // ---------------------------------------------------------------------------
 // kernel 3: execute items
 // ---------------------------------------------------------------------------
-constexpr int R = 8192;
+constexpr int R = 4096;
 constexpr int RMASK = R - 1;
-constexpr int LW = 4096;          // literal staging window
+constexpr int LW = 2048;          // literal staging window
 constexpr int FLUSH_T = 1024;
 
 constexpr int CH = 256;           // output chunk of the parallel gather (4 bytes per lane)
 
+constexpr int FB = 64;           // far-source prefetch bytes per lane (16 B alignment slack)
+constexpr int FBUSE = FB - 16;
+constexpr int BSPAN = R / 2;     // max output span of one lane-parallel batch
+constexpr int LONGI = 1024;      // items longer than this are copied by the whole wave
+
 struct XSmem {
     alignas(16) uint8_t ring[R];
-    alignas(16) uint8_t lw[LW];
-    alignas(16) uint4 run[64];    // current run: output start, ll, offset, literal start
-    alignas(16) uint8_t mk[CH];   // item-start markers (1-based run index), cleared after use
-    alignas(16) uint8_t done[CH]; // in-chunk bytes already written (pending rounds)
+    alignas(16) uint8_t lw[LW + 16];
+    alignas(16) uint8_t farbuf[64 * FB + 16];
     uint64_t xxh[4];
 };
 
@@ -1385,164 +1388,228 @@ __device__ __forceinline__ uint64_t xxh64_dev(XSmem &s, const gc_u8 *p, int64_t 
     return h;
 }
 
-// Execute a run of sequence items in parallel.  Lane j < r holds item j
-// (ll, ml, off); all checks were done by the caller.  Output [O0, O1) is
-// produced in 256-byte chunks (4 bytes per lane), software-pipelined: chunk
-// i+1 is classified and its far (HBM) source bytes are requested before chunk
-// i is written, so the HBM latency overlaps the LDS work of chunk i.
-struct Cls {
-    int32_t c, cp;                  // chunk start; sources >= cp are produced in this chunk
-    uint32_t live, lit, far, pend;  // 4-bit masks over the lane's bytes
-    int32_t src[4];                 // literal index or output position of the source
-    uint32_t fv[4];                 // far bytes (loads in flight)
-    int32_t litmin;                 // wave-uniform smallest literal index (INT_MAX: none)
-    int32_t fsnap;                  // F when the far loads were issued
-};
-
-__device__ __forceinline__ void x_classify(XSmem &s, const X &x, Cls &k, int32_t c, uint32_t *carry, uint32_t r,
-                                           uint32_t len, int32_t o, int32_t O0, int32_t O1) {
-    const int l = lane_id();
-    k.c = c;
-    k.cp = c > O0 ? c : O0;
-    const int32_t cend = c + CH, ringfloor = cend - R;
-    if ((uint32_t)l < r && len > 0 && o >= c && o < cend) s.mk[o - c] = (uint8_t)(l + 1);
-    __builtin_amdgcn_wave_barrier();
-    const uint32_t w = *(const uint32_t *)(s.mk + 4 * l);
-    *(uint32_t *)(s.mk + 4 * l) = 0u;
-    const uint32_t m0 = w & 0xFF, m1 = (w >> 8) & 0xFF, m2 = (w >> 16) & 0xFF, m3 = w >> 24;
-    const uint32_t scan = dpp_scan_max(umax32(umax32(m0, m1), umax32(m2, m3)));
-    uint32_t own[4];
-    own[0] = umax32(umax32(dpp_shift_up(scan, 0u), *carry), m0);
-    own[1] = umax32(own[0], m1);
-    own[2] = umax32(own[1], m2);
-    own[3] = umax32(own[2], m3);
-    *carry = umax32(*carry, readlane(scan, 63));
-    k.live = k.lit = k.far = k.pend = 0;
-    int32_t litmin = 0x7FFFFFFF;
-    uint32_t needmod = 0;
-    uint32_t dd[4], oz[4];
-#pragma unroll
-    for (int b = 0; b < 4; b++) {
-        const int32_t xb = c + 4 * l + b;
-        k.src[b] = 0;
-        dd[b] = 0; oz[b] = 1;
-        if (own[b] == 0 || xb >= O1 || xb < O0) continue;
-        k.live |= 1u << b;
-        const uint4 e = s.run[own[b] - 1];
-        const int32_t rr = xb - (int32_t)e.x;
-        if (rr < (int32_t)e.y) {
-            k.src[b] = (int32_t)e.w + rr;
-            k.lit |= 1u << b;
-            litmin = litmin < k.src[b] ? litmin : k.src[b];
-        } else {
-            const uint32_t d = (uint32_t)(rr - (int32_t)e.y);
-            if (e.z > d) {
-                k.src[b] = xb - (int32_t)e.z;
-            } else {  // overlapping copy: the byte repeats with period `off`
-                k.src[b] = (int32_t)e.x + (int32_t)e.y - (int32_t)e.z;
-                dd[b] = d; oz[b] = e.z;
-                needmod |= 1u << b;
-            }
+// ---------------------------------------------------------------------------
+// lane-per-item copy engine.  A batch is <= 64 consecutive sequence items,
+// one per lane, producing output [O0, O1) with O1 - O0 <= BSPAN.  Literal
+// runs copy first (their source is the staged literal window); matches then
+// copy in rounds: a match is ready once every output byte below its source
+// end is final, i.e. its source ends at or below the earliest still-pending
+// match start.  Copies move 4 bytes per step (LDS dword pair + alignbyte,
+// byte-granular ring writes).  Sources that the batch's own ring writes could
+// overwrite (below O1 - R) are read from HBM; for those the first FBUSE bytes
+// are prefetched into LDS before the literal copies.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t ld4(const uint8_t *base, uint32_t a) {
+    const uint32_t a0 = a & ~3u;
+    const uint32_t d0 = *(const uint32_t *)(base + a0), d1 = *(const uint32_t *)(base + a0 + 4);
+    return __builtin_amdgcn_alignbyte(d1, d0, a & 3u);
+}
+// 4 bytes at source byte address a (any alignment): linear LDS buffer or ring slot space
+template <bool RING>
+__device__ __forceinline__ uint32_t ld4r(const XSmem &s, const uint8_t *base, uint32_t a) {
+    const uint32_t a0 = a & ~3u;
+    uint32_t d0, d1;
+    if (RING) {
+        d0 = *(const uint32_t *)(s.ring + (a0 & RMASK));
+        d1 = *(const uint32_t *)(s.ring + ((a0 + 4) & RMASK));
+    } else {
+        d0 = *(const uint32_t *)(base + a0);
+        d1 = *(const uint32_t *)(base + a0 + 4);
+    }
+    return __builtin_amdgcn_alignbyte(d1, d0, a & 3u);
+}
+__device__ __forceinline__ uint32_t hbm4(const X &x, int32_t pos) {
+    const uintptr_t a = (uintptr_t)(x.dst + pos);
+    const gc_u32 *q = (const gc_u32 *)(a & ~(uintptr_t)3);
+    return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
+}
+__device__ __forceinline__ void put4(XSmem &s, const X &x, int32_t o, uint32_t w, int32_t n) {
+    s.ring[slot(x, o)] = (uint8_t)w;
+    if (n > 1) s.ring[slot(x, o + 1)] = (uint8_t)(w >> 8);
+    if (n > 2) s.ring[slot(x, o + 2)] = (uint8_t)(w >> 16);
+    if (n > 3) s.ring[slot(x, o + 3)] = (uint8_t)(w >> 24);
+}
+// source dword at byte address a (4-aligned) of a linear LDS buffer or of the ring
+template <bool RING>
+__device__ __forceinline__ uint32_t sdw(const XSmem &s, const uint8_t *base, uint32_t a) {
+    if (RING) return *(const uint32_t *)(s.ring + (a & RMASK));
+    return *(const uint32_t *)(base + a);
+}
+// Copy n bytes from source byte address sa (linear LDS buffer, or ring slot
+// space when RING) to output [o, o+n).  Source bytes must be final before the
+// copy, or lie >= 16 bytes (STEP16) / >= 4 bytes before each destination byte.
+// Destination: head bytes, then aligned dwords (16 bytes per step), then tail.
+template <bool RING>
+__device__ __forceinline__ void cp_run(XSmem &s, const X &x, const uint8_t *base, uint32_t sa, int32_t o, int32_t n,
+                                       bool step16) {
+    const uint32_t da = slot(x, o) & 3u;
+    int32_t head = (int32_t)((4u - da) & 3u);
+    head = head < n ? head : n;
+    if (head) put4(s, x, o, ld4r<RING>(s, base, sa), head);
+    int32_t k = head;
+    if (step16) {
+        for (; k + 16 <= n; k += 16) {
+            const uint32_t b = sa + (uint32_t)k, b0 = b & ~3u, sh = b & 3u;
+            const uint32_t r0 = sdw<RING>(s, base, b0), r1 = sdw<RING>(s, base, b0 + 4), r2 = sdw<RING>(s, base, b0 + 8),
+                           r3 = sdw<RING>(s, base, b0 + 12), r4 = sdw<RING>(s, base, b0 + 16);
+            const uint32_t d = slot(x, o + k);
+            *(uint32_t *)(s.ring + d) = __builtin_amdgcn_alignbyte(r1, r0, sh);
+            *(uint32_t *)(s.ring + ((d + 4) & RMASK)) = __builtin_amdgcn_alignbyte(r2, r1, sh);
+            *(uint32_t *)(s.ring + ((d + 8) & RMASK)) = __builtin_amdgcn_alignbyte(r3, r2, sh);
+            *(uint32_t *)(s.ring + ((d + 12) & RMASK)) = __builtin_amdgcn_alignbyte(r4, r3, sh);
         }
     }
-    if (__ballot(needmod != 0)) {
-#pragma unroll
-        for (int b = 0; b < 4; b++)
-            if (needmod & (1u << b)) k.src[b] += (int32_t)(dd[b] % oz[b]);
+    for (; k + 4 <= n; k += 4) *(uint32_t *)(s.ring + slot(x, o + k)) = ld4r<RING>(s, base, sa + (uint32_t)k);
+    if (k < n) put4(s, x, o + k, ld4r<RING>(s, base, sa + (uint32_t)k), n - k);
+}
+__device__ __forceinline__ void cp_lds(XSmem &s, const X &x, const uint8_t *base, uint32_t a, int32_t o, int32_t n) {
+    cp_run<false>(s, x, base, a, o, n, true);
+}
+__device__ __forceinline__ void cp_ring(XSmem &s, const X &x, int32_t src, int32_t o, int32_t n, uint32_t off) {
+    if (off >= 4) {
+        cp_run<true>(s, x, nullptr, slot(x, src), o, n, off >= 16);
+    } else {
+        for (int32_t k = 0; k < n; k++) s.ring[slot(x, o + k)] = s.ring[slot(x, src + k)];
     }
-#pragma unroll
-    for (int b = 0; b < 4; b++) {
-        if ((k.live & ~k.lit) & (1u << b)) {
-            if (k.src[b] >= k.cp) k.pend |= 1u << b;
-            else if (k.src[b] < ringfloor) k.far |= 1u << b;
-        }
-    }
-    k.litmin = (int32_t)dwave_min((uint32_t)litmin);
-    k.fsnap = x.F;
-    // far source bytes: always 4 loads (dummy address when not far) so the
-    // compiler can count the outstanding loads across the pipeline
-#pragma unroll
-    for (int b = 0; b < 4; b++) k.fv[b] = x.dst[(k.far & (1u << b)) ? k.src[b] : 0];
 }
 
-__device__ __forceinline__ void x_write(XSmem &s, X &x, const Cls &k) {
+__device__ __forceinline__ void x_batch(XSmem &s, X &x, bool act, int32_t o, uint32_t ll, uint32_t ml, uint32_t off,
+                                        int32_t lit, int32_t O0, int32_t O1) {
     const int l = lane_id();
-    if (k.litmin != 0x7FFFFFFF) lit_window(s, x, k.litmin, CH);
-    uint32_t val = 0;
-#pragma unroll
-    for (int b = 0; b < 4; b++) {
-        uint32_t v;
-        if (k.lit & (1u << b)) v = s.lw[k.src[b] - (int32_t)x.lw0];
-        else if (k.far & (1u << b)) v = k.fv[b];
-        else v = s.ring[slot(x, k.src[b])];
-        val |= (v & 0xFF) << (8 * b);
+    const int32_t hz = O1 - R;  // sources below hz come from HBM
+    uint64_t tq0 = ZP_NOW();
+    if (O0 - x.F >= FLUSH_T) xflush_line(s, x, O0, false);
+    if (hz > x.Fw) { wait_vm(); x.Fw = x.F; }
+    const int32_t ms = o + (int32_t)ll, msrc = ms - (int32_t)off;
+    const bool hasm = act && ml > 0;
+    // bytes [msrc, msrc + nfar) come from HBM (far part), the rest from the ring
+    int32_t nfar = hasm && msrc < hz ? (msrc + (int32_t)ml <= hz ? (int32_t)ml : hz - msrc) : 0;
+    const bool far = nfar > 0;
+    const int32_t fsnap = x.F;
+    // far prefetch, first pass (4 x 16 B, aligned) into this lane's farbuf slot
+    uint4 f0 = make_uint4(0, 0, 0, 0), f1 = f0, f2 = f0, f3 = f0;
+    const uintptr_t fa = (uintptr_t)(x.dst + msrc);
+    if (far) {
+        const gc_u4 *q = (const gc_u4 *)(fa & ~(uintptr_t)15);
+        f0 = q[0]; f1 = q[1]; f2 = q[2]; f3 = q[3];
     }
-    if (k.fsnap > x.Fw) x.Fw = k.fsnap;  // the far loads were waited for: earlier flush stores are complete
-    const uint32_t ready = k.live & ~k.pend;
-#pragma unroll
-    for (int b = 0; b < 4; b++)
-        if (ready & (1u << b)) s.ring[slot(x, k.c + 4 * l + b)] = (uint8_t)(val >> (8 * b));
-    uint32_t dw = 0;
-#pragma unroll
-    for (int b = 0; b < 4; b++) dw |= ((ready >> b) & 1u) << (8 * b);
-    *(uint32_t *)(s.done + 4 * l) = dw;
+    uint64_t tq1 = ZP_NOW();
+    // round 0: literal runs
+    if (act) cp_lds(s, x, s.lw, (uint32_t)(lit - (int32_t)x.lw0), o, (int32_t)ll);
+    uint64_t tq2 = ZP_NOW();
+    if (__ballot(far)) {
+        uint4 *fb = (uint4 *)(s.farbuf + FB * l);
+        if (far) { fb[0] = f0; fb[1] = f1; fb[2] = f2; fb[3] = f3; }
+        if (fsnap > x.Fw) x.Fw = fsnap;  // the prefetch was waited for: earlier flushes are complete
+    }
     __builtin_amdgcn_wave_barrier();
-    uint32_t pend = k.pend;
-    int guard = 0;
-    while (__ballot(pend != 0)) {
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-            if (pend & (1u << b)) {
-                if (s.done[k.src[b] - k.c]) {
-                    const int32_t xb = k.c + 4 * l + b;
-                    s.ring[slot(x, xb)] = s.ring[slot(x, k.src[b])];
-                    s.done[xb - k.c] = 1;
-                    pend &= ~(1u << b);
-                }
+    uint64_t tq3 = ZP_NOW();
+    XP_ADD(1, tq1 - tq0);
+    XP_ADD(2, tq2 - tq1);
+    XP_ADD(3, tq3 - tq2);
+    XP_ADD(5, 1);
+    // far parts: FBUSE bytes per pass through the farbuf, all far lanes together
+    if (__ballot(far)) {
+        int32_t done = 0;
+        for (;;) {
+            const int32_t n1 = nfar - done < FBUSE ? nfar - done : FBUSE;
+            if (far && n1 > 0)
+                cp_lds(s, x, s.farbuf, (uint32_t)(FB * l) + (uint32_t)((fa + (uintptr_t)done) & 15), ms + done, n1);
+            done += FBUSE;
+            const bool more = far && done < nfar;
+            if (!__ballot(more)) break;
+            if (more) {
+                const gc_u4 *q = (const gc_u4 *)((fa + (uintptr_t)done) & ~(uintptr_t)15);
+                uint4 *fb = (uint4 *)(s.farbuf + FB * l);
+                uint4 g0 = q[0], g1 = q[1], g2 = q[2], g3 = q[3];
+                fb[0] = g0; fb[1] = g1; fb[2] = g2; fb[3] = g3;
             }
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    // matches (ring parts) in rounds
+    bool pend = hasm && nfar < (int32_t)ml;
+    const int32_t ms2 = ms + nfar, msrc2 = msrc + nfar, ml2 = (int32_t)ml - nfar;
+    int guard = 0;
+    while (__ballot(pend)) {
+        const int32_t front = (int32_t)dwave_min(pend ? (uint32_t)ms : 0x7FFFFFFFu);
+        const int32_t send = msrc + (int32_t)ml < ms ? msrc + (int32_t)ml : ms;
+        const bool ready = pend && (far || send <= front);
+        if (ready) {
+            cp_ring(s, x, msrc2, ms2, ml2, off);
+            pend = false;
         }
         __builtin_amdgcn_wave_barrier();
-        if (++guard > CH) { x.bug = 101; break; }
+        XP_ADD(6, 1);
+        if (++guard > 64) { x.bug = 101; break; }
     }
+    XP_ADD(4, ZP_NOW() - tq3);
 }
 
-__device__ __forceinline__ void x_run(XSmem &s, X &x, uint32_t r, uint32_t ll, uint32_t ml, uint32_t off,
-                                      int32_t O0, int32_t lit0) {
+// whole-wave copy of one long match (ring or HBM sources)
+__device__ __forceinline__ void x_match(XSmem &s, X &x, uint32_t off, int32_t len) {
     const int l = lane_id();
-    const uint32_t len = (uint32_t)l < r ? ll + ml : 0u;
-    const uint32_t lln = (uint32_t)l < r ? ll : 0u;
-    const uint32_t incl = dpp_scan_add(len), lincl = dpp_scan_add(lln);
-    const int32_t o = O0 + (int32_t)(incl - len);
-    const int32_t lit = lit0 + (int32_t)(lincl - lln);
-    const int32_t O1 = O0 + (int32_t)readlane(incl, 63);
-    if (O1 == O0) return;
-    if ((uint32_t)l < r) s.run[l] = make_uint4((uint32_t)o, ll, off, (uint32_t)lit);
-    __builtin_amdgcn_wave_barrier();
-    const int32_t c0 = O0 - (int32_t)((uint32_t)(O0 + (int32_t)x.dmis) & (CH - 1));
-    uint32_t carry = 0;
-    if (c0 + CH - R > x.Fw) { wait_vm(); x.Fw = x.F; }
-    Cls cur, nxt;
-    uint64_t t0 = ZP_NOW();
-    x_classify(s, x, cur, c0, &carry, r, len, o, O0, O1);
-    uint64_t t1 = ZP_NOW();
-    XP_ADD(2, t1 - t0);
-    for (int32_t c = c0; c < O1; c += CH) {
-        const int32_t cn = c + CH;
-        if (cn - x.F >= FLUSH_T + CH) xflush_line(s, x, c, false);
-        const bool more = cn < O1;
-        if (more) {
-            if (cn + CH - R > x.Fw) { wait_vm(); x.Fw = x.F; }
-            x_classify(s, x, nxt, cn, &carry, r, len, o, O0, O1);
+    int32_t m = 0, step = 0;
+    if (off < 64) { m = l % (int32_t)off; step = 64 % (int32_t)off; }
+    for (int32_t k = 0; k < len; k += 64) {
+        int32_t hi = x.op + k;
+        if (hi - x.F >= FLUSH_T) xflush_line(s, x, hi);
+        int32_t ringfloor = hi + 64 - R;
+        int32_t i = k + l;
+        int32_t src = off >= 64 ? x.op - (int32_t)off + i : x.op - (int32_t)off + m;
+        bool needg = (i < len) && src < ringfloor;
+        if (__ballot(needg)) {
+            if (ringfloor > x.Fw) { wait_vm(); x.Fw = x.F; }
         }
-        uint64_t t2 = ZP_NOW();
-        x_write(s, x, cur);
-        uint64_t t3 = ZP_NOW();
-        XP_ADD(2, t2 - t1);
-        XP_ADD(3, t3 - t2);
-        XP_ADD(5, 1);
-        t1 = t3;
-        if (more) cur = nxt;
+        if (i < len) {
+            uint32_t v = src >= ringfloor ? s.ring[slot(x, src)] : x.dst[src];
+            s.ring[slot(x, x.op + i)] = (uint8_t)v;
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (off < 64) { m += step; if (m >= (int32_t)off) m -= (int32_t)off; }
     }
+    x.op += len;
+}
+
+// Execute items [0, n) of a checked run (lane j holds item j): split into
+// lane-parallel batches; long items are copied by the whole wave.
+__device__ __forceinline__ void x_run(XSmem &s, X &x, uint32_t n, uint32_t ll, uint32_t ml, uint32_t off,
+                                      int64_t *lp) {
+    const int l = lane_id();
+    const bool in = (uint32_t)l < n;
+    const uint32_t len = in ? ll + ml : 0u, lln = in ? ll : 0u;
+    const uint32_t incl = dpp_scan_add(len), lincl = dpp_scan_add(lln);
+    const int32_t O0run = x.op;
+    const int32_t o = O0run + (int32_t)(incl - len);
+    const int32_t lit = (int32_t)*lp + (int32_t)(lincl - lln);
+    const bool lng = in && len > (uint32_t)LONGI;
+    uint32_t j = 0;
+    while (j < n) {
+        const int32_t oj = (int32_t)readlane((uint32_t)o, (int)j), lj = (int32_t)readlane((uint32_t)lit, (int)j);
+        if (readlane(lng ? 1u : 0u, (int)j)) {  // one long item, whole wave
+            const uint32_t jll = readlane(ll, (int)j), jml = readlane(ml, (int)j), joff = readlane(off, (int)j);
+            x.op = oj;
+            x_lit(s, x, lj, (int32_t)jll);
+            if (jml) x_match(s, x, joff, (int32_t)jml);
+            j++;
+            continue;
+        }
+        // maximal batch from j: span, literal window and no long item
+        const int32_t endo = o + (int32_t)len, endl = lit + (int32_t)ll;
+        const bool ok = (uint32_t)l >= j && in && !lng && endo - oj <= BSPAN && endl - lj <= LW - 64;
+        const uint64_t stop = __ballot(!ok) & (~0ull << j);
+        const uint32_t e = stop ? (uint32_t)__builtin_ctzll(stop) : 64u;
+        const uint32_t eb = e > n ? n : e;
+        const bool act = (uint32_t)l >= j && (uint32_t)l < eb;
+        const int32_t O1 = (int32_t)readlane((uint32_t)endo, (int)eb - 1);
+        const int32_t L1 = (int32_t)readlane((uint32_t)endl, (int)eb - 1);
+        if (L1 > lj) lit_window(s, x, lj, L1 - lj);
+        x_batch(s, x, act, o, ll, ml, off, lit, oj, O1);
+        x.op = O1;
+        j = eb;
+    }
+    x.op = O0run + (int32_t)readlane(incl, 63);
+    *lp += readlane(lincl, 63);
 }
 
 __global__ __launch_bounds__(64) void zexec_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
@@ -1563,7 +1630,6 @@ __global__ __launch_bounds__(64) void zexec_kernel(const jfs_dev_block *__restri
 #ifdef JFS_PROF
     for (int i = 0; i < 8; i++) x.pacc[i] = 0;
 #endif
-    *(uint32_t *)(s.mk + 4 * l) = 0u;  // markers are cleared after each use; LDS starts undefined
     const uint64_t tz0 = ZP_NOW();
     __builtin_amdgcn_wave_barrier();
     x.dmis = (uint32_t)((uintptr_t)b.dst & 15u);
@@ -1606,11 +1672,9 @@ __global__ __launch_bounds__(64) void zexec_kernel(const jfs_dev_block *__restri
                 const int32_t code = (int32_t)readlane(fdst ? (uint32_t)E_DSTSMALL : (uint32_t)E_CORRUPT, (int)(nexec & 63));
                 const uint32_t el = (uint32_t)l < nexec ? len : 0u, ell = (uint32_t)l < nexec ? lln : 0u;
                 const uint32_t tot = readlane(dpp_scan_add(el), 63), totll = readlane(dpp_scan_add(ell), 63);
-                XP_ADD(6, 1);
-                if (nexec) x_run(s, x, nexec, ll, ml, off, x.op, (int32_t)lp);
-                x.op += (int32_t)tot;
-                lp += totll;
+                if (nexec) x_run(s, x, nexec, ll, ml, off, &lp);
                 lused += (int32_t)totll;
+                (void)tot;
                 if (bad) { result = code; done = true; break; }
                 k += r - 1;
             } else if (kind == IT_BSTART) {
