@@ -7,26 +7,26 @@
 //
 // Design (DESIGN.md "LZ4 decode"):
 //   The compressed stream is processed in windows of CW bytes staged in LDS.
-//   1. Parse DP: each lane owns a 32-byte piece of the window and, walking its
-//      piece backwards, computes for EVERY byte position p the position where
-//      the token chain that would start at p leaves the piece (exit[p]).
+//   1. Speculative parse: lane k owns the k-th P-byte piece of the window and
+//      walks the token chain that starts at the piece start, keeping every
+//      token's fields in registers and a bitmask of the positions it visited.
+//      Chains started at arbitrary bytes fall into the true chain within a few
+//      tokens, so after one fix-up round (entry of piece k = exit of piece k-1;
+//      a lane whose true entry is in its visited mask just drops the prefix)
+//      almost every lane already holds its true tokens; the rest re-walk.
 //      Tokens that need the exact liblz4 end-of-buffer rules, or whose length
-//      fields are very long, are marked STOP.
-//   2. Fix-up: the true entry of every piece, from the window entry.  Done as
-//      parallel fixed-point rounds (entry_k <- exit_{k-1}(entry_{k-1}), one LDS
-//      lookup per lane per round) followed by a wave-uniform verification
-//      pass that only touches LDS where a guess was wrong.
-//   3. Each lane walks the true chain of its piece, recording token positions;
-//      DPP prefix sums give token indices and output offsets; tokens land in
-//      an LDS table in stream order (SoA).
-//   4. Copy (output-centric gather): the window's output is produced in
-//      256-byte chunks, lane l owning bytes [4l, 4l+4).  Each lane finds its
-//      token(s) from a per-chunk start marker + DPP max-scan, computes each
-//      byte's source (literal in the staged input, earlier output in the LDS
-//      ring, or HBM for offsets beyond the ring), and writes one dword.  Bytes
-//      whose source lies earlier in the same chunk resolve in extra rounds.
-//      Sources in HBM for chunk i+1 are loaded while chunk i is produced.
-//      The ring is streamed to HBM with 16-byte stores at 128-byte lines.
+//      fields are very long, stop the window.
+//   2. DPP prefix sums give token indices and output offsets; the output-side
+//      fast-loop checks run; tokens go to an LDS table (8 bytes each).
+//   3. Copy, lane per token, 64 consecutive tokens per batch: literal runs
+//      first (source: the staged window), then far matches (source older than
+//      the LDS output ring: HBM, prefetched before the literal pass), then
+//      near matches in rounds -- a match is ready once its source ends at or
+//      below the earliest still-pending match start.  Copies move up to 16
+//      bytes per step (aligned LDS dword reads + v_alignbyte, byte-exact ring
+//      writes); overlapping matches (offset < 16) double their step distance.
+//      Tokens longer than LMAX are copied by the whole wave.
+//   4. The ring streams to HBM with 16-byte stores at 128-byte lines.
 //   5. Everything the fast path does not cover (the last bytes of input /
 //      output, malformed input, very long length fields) runs through an
 //      exact, wave-uniform restatement of the liblz4 1.9.3 state machine.
@@ -39,18 +39,23 @@
 namespace jfs {
 namespace lz4d {
 
-constexpr int P = 32;                  // bytes per lane piece
+constexpr int P = 64;                  // bytes per lane piece (visited set = one u64)
 constexpr int CW = 64 * P;             // compressed window bytes handled per pass
 constexpr int CWIN = CW + 80;          // LDS staging incl. lookahead (multiple of 16)
-constexpr int R = 8192;                // output ring bytes
+#ifndef JFS_LZ4_RING
+#define JFS_LZ4_RING 4096
+#endif
+constexpr int R = JFS_LZ4_RING;        // output ring bytes (power of two)
 constexpr int RMASK = R - 1;
 constexpr int TMAX = CW / 3 + 2;       // max tokens in a window (interior token >= 3 bytes)
-constexpr int TPMAX = (P + 2) / 3;     // max tokens starting in one piece (11)
 constexpr uint32_t STOP = 0x80000000u;
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr int KEXT = 64;               // max 255-extension bytes handled by the fast path
 constexpr int FLUSH_T = 1024;          // flush the ring when this many bytes are pending
-constexpr int FIX_ROUNDS = 6;          // parallel fix-up rounds before the verification pass
+constexpr int LMAX = 64;               // longer literal runs / matches are copied by the whole wave
+constexpr int BSPAN = 2048;            // max output span of one lane-parallel batch
+static_assert(BSPAN + FLUSH_T + 128 <= R, "ring must hold the unflushed tail plus one batch");
+static_assert(R - BSPAN >= LMAX + 16, "far sources must lie below the flushed prefix");
 
 #ifdef JFS_PROF
 // diagnostic build only: per-phase cycle sums (s_memtime), never in the product .so
@@ -84,18 +89,11 @@ struct Prof {
 struct Smem {
     alignas(16) uint8_t ring[R];
     alignas(16) uint8_t cwin[CWIN];
-    alignas(16) union {
-        uint32_t ex[CW];
-        struct {
-            uint32_t o[TMAX + 1];    // output position of the token
-            uint32_t lit[TMAX + 1];  // literal source position (input)
-            uint32_t lo[TMAX + 1];   // ll | off << 16
-        } tk;
-    } u;
-    uint32_t mk[64];  // per-chunk token-start markers
+    alignas(16) uint16_t tab[TMAX];  // token positions relative to cbase, stream order
+    alignas(16) uint8_t trash[256];  // per-lane sink for stores a lane does not need
 };
 
-static_assert(__builtin_offsetof(Smem, cwin) == R, "chunk gather addresses cwin as ring + R");
+static_assert(__builtin_offsetof(Smem, cwin) == R, "literal sources are addressed as ring + R");
 
 struct Ctx {
     const gc_u8 *src;
@@ -110,13 +108,6 @@ struct Ctx {
 };
 
 __device__ __forceinline__ uint32_t slot(const Ctx &c, int32_t pos) { return (uint32_t)(pos + (int32_t)c.dmis) & RMASK; }
-
-// exit table index of window position p: column-major (index-in-piece * 64 +
-// piece) so the 64 lanes, one piece each, touch 64 consecutive dwords
-__device__ __forceinline__ uint32_t exi(const Ctx &c, int32_t p) {
-    uint32_t r = (uint32_t)(p - c.cbase);
-    return (r & (P - 1)) * 64 + (r / P);
-}
 
 // ---------------------------------------------------------------------------
 // staging and byte access
@@ -200,35 +191,44 @@ __device__ __forceinline__ Tok parse_tok(const Smem &s, const Ctx &c, int32_t p)
     return t;
 }
 
-// rest of a 255-run of match-length extension bytes (rare): next position or STOP|p
-__device__ __forceinline__ uint32_t ext_tail(const Smem &s, const Ctx &c, int32_t p, int32_t q) {
-    const int32_t n = c.n;
-    int k = 1;
-    uint32_t sv;
-    do {
-        sv = cb(s, c, q);
-        q++;
-        if (q >= n - 4 || ++k > KEXT) return STOP | (uint32_t)p;
-    } while (sv == 255);
-    return (uint32_t)q;
-}
+// The same parse from the staged window only, without branches or HBM reads:
+// reads are clamped to the window, and `slow` marks tokens that need bytes
+// beyond it or a second 255-extension byte (those go through parse_tok).
+struct FTok {
+    int32_t nxt, lit;
+    uint32_t ll, ml, off, llx;
+    bool slow, stop;
+};
 
-// next-token position only (the DP's inner step); STOP|p when not a fast-path
-// token.  tb = the byte at p (from registers).  The first match-length
-// extension byte is read unconditionally (no divergent loop in the common case).
-__device__ __forceinline__ uint32_t next_pos(const Smem &s, const Ctx &c, int32_t p, uint32_t tb) {
-    const int32_t n = c.n;
-    if (p > n - 18) return STOP | (uint32_t)p;
-    uint32_t ll = tb >> 4;
-    if (ll == 15) return (uint32_t)parse_tok(s, c, p).nxt;
-    int32_t q = p + 3 + (int32_t)ll;  // first byte after the offset (<= p + 17: staged)
-    uint32_t e1 = s.cwin[q - c.cbase];
-    if ((tb & 15) == 15) {
-        q++;
-        if (q >= n - 4) return STOP | (uint32_t)p;
-        if (e1 == 255) return ext_tail(s, c, p, q);
-    }
-    return (uint32_t)q;
+__device__ __forceinline__ uint32_t w8(const Smem &s, int32_t r) { return s.cwin[r < CWIN - 1 ? r : CWIN - 1]; }
+
+__device__ __forceinline__ FTok parse_fast(const Smem &s, const Ctx &c, int32_t p) {
+    FTok t;
+    const int32_t n = c.n, b0 = c.cbase;
+    const int32_t r = p - b0;
+    const uint32_t tb = w8(s, r), e1 = w8(s, r + 1);
+    const bool llx = (tb >> 4) == 15;
+    int32_t q = r + 1 + (llx ? 1 : 0);
+    t.ll = (tb >> 4) + (llx ? e1 : 0u);
+    bool slow = llx && e1 == 255;
+    bool stop = p > n - 18;
+    stop |= llx && (b0 + q >= n - 15 || b0 + q + (int32_t)t.ll > n - 32);
+    t.lit = b0 + q;
+    q += (int32_t)t.ll;
+    slow |= q + 3 > CWIN;  // offset and the first match-length extension byte must be staged
+    const uint32_t o0 = w8(s, q), o1 = w8(s, q + 1), e2 = w8(s, q + 2);
+    q += 2;
+    const bool mlx = (tb & 15) == 15;
+    t.ml = (tb & 15) + (mlx ? e2 : 0u) + 4;
+    q += mlx ? 1 : 0;
+    slow |= mlx && e2 == 255;
+    stop |= mlx && b0 + q >= n - 4;
+    t.off = o0 | (o1 << 8);
+    t.llx = llx ? 1u : 0u;
+    t.nxt = b0 + q;
+    t.slow = slow;
+    t.stop = stop;
+    return t;
 }
 
 // ---------------------------------------------------------------------------
@@ -273,7 +273,7 @@ __device__ __forceinline__ void need_flushed(Ctx &c, int32_t lim) {
 }
 
 // ---------------------------------------------------------------------------
-// whole-wave copies (serial path)
+// whole-wave copies (serial path and long tokens)
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void coop_lit(Smem &s, Ctx &c, int32_t srcpos, int32_t op, int32_t len) {
     const int l = lane_id();
@@ -437,179 +437,238 @@ err:
 }
 
 // ---------------------------------------------------------------------------
-// chunk gather (copy phase)
+// lane-parallel copies (<= 16 bytes per step, byte-exact ring writes)
 // ---------------------------------------------------------------------------
-// Byte source kinds
-enum { K_LDS = 0, K_GLB = 1, K_ZERO = 2, K_OWN = 3, K_PEND = 4 };
+__device__ __forceinline__ void st8(uint8_t *lds, uint32_t a, uint32_t v) { lds[a] = (uint8_t)v; }
+__device__ __forceinline__ void st16(uint8_t *lds, uint32_t a, uint32_t v) { *(uint16_t *)(lds + a) = (uint16_t)v; }
+__device__ __forceinline__ void st32(uint8_t *lds, uint32_t a, uint32_t v) { *(uint32_t *)(lds + a) = v; }
 
-struct Chunk {
-    int32_t c0;       // output position of the chunk (ring slot 256-aligned)
-    uint32_t kind;    // 4 x 4-bit kinds
-    uint32_t own;     // 4 x 8-bit own-byte index (K_OWN) or source dword lane (K_PEND)
-    uint32_t addr[4]; // LDS byte address (K_LDS, K_PEND)
-    uint32_t g[4];    // prefetched HBM byte (K_GLB)
-};
-
-__device__ __forceinline__ uint32_t umod(uint32_t a, uint32_t b) {
-    // a % b for a < 2^24, 1 <= b < 2^16, via float reciprocal + fix-ups
-    uint32_t q = (uint32_t)((float)a * __builtin_amdgcn_rcpf((float)b));
-    int32_t r = (int32_t)a - (int32_t)(q * b);
-    if (r < 0) r += (int32_t)b;
-    if (r < 0) r += (int32_t)b;
-    if (r >= (int32_t)b) r -= (int32_t)b;
-    if (r >= (int32_t)b) r -= (int32_t)b;
-    return (uint32_t)r;
+// Write bytes [ha, ha + m) (1 <= m <= 16, ha = da & 3) of the 20-byte span
+// whose dwords are w0..w4 to the ring at slot da (dword 0 at da & ~3).
+// Branch-free: a store a lane does not need goes to that lane's trash dword.
+__device__ __forceinline__ void put16(Smem &s, uint32_t da, int32_t m, uint32_t w0, uint32_t w1, uint32_t w2,
+                                      uint32_t w3, uint32_t w4) {
+    uint8_t *ring = s.ring;  // offset 0 of Smem: ring slots and trash share one address space
+    const uint32_t TR = (uint32_t)__builtin_offsetof(Smem, trash) + 4u * (uint32_t)lane_id();
+    const uint32_t ha = da & 3u, D0 = da & ~3u;
+    const uint32_t e = ha + (uint32_t)m;  // 1..19
+    // dword 0: bytes [ha, min(e, 4)) -- whole dword, or b8 / b16 / b8 pieces
+    const bool full0 = ha == 0 && e >= 4u;
+    const uint32_t y0 = e < 4u ? e : 4u;
+    st32(ring, full0 ? D0 : TR, w0);
+    const bool a8 = !full0 && (ha & 1u);
+    st8(ring, a8 ? D0 + ha : TR, w0 >> (8 * ha));
+    const uint32_t x1 = ha + (ha & 1u);  // 0, 2 or 4
+    const bool a16 = !full0 && y0 >= x1 + 2;
+    st16(ring, a16 ? D0 + x1 : TR, w0 >> ((8 * x1) & 31));
+    const uint32_t x2 = x1 + (a16 ? 2u : 0u);
+    const bool b8 = !full0 && y0 > x2;
+    st8(ring, b8 ? D0 + x2 : TR, w0 >> ((8 * x2) & 31));
+    // full dwords 1..3
+    st32(ring, e >= 8u ? ((D0 + 4) & RMASK) : TR, w1);
+    st32(ring, e >= 12u ? ((D0 + 8) & RMASK) : TR, w2);
+    st32(ring, e >= 16u ? ((D0 + 12) & RMASK) : TR, w3);
+    // last partial dword L = e >> 2 (L >= 1): bytes [0, e & 3)
+    const uint32_t L = e >> 2, y = e & 3u;
+    const bool lp = L >= 1 && y != 0;
+    const uint32_t v = L <= 1 ? w1 : L == 2 ? w2 : L == 3 ? w3 : w4;
+    const uint32_t D = (D0 + 4 * L) & RMASK;
+    st16(ring, lp && y >= 2 ? D : TR, v);
+    st8(ring, lp && (y & 1u) ? D + y - 1 : TR, v >> ((8 * (y - 1)) & 31));
 }
 
-// Assign tokens to the chunk's dwords and compute every byte's source.
-// ta: token containing the chunk start (or 0 for the window's first chunk);
-// returns the token containing the chunk's last byte.
-__device__ __forceinline__ uint32_t chunk_assign(Smem &s, Ctx &c, Chunk &ch, int32_t c0, uint32_t ta, uint32_t T,
-                                                 int32_t lo, int32_t hi) {
-    const int l = lane_id();
-    const int32_t cend = c0 + 256;
-    const int32_t q = c0 + 4 * l;
-    ch.c0 = c0;
-    // HBM reads below the ring floor must see completed flush stores (never
-    // taken in steady state: flushes run ~1 KiB behind, the floor is ~8 KiB back)
-    need_flushed(c, cend - R);
-    // token-start markers: at most one token starts in any dword (tokens are >= 4 bytes)
-    uint32_t t = ta + 1 + (uint32_t)l;
-    bool tv = t < T;
-    int32_t ot = tv ? (int32_t)s.u.tk.o[t] : 0;
-    bool inch = tv && ot < cend;
-    if (inch) s.mk[(ot - c0) >> 2] = t;
-    __builtin_amdgcn_wave_barrier();
-    uint32_t m = s.mk[l];
-    s.mk[l] = NONE;
-    uint32_t mv = (m == NONE) ? 0u : m + 1;  // 1-based for the max-scan
-    uint32_t incl = dpp_scan_max(mv);
-    uint32_t excl = dpp_shift_up(incl, 0u);
-    uint32_t prev = excl ? excl - 1 : ta;  // last token starting before this dword
-    if (prev < ta) prev = ta;
-    uint32_t tnext = readlane(incl, 63);
-    tnext = tnext ? tnext - 1 : ta;
-    if (tnext < ta) tnext = ta;
-    // records of the (up to) two tokens touching this dword
-    uint32_t t0 = prev, t1 = NONE;
-    int32_t o1 = 0;
-    if (m != NONE) {
-        o1 = (int32_t)s.u.tk.o[m];
-        if (o1 == q) t0 = m;
-        else t1 = m;
-    }
-    int32_t o0 = (int32_t)s.u.tk.o[t0];
-    int32_t lit0 = (int32_t)s.u.tk.lit[t0];
-    uint32_t lo0 = s.u.tk.lo[t0];
-    int32_t lit1 = 0;
-    uint32_t lo1 = 0;
-    if (t1 != NONE) {
-        lit1 = (int32_t)s.u.tk.lit[t1];
-        lo1 = s.u.tk.lo[t1];
-    }
-    const int32_t ringfloor = cend - R;
-    const int32_t rdy = c0 > lo ? c0 : lo;
-    uint32_t kind = 0, own = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int32_t pos = q + k;
-        const bool use1 = (t1 != NONE) && pos >= o1;
-        const int32_t o = use1 ? o1 : o0;
-        const int32_t lit = use1 ? lit1 : lit0;
-        const uint32_t lw = use1 ? lo1 : lo0;
-        const int32_t ll = (int32_t)(lw & 0xFFFFu);
-        const int32_t off = (int32_t)(lw >> 16);
-        const int32_t ms = o + ll;
-        const bool inwin = pos >= lo && pos < hi;
-        const bool islit = pos < ms;
-        const int32_t sp = lit + (pos - o);
-        const uint32_t rl = (uint32_t)(sp - c.cbase);
-        uint32_t kk = (uint32_t)(pos - ms);
-        if (inwin && !islit && off != 0 && kk >= (uint32_t)off) kk = umod(kk, (uint32_t)off);
-        const int32_t x = ms - off + (int32_t)kk;
-        // classify (selects, not branches)
-        const bool lit_lds = rl < (uint32_t)CWIN;
-        const bool m_ready = x < rdy;
-        const bool m_ring = x >= ringfloor;
-        const bool m_own = x >= q;
-        uint32_t kd = !inwin ? K_LDS
-                    : islit ? (lit_lds ? K_LDS : K_GLB)
-                    : off == 0 ? K_ZERO
-                    : m_ready ? (m_ring ? K_LDS : K_GLB)
-                    : m_own ? K_OWN : K_PEND;
-        uint32_t ad = !inwin ? slot(c, pos) : islit ? (uint32_t)R + rl : slot(c, x);
-        uint32_t ow = m_own ? (uint32_t)(x - q) : (uint32_t)((x - c0) >> 2);
-        uint32_t gv = 0;
-        if (kd == K_GLB) gv = islit ? (uint32_t)c.src[sp] : (uint32_t)c.dst[x];
-        kind |= kd << (4 * k);
-        own |= (ow & 0xFFu) << (8 * k);
-        ch.addr[k] = ad;
-        ch.g[k] = gv;
-    }
-    ch.kind = kind;
-    ch.own = own;
-    return tnext;
-}
-
-__device__ __forceinline__ uint32_t pick_own(uint32_t j, uint32_t v0, uint32_t v1, uint32_t v2) {
-    return j == 0 ? v0 : (j == 1 ? v1 : v2);
-}
-
-// Produce the chunk described by ch into the ring.
-__device__ __forceinline__ void chunk_write(Smem &s, Ctx &c, const Chunk &ch) {
-    const int l = lane_id();
+// Copy m (1..16) bytes from LDS source byte address sa to ring slot da.
+// RING: sa is a ring slot (dword reads wrap); else an offset into Smem.
+template <bool RING>
+__device__ __forceinline__ void copy16(Smem &s, uint32_t sa, uint32_t da, int32_t m) {
     const uint8_t *lds = (const uint8_t *)&s;
-    uint32_t v[4];
-    uint32_t pend = 0;  // bit k: byte k not yet known
+    const uint32_t ha = da & 3u;
+    const uint32_t sb = sa - ha, S0 = sb & ~3u, sh = sb & 3u;
+    uint32_t r[6];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        uint32_t kd = (ch.kind >> (4 * k)) & 15u;
-        uint32_t x = 0;
-        if (kd == K_LDS) x = lds[ch.addr[k]];
-        else if (kd == K_GLB) x = ch.g[k];
-        else if (kd == K_PEND) pend |= 1u << k;
-        v[k] = x;
+    for (int j = 0; j < 6; ++j) {
+        const uint32_t a = RING ? ((S0 + 4 * j) & RMASK) : (S0 + 4 * j);
+        r[j] = *(const uint32_t *)(lds + a);
     }
-#pragma unroll
-    for (int k = 1; k < 4; ++k) {
-        uint32_t kd = (ch.kind >> (4 * k)) & 15u;
-        if (kd == K_OWN) {
-            uint32_t j = (ch.own >> (8 * k)) & 0xFFu;
-            v[k] = pick_own(j, v[0], v[1], v[2]);
-            if (pend & (1u << j)) pend |= 1u << k;
+    put16(s, da, m, __builtin_amdgcn_alignbyte(r[1], r[0], sh), __builtin_amdgcn_alignbyte(r[2], r[1], sh),
+          __builtin_amdgcn_alignbyte(r[3], r[2], sh), __builtin_amdgcn_alignbyte(r[4], r[3], sh),
+          __builtin_amdgcn_alignbyte(r[5], r[4], sh));
+}
+
+__device__ __forceinline__ uint32_t pick5(int32_t q, uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t e) {
+    return q < 0 ? a : q == 0 ? b : q == 1 ? c : q == 2 ? d : e;
+}
+
+// One lane-parallel batch: lanes with act hold consecutive tokens producing
+// output [O0, O1), O1 - O0 <= BSPAN, every ll/ml <= LMAX.
+__device__ __forceinline__ void batch(Smem &s, Ctx &c, bool act, int32_t o, uint32_t ll, uint32_t ml, uint32_t off,
+                                      uint32_t litr, int32_t O0, int32_t O1 PROF_ARG) {
+    const int32_t hz = O1 - R;  // sources below hz come from HBM
+    if (O0 - c.F >= FLUSH_T) flush_to_line(s, c, O0);
+    const int32_t ms = o + (int32_t)ll, msrc = ms - (int32_t)off;
+    const bool hasm = act && ml > 0;
+    const bool zero = hasm && off == 0;
+    const bool far = hasm && off != 0 && msrc < hz;
+    if (__ballot(far) && hz + LMAX > c.Fw) {
+        wait_vm();
+        c.Fw = c.F;
+        if (hz + LMAX > c.Fw) c.bug = 4;
+    }
+    // far prefetch: 32 bytes from the 16-byte line holding the source start
+    uint4 f0 = make_uint4(0, 0, 0, 0), f1 = f0;
+    if (far) {
+        const gc_u4 *q = (const gc_u4 *)((uintptr_t)(c.dst + msrc) & ~(uintptr_t)15);
+        f0 = q[0];
+        f1 = q[1];
+    }
+    // literal runs (source: staged window, addressed as ring + R + litr)
+    for (uint32_t k = 0; __ballot(act && k < ll); k += 16) {
+        if (act && k < ll) {
+            const int32_t m = ll - k < 16u ? (int32_t)(ll - k) : 16;
+            copy16<false>(s, (uint32_t)R + litr + k, slot(c, o + (int32_t)k), m);
         }
     }
-    const uint32_t dslot = slot(c, ch.c0 + 4 * l);
-    if (pend == 0) *(uint32_t *)(s.ring + dslot) = v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24);
-    // in-chunk dependencies: resolve in rounds (lower dwords first); every
-    // round resolves at least the lowest pending dword, so <= 64 rounds
-    for (int guard = 0; __ballot(pend != 0); ++guard) {
-        if (guard > 64) { c.bug = 1; break; }
-        uint64_t done = __ballot(pend == 0);
-        uint32_t dlo = (uint32_t)done, dhi = (uint32_t)(done >> 32);
-        uint32_t was = pend;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (pend & (1u << k)) {
-                uint32_t kd = (ch.kind >> (4 * k)) & 15u;
-                if (kd == K_PEND) {
-                    uint32_t d = (ch.own >> (8 * k)) & 0xFFu;
-                    bool ok = d < 32 ? ((dlo >> d) & 1u) : ((dhi >> (d - 32)) & 1u);
-                    if (ok) {
-                        v[k] = lds[ch.addr[k]];
-                        pend &= ~(1u << k);
-                    }
-                } else {  // K_OWN waiting on an earlier byte of this dword
-                    uint32_t j = (ch.own >> (8 * k)) & 0xFFu;
-                    if (!(pend & (1u << j))) {
-                        v[k] = pick_own(j, v[0], v[1], v[2]);
-                        pend &= ~(1u << k);
-                    }
+    PSTAMP(4);
+    // far matches (and offset-0 matches, which write zeros)
+    if (__ballot(far || zero)) {
+        for (uint32_t k = 0; __ballot((far || zero) && k < ml); k += 16) {
+            if ((far || zero) && k < ml) {
+                const int32_t m = ml - k < 16u ? (int32_t)(ml - k) : 16;
+                const uint32_t da = slot(c, ms + (int32_t)k);
+                uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0, w4 = 0;
+                if (far) {
+                    const uintptr_t sA = (uintptr_t)(c.dst + msrc + (int32_t)k) - (da & 3u);
+                    const uintptr_t B = (uintptr_t)(c.dst + msrc + (int32_t)k) & ~(uintptr_t)15;
+                    const int32_t rel = (int32_t)((intptr_t)sA - (intptr_t)B);  // -3..15
+                    const int32_t q = rel >> 2;                                   // -1..3
+                    const uint32_t sh = (uint32_t)rel & 3u;
+                    const uint32_t d0 = f0.x, d1 = f0.y, d2 = f0.z, d3 = f0.w, d4 = f1.x, d5 = f1.y, d6 = f1.z,
+                                   d7 = f1.w;
+                    const uint32_t e0 = pick5(q, 0u, d0, d1, d2, d3), e1 = pick5(q, d0, d1, d2, d3, d4),
+                                   e2 = pick5(q, d1, d2, d3, d4, d5), e3 = pick5(q, d2, d3, d4, d5, d6),
+                                   e4 = pick5(q, d3, d4, d5, d6, d7), e5 = pick5(q, d4, d5, d6, d7, 0u);
+                    w0 = __builtin_amdgcn_alignbyte(e1, e0, sh);
+                    w1 = __builtin_amdgcn_alignbyte(e2, e1, sh);
+                    w2 = __builtin_amdgcn_alignbyte(e3, e2, sh);
+                    w3 = __builtin_amdgcn_alignbyte(e4, e3, sh);
+                    w4 = __builtin_amdgcn_alignbyte(e5, e4, sh);
+                }
+                put16(s, da, m, w0, w1, w2, w3, w4);
+            }
+            const bool more = far && k + 16 < ml;
+            if (__ballot(more)) {
+                if (more) {
+                    const gc_u4 *q = (const gc_u4 *)((uintptr_t)(c.dst + msrc + (int32_t)k + 16) & ~(uintptr_t)15);
+                    f0 = q[0];
+                    f1 = q[1];
                 }
             }
         }
-        if (pend == 0 && was != 0) *(uint32_t *)(s.ring + dslot) = v[0] | (v[1] << 8) | (v[2] << 16) | (v[3] << 24);
     }
+    PSTAMP(5);
+    // near matches in rounds
+    bool pend = hasm && !far && !zero;
+    int32_t pos = ms, rem = (int32_t)ml, D = (int32_t)off;
+    const int32_t send = msrc + (int32_t)ml < ms ? msrc + (int32_t)ml : ms;
+    for (int guard = 0; __ballot(pend); ++guard) {
+        if (guard > 64) { c.bug = 5; break; }
+        const int32_t front = (int32_t)dwave_min(pend ? (uint32_t)ms : 0x7FFFFFFFu);
+        bool go = pend && send <= front;
+        while (__ballot(go)) {
+            if (go) {
+                const int32_t m = rem < 16 ? (rem < D ? rem : D) : (D < 16 ? D : 16);
+                copy16<true>(s, slot(c, pos - D), slot(c, pos), m);
+                pos += m;
+                rem -= m;
+                if (m == D && D < 16) D <<= 1;
+                if (rem <= 0) { go = false; pend = false; }
+            }
+        }
+    }
+    PSTAMP(6);
+}
+
+// Copy the window's tokens [0, T) (positions in s.tab, relative to cbase),
+// starting at output op0.  Returns the number of tokens copied; fewer than T
+// when an output-side fast-loop check declines a token (*bad_ip = its input
+// position).  *end_op = output position after the copied tokens.
+__device__ __forceinline__ uint32_t copy_tokens(Smem &s, Ctx &c, uint32_t T, int32_t op0, int32_t *end_op,
+                                                int32_t *bad_ip PROF_ARG) {
+    const int l = lane_id();
+    int32_t op = op0;
+    const int32_t cap = c.cap;
+    for (uint32_t g0 = 0; g0 < T; g0 += 64) {
+        const uint32_t n0 = T - g0 < 64u ? T - g0 : 64u;
+        const bool in0 = (uint32_t)l < n0;
+        const int32_t p = c.cbase + (in0 ? (int32_t)s.tab[g0 + l] : 0);
+        FTok t = parse_fast(s, c, p);
+        const bool sl = in0 && t.slow;
+        if (__ballot(sl)) {
+            if (sl) {
+                const Tok u = parse_tok(s, c, p);
+                t.lit = u.lit;
+                t.ll = (uint32_t)u.ll;
+                t.ml = (uint32_t)u.ml;
+                t.off = (uint32_t)u.off;
+                t.llx = (uint32_t)u.llx;
+            }
+        }
+        const uint32_t ll = in0 ? t.ll : 0u, ml = in0 ? t.ml : 0u, off = t.off;
+        const uint32_t litr = (uint32_t)(t.lit - c.cbase);
+        const uint32_t len = ll + ml;
+        const uint32_t incl = dpp_scan_add(len);
+        const int32_t o = op + (int32_t)(incl - len);
+        const int32_t om = o + (int32_t)ll;
+        const bool bad = in0 && ((t.llx && om > cap - 32) || (om + (int32_t)ml >= cap - 64) || ((int32_t)off > om));
+        const uint64_t bm = __ballot(bad);
+        const uint32_t n = bm ? (uint32_t)__builtin_ctzll(bm) : n0;
+        const bool in = (uint32_t)l < n;
+        const int32_t endo = o + (int32_t)len;
+        const bool lng = in && (ll > (uint32_t)LMAX || ml > (uint32_t)LMAX);
+        PSTAMP(2);
+        uint32_t j = 0;
+        while (j < n) {
+            const int32_t oj = (int32_t)readlane((uint32_t)o, (int)j);
+            if (readlane(lng ? 1u : 0u, (int)j)) {  // one long token, whole wave
+                const uint32_t jll = readlane(ll, (int)j), jml = readlane(ml, (int)j), joff = readlane(off, (int)j);
+                const uint32_t jlit = readlane(litr, (int)j);
+                coop_lit(s, c, c.cbase + (int32_t)jlit, oj, (int32_t)jll);
+                coop_match(s, c, oj + (int32_t)jll, (int32_t)joff, (int32_t)jml);
+                PSTAMP(7);
+                j++;
+                continue;
+            }
+            const bool ok = (uint32_t)l >= j && in && !lng && endo - oj <= BSPAN;
+            const uint64_t stop = __ballot(!ok) & (~0ull << j);
+            const uint32_t e = stop ? (uint32_t)__builtin_ctzll(stop) : 64u;
+            const uint32_t eb = e > n ? n : e;
+            const bool act = (uint32_t)l >= j && (uint32_t)l < eb;
+            const int32_t O1 = (int32_t)readlane((uint32_t)endo, (int)eb - 1);
+            PSTAMP(3);
+            batch(s, c, act, o, ll, ml, off, litr, oj, O1 PROF_PASS);
+            j = eb;
+        }
+        if (bm) {
+            *bad_ip = (int32_t)readlane((uint32_t)p, (int)n);
+            *end_op = (int32_t)readlane((uint32_t)o, (int)n);
+            return g0 + n;
+        }
+        op += (int32_t)readlane(incl, 63);
+    }
+    *end_op = op;
+    return T;
+}
+
+// next token position after p (or STOP | p), fast path with the exact parse
+// for the rare tokens the window-only parse cannot take
+__device__ __forceinline__ uint32_t step_next(const Smem &s, const Ctx &c, int32_t p, bool act) {
+    const FTok t = parse_fast(s, c, p);
+    uint32_t x = t.stop ? (STOP | (uint32_t)p) : (uint32_t)t.nxt;
+    const bool sl = act && t.slow;
+    if (__ballot(sl)) {
+        if (sl) x = (uint32_t)parse_tok(s, c, p).nxt;
+    }
+    return x;
 }
 
 // ---------------------------------------------------------------------------
@@ -621,203 +680,124 @@ __device__ __forceinline__ void window(Smem &s, Ctx &c, Ser &st, int *stopped PR
     const int32_t op0 = st.op;
     stage_window(s, c, wbase);
     const int32_t cbase = c.cbase;
+    __builtin_amdgcn_wave_barrier();
     PSTAMP(0);
 
-    // 1. exit DP over this lane's piece, backwards
+    // 1. speculative walk of this lane's piece: visited positions + exit
     const int32_t plo = cbase + l * P, phi = plo + P;
-    uint32_t pw[8];
+    uint32_t cur = l == 0 ? (uint32_t)wbase : (uint32_t)plo;
+    uint64_t vs = 0;  // positions the speculative chain visited (bit = position - plo)
+    uint32_t sx = 0;  // its exit: first position >= phi, or STOP | p
     {
-        uint4 a = *(const uint4 *)(s.cwin + P * l);
-        uint4 b = *(const uint4 *)(s.cwin + P * l + 16);
-        pw[0] = a.x; pw[1] = a.y; pw[2] = a.z; pw[3] = a.w;
-        pw[4] = b.x; pw[5] = b.y; pw[6] = b.z; pw[7] = b.w;
-    }
-    // positions in groups of three: a token is >= 3 bytes, so every next
-    // position of the group lies above it and the three exit lookups are
-    // independent (one LDS round trip per group instead of per position)
-#pragma unroll
-    for (int g = P - 1; g >= 0; g -= 3) {
-        uint32_t nx[3];
-#pragma unroll
-        for (int u = 0; u < 3; ++u) {
-            const int i = g - u;
-            if (i < 0) continue;
-            uint32_t tb = (pw[i >> 2] >> ((i & 3) * 8)) & 0xFFu;
-            nx[u] = next_pos(s, c, plo + i, tb);
-        }
-        uint32_t e[3];
-#pragma unroll
-        for (int u = 0; u < 3; ++u) {
-            const int i = g - u;
-            if (i < 0) continue;
-            uint32_t x = nx[u];
-            bool direct = (x & STOP) || (int32_t)x >= phi;
-            uint32_t idx = direct ? (uint32_t)l : ((uint32_t)((int32_t)x - plo)) * 64 + (uint32_t)l;
-            uint32_t v = s.u.ex[idx];
-            e[u] = direct ? x : v;
-        }
-#pragma unroll
-        for (int u = 0; u < 3; ++u) {
-            const int i = g - u;
-            if (i < 0) continue;
-            s.u.ex[(uint32_t)i * 64 + (uint32_t)l] = e[u];
+        int32_t q = (int32_t)cur;
+        bool act = true;
+        for (int guard = 0; __ballot(act); ++guard) {
+            if (act) {
+                const uint32_t x = step_next(s, c, q, act);
+                if (x & STOP) {
+                    sx = x;
+                    act = false;
+                } else {
+                    vs |= 1ull << (uint32_t)(q - plo);
+                    q = (int32_t)x;
+                    if (q >= phi) {
+                        sx = (uint32_t)q;
+                        act = false;
+                    }
+                }
+            }
+            if (guard > P) { c.bug = 6; break; }
         }
     }
-    __builtin_amdgcn_wave_barrier();
+    // 2. fix-up: true entry of piece k = exit of piece k-1.  An entry on the
+    //    speculative chain keeps its suffix; otherwise walk from the entry until
+    //    the chain meets the speculative one (or leaves the piece).
+    uint64_t vt = vs;  // true chain positions in this piece
+    uint32_t ex = sx;  // true exit
+    for (int r = 0;; ++r) {
+        const uint32_t In = dpp_shift_up(ex, (uint32_t)wbase);
+        const bool ch = In != cur;
+        if (!__ballot(ch)) break;
+        if (r > 64) { c.bug = 3; break; }
+        bool part = false;
+        if (ch) {
+            cur = In;
+            if ((In & STOP) || (int32_t)In >= phi) {
+                vt = 0;
+                ex = In;
+            } else {
+                const uint32_t d = In - (uint32_t)plo;
+                if ((vs >> d) & 1ull) {
+                    vt = vs & (~0ull << d);
+                    ex = sx;
+                } else {
+                    part = true;
+                }
+            }
+        }
+        int32_t q = (int32_t)In;
+        uint64_t vp = 0;
+        for (int guard = 0; __ballot(part); ++guard) {
+            if (part) {
+                const uint32_t d = (uint32_t)(q - plo);
+                if ((vs >> d) & 1ull) {  // joined the speculative chain
+                    vt = vp | (vs & (~0ull << d));
+                    ex = sx;
+                    part = false;
+                } else {
+                    const uint32_t x = step_next(s, c, q, part);
+                    if (x & STOP) {
+                        vt = vp;
+                        ex = x;
+                        part = false;
+                    } else {
+                        vp |= 1ull << d;
+                        q = (int32_t)x;
+                        if (q >= phi) {
+                            vt = vp;
+                            ex = (uint32_t)q;
+                            part = false;
+                        }
+                    }
+                }
+            }
+            if (guard > P) { c.bug = 7; break; }
+        }
+    }
+    const uint32_t efin = readlane(ex, 63);
     PSTAMP(1);
 
-    // 2. fix-up: parallel fixed-point rounds, then verify
-    uint32_t E = dpp_shift_up(s.u.ex[l], (uint32_t)wbase);
-    uint32_t X = 0;
-    bool conv = false;
-    for (int r = 0; r < FIX_ROUNDS; ++r) {
-        X = ((E & STOP) || (int32_t)E >= phi) ? E : s.u.ex[exi(c, (int32_t)E)];
-        uint32_t En = dpp_shift_up(X, (uint32_t)wbase);
-        uint64_t chg = __ballot(En != E);
-        E = En;
-        if (!chg) { conv = true; break; }
-    }
-    uint32_t ent, efin;
-    X = ((E & STOP) || (int32_t)E >= phi) ? E : s.u.ex[exi(c, (int32_t)E)];
-    if (conv) {
-        ent = E;
-        efin = readlane(X, 63);
-    } else {
-        uint32_t e = (uint32_t)wbase;
-        ent = STOP;
-        for (int k = 0; k < 64; ++k) {
-            if (l == k) ent = e;
-            uint32_t Ek = readlane(E, k);
-            if (e == Ek) {
-                e = readlane(X, k);
-            } else if (!(e & STOP) && (int32_t)e < cbase + (k + 1) * P) {
-                e = uniform(s.u.ex[exi(c, (int32_t)e)]);
+    // 3. token table: positions (relative to cbase) in stream order
+    const uint32_t cnt = (uint32_t)__builtin_popcountll(vt);
+    const uint32_t cinc = dpp_scan_add(cnt);
+    const uint32_t T = readlane(cinc, 63);
+    {
+        uint32_t idx = cinc - cnt;
+        uint64_t v = vt;
+        while (__ballot(v != 0)) {
+            if (v) {
+                const uint32_t b = (uint32_t)__builtin_ctzll(v);
+                s.tab[idx] = (uint16_t)((uint32_t)l * P + b);
+                idx++;
+                v &= v - 1;
             }
         }
-        efin = e;
     }
+    __builtin_amdgcn_wave_barrier();
     PSTAMP(2);
 
-    // 3a. walk the true chain of this piece, recording every token's fields
-    int32_t tpos[TPMAX], tlit[TPMAX];
-    uint32_t tlm[TPMAX], tof[TPMAX];  // ll | ml << 16 ; off | llx << 16
-    uint32_t cnt = 0, olen = 0;
-    int32_t stop_ip = -1;
-    {
-        int32_t qq = (int32_t)ent;
-        bool act = !(ent & STOP) && qq < phi;
-#pragma unroll
-        for (int j = 0; j < TPMAX; ++j) {
-            tpos[j] = qq;
-            tlit[j] = 0;
-            tlm[j] = 0;
-            tof[j] = 0;
-            if (act) {
-                Tok t = parse_tok(s, c, qq);
-                if ((uint32_t)t.nxt & STOP) {
-                    stop_ip = qq;
-                    act = false;
-                } else {
-                    cnt++;
-                    olen += (uint32_t)(t.ll + t.ml);
-                    tlit[j] = t.lit;
-                    tlm[j] = (uint32_t)t.ll | ((uint32_t)t.ml << 16);
-                    tof[j] = (uint32_t)t.off | ((uint32_t)t.llx << 16);
-                    qq = t.nxt;
-                    if (qq >= phi) act = false;
-                }
-            }
-        }
-    }
-    uint32_t cinc = dpp_scan_add(cnt), oinc = dpp_scan_add(olen);
-    uint32_t tbase = cinc - cnt, obase = oinc - olen;
-    uint32_t ntok = readlane(cinc, 63), nout = readlane(oinc, 63);
-    __builtin_amdgcn_wave_barrier();
-
-    // 3b. emit records, with the output-side fast-loop checks
-    uint32_t bad_idx = NONE;
-    int32_t bad_ip = 0, bad_op = 0;
-    if (stop_ip >= 0) {
-        bad_idx = tbase + cnt;
-        bad_ip = stop_ip;
-        bad_op = op0 + (int32_t)(obase + olen);
-    }
-    {
-        int32_t o = op0 + (int32_t)obase;
-        bool act = true;
-        const int32_t cap = c.cap;
-#pragma unroll
-        for (int j = 0; j < TPMAX; ++j) {
-            if (act && (uint32_t)j < cnt) {
-                int32_t ll = (int32_t)(tlm[j] & 0xFFFFu), ml = (int32_t)(tlm[j] >> 16);
-                int32_t off = (int32_t)(tof[j] & 0xFFFFu);
-                bool llx = (tof[j] >> 16) != 0;
-                int32_t om = o + ll;
-                bool bad = (llx && om > cap - 32) || (om + ml >= cap - 64) || (off > om);
-                uint32_t idx = tbase + (uint32_t)j;
-                if (bad) {
-                    bad_idx = idx;
-                    bad_ip = tpos[j];
-                    bad_op = o;
-                    act = false;
-                } else {
-                    s.u.tk.o[idx] = (uint32_t)o;
-                    s.u.tk.lit[idx] = (uint32_t)tlit[j];
-                    s.u.tk.lo[idx] = (uint32_t)ll | ((uint32_t)off << 16);
-                    o = om + ml;
-                }
-            }
-        }
-    }
-    uint32_t T = dwave_min(bad_idx);
-    int32_t end_ip, end_op;
-    if (T == NONE) {
-        T = ntok;
-        end_ip = (int32_t)efin;
-        end_op = op0 + (int32_t)nout;
-        *stopped = (efin & STOP) ? 1 : 0;  // (cannot be STOP without a stop token)
-    } else {
-        uint64_t mm = __ballot(bad_idx == T);
-        int src_l = (int)__builtin_ctzll(mm);
-        end_ip = (int32_t)readlane((uint32_t)bad_ip, src_l);
-        end_op = (int32_t)readlane((uint32_t)bad_op, src_l);
-        *stopped = 1;
-    }
+    // 4. copy
+    int32_t end_op = op0, bad_ip = 0;
+    const uint32_t done = T > 0 ? copy_tokens(s, c, T, op0, &end_op, &bad_ip PROF_PASS) : 0u;
     __builtin_amdgcn_wave_barrier();
     PSTAMP(3);
-
-    // 4. chunk gather over output [op0, end_op)
-    if (T > 0) {
-        const int32_t lo = op0, hi = end_op;
-        int32_t c0 = (int32_t)(((uint32_t)op0 + c.dmis) & ~255u) - (int32_t)c.dmis;
-        // two chunk descriptors alternate roles (no register copies: a copy of
-        // a prefetch destination would wait for the HBM load)
-        Chunk A, B;
-        uint32_t ta = chunk_assign(s, c, A, c0, 0u, T, lo, hi);
-        for (;;) {
-            int32_t c1 = c0 + 256;
-            bool more = c1 < hi;
-            if (more) ta = chunk_assign(s, c, B, c1, ta, T, lo, hi);
-            PSTAMP(4);
-            if (c0 - c.F >= FLUSH_T) flush_to_line(s, c, c0);
-            PSTAMP(7);
-            chunk_write(s, c, A);
-            PSTAMP(5);
-            if (!more) break;
-            c0 = c1;
-            c1 = c0 + 256;
-            more = c1 < hi;
-            if (more) ta = chunk_assign(s, c, A, c1, ta, T, lo, hi);
-            PSTAMP(4);
-            if (c0 - c.F >= FLUSH_T) flush_to_line(s, c, c0);
-            PSTAMP(7);
-            chunk_write(s, c, B);
-            PSTAMP(5);
-            if (!more) break;
-            c0 = c1;
-        }
+    if (done < T) {
+        st.ip = bad_ip;
+        *stopped = 1;
+    } else {
+        st.ip = (int32_t)(efin & ~STOP);
+        *stopped = (efin & STOP) ? 1 : 0;
     }
-    st.ip = end_ip;
     st.op = end_op;
 }
 
@@ -843,7 +823,7 @@ __global__ __launch_bounds__(64) void lz4_decode_kernel(const jfs_dev_block *__r
     Prof pr;
     pr.start();
 #endif
-    s.mk[l] = NONE;
+    (void)l;
     if (d.src == nullptr || c.n < 0 || c.cap < 0) {
         result = -1;
     } else if (c.cap == 0) {
@@ -858,7 +838,7 @@ __global__ __launch_bounds__(64) void lz4_decode_kernel(const jfs_dev_block *__r
         st.ret = 0;
         int status = SER_CONT;
         for (int64_t guard = 0;; ++guard) {
-            if (c.bug || guard > (int64_t)c.n + 64) { status = SER_ERR; st.ret = INT32_MIN; c.bug = 1; break; }
+            if (c.bug || guard > (int64_t)c.n + 64) { status = SER_ERR; st.ret = INT32_MIN; c.bug |= 1; break; }
             int32_t ip_before = st.ip;
             if (st.fast && st.ip < c.n - 64 && st.op < c.cap - 128) {
                 int stopped = 0;
@@ -879,7 +859,7 @@ __global__ __launch_bounds__(64) void lz4_decode_kernel(const jfs_dev_block *__r
             result = st.ret;
         }
     }
-    if (l == 0) ret[b] = result;
+    if (lane_id() == 0) ret[b] = result;
 #ifdef JFS_PROF
     pr.stamp(9);
     pr.flush_out();

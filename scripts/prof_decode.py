@@ -17,7 +17,7 @@ t0 = time.perf_counter(); b.decompress(); torch.cuda.synchronize(); dt = time.pe
 assert b.verify()
 buf = (ctypes.c_uint64 * 10)()
 lib.jfs_prof_read(buf)
-names = ["stage", "dp", "fixup", "walks+emit", "lits+grouping", "match_rounds", "long_coop", "flush", "serial", "tail"]
+names = ["stage", "walk+fixup", "table+tokparse", "batching", "lits+pref", "far", "near", "long", "serial", "tail"]
 tot = sum(buf)
 print(f"blocks={nblk} cls={cls} wall={dt*1e3:.1f} ms  GiB/s={nblk*4/1024/dt:.1f}")
 for n, v in zip(names, buf):
