@@ -566,10 +566,39 @@ __device__ __forceinline__ void batch(Smem &s, Ctx &c, bool act, int32_t o, uint
         }
     }
     PSTAMP(5);
-    // near matches in rounds
+    // source substitution: out[x] == out[x - off_i] for every byte x a match i
+    // writes, so a pending match whose whole source lies inside another pending
+    // match of this batch can read that match's source instead (repeatedly).
+    // This shortens the dependency chains the rounds below must walk.
     bool pend = hasm && !far && !zero;
-    int32_t pos = ms, rem = (int32_t)ml, D = (int32_t)off;
-    const int32_t send = msrc + (int32_t)ml < ms ? msrc + (int32_t)ml : ms;
+    int32_t src = msrc;
+    {
+        const uint64_t am = __ballot(act);
+        const int first = am ? (int)__builtin_ctzll(am) : 0;
+        const uint32_t key = act ? (uint32_t)ms : (lane_id() < first ? 0u : 0xFFFFFFFFu);  // non-decreasing
+        const uint32_t mek = pend ? (uint32_t)(ms + (int32_t)ml) : 0u;
+        bool cand = pend && off >= ml;
+        for (int it = 0; it < 3; ++it) {
+            const bool want = cand && src >= O0;
+            if (!__ballot(want)) break;
+            int lo = 0;  // last lane with key <= src
+#pragma unroll
+            for (int stp = 32; stp; stp >>= 1) {
+                const uint32_t v = (uint32_t)__shfl((int)key, lo + stp, 64);
+                lo = v <= (uint32_t)src ? lo + stp : lo;
+            }
+            const uint32_t vms = (uint32_t)__shfl((int)key, lo, 64);
+            const uint32_t vme = (uint32_t)__shfl((int)mek, lo, 64);
+            const int32_t voff = __shfl((int)off, lo, 64);
+            const bool ok = want && vms <= (uint32_t)src && (uint32_t)(src + (int32_t)ml) <= vme && voff > 0 &&
+                            src - voff >= hz;
+            src = ok ? src - voff : src;
+            cand = ok;
+        }
+    }
+    // near matches in rounds
+    int32_t pos = ms, rem = (int32_t)ml, D = ms - src;
+    const int32_t send = src + (int32_t)ml < ms ? src + (int32_t)ml : ms;
     for (int guard = 0; __ballot(pend); ++guard) {
         if (guard > 64) { c.bug = 5; break; }
         const int32_t front = (int32_t)dwave_min(pend ? (uint32_t)ms : 0x7FFFFFFFu);
