@@ -90,8 +90,7 @@ struct Smem {
     alignas(16) uint8_t ring[R];
     alignas(16) uint8_t cwin[CWIN];
     alignas(16) uint16_t tab[TMAX];  // token positions relative to cbase, stream order
-    alignas(16) uint8_t trash[256];  // per-lane sink for stores a lane does not need
-};
+    };
 
 static_assert(__builtin_offsetof(Smem, cwin) == R, "literal sources are addressed as ring + R");
 
@@ -439,42 +438,43 @@ err:
 // ---------------------------------------------------------------------------
 // lane-parallel copies (<= 16 bytes per step, byte-exact ring writes)
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void st8(uint8_t *lds, uint32_t a, uint32_t v) { lds[a] = (uint8_t)v; }
-__device__ __forceinline__ void st16(uint8_t *lds, uint32_t a, uint32_t v) { *(uint16_t *)(lds + a) = (uint16_t)v; }
-__device__ __forceinline__ void st32(uint8_t *lds, uint32_t a, uint32_t v) { *(uint32_t *)(lds + a) = v; }
+// Bytes [0, k) of a dword, k clamped to [0, 4].
+__device__ __forceinline__ uint32_t lomask(int32_t k) {
+    k = k < 0 ? 0 : k;
+    return k >= 4 ? 0xFFFFFFFFu : ((1u << (8 * k)) - 1u);
+}
+
+__device__ __forceinline__ void lds_or(uint8_t *ring, uint32_t a, uint32_t v) {  // a % 4 == 0
+    __hip_atomic_fetch_or(reinterpret_cast<uint32_t *>(ring) + (a >> 2), v, __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 
 // Write bytes [ha, ha + m) (1 <= m <= 16, ha = da & 3) of the 20-byte span
 // whose dwords are w0..w4 to the ring at slot da (dword 0 at da & ~3).
-// Branch-free: a store a lane does not need goes to that lane's trash dword.
+// The batch's output span is zeroed before it is produced, so every lane ORs
+// its bytes in with whole-dword LDS atomics: lanes sharing a boundary dword
+// cannot clobber each other, and no byte stores or branches are needed.
 __device__ __forceinline__ void put16(Smem &s, uint32_t da, int32_t m, uint32_t w0, uint32_t w1, uint32_t w2,
                                       uint32_t w3, uint32_t w4) {
-    uint8_t *ring = s.ring;  // offset 0 of Smem: ring slots and trash share one address space
-    const uint32_t TR = (uint32_t)__builtin_offsetof(Smem, trash) + 4u * (uint32_t)lane_id();
-    const uint32_t ha = da & 3u, D0 = da & ~3u;
-    const uint32_t e = ha + (uint32_t)m;  // 1..19
-    // dword 0: bytes [ha, min(e, 4)) -- whole dword, or b8 / b16 / b8 pieces
-    const bool full0 = ha == 0 && e >= 4u;
-    const uint32_t y0 = e < 4u ? e : 4u;
-    st32(ring, full0 ? D0 : TR, w0);
-    const bool a8 = !full0 && (ha & 1u);
-    st8(ring, a8 ? D0 + ha : TR, w0 >> (8 * ha));
-    const uint32_t x1 = ha + (ha & 1u);  // 0, 2 or 4
-    const bool a16 = !full0 && y0 >= x1 + 2;
-    st16(ring, a16 ? D0 + x1 : TR, w0 >> ((8 * x1) & 31));
-    const uint32_t x2 = x1 + (a16 ? 2u : 0u);
-    const bool b8 = !full0 && y0 > x2;
-    st8(ring, b8 ? D0 + x2 : TR, w0 >> ((8 * x2) & 31));
-    // full dwords 1..3
-    st32(ring, e >= 8u ? ((D0 + 4) & RMASK) : TR, w1);
-    st32(ring, e >= 12u ? ((D0 + 8) & RMASK) : TR, w2);
-    st32(ring, e >= 16u ? ((D0 + 12) & RMASK) : TR, w3);
-    // last partial dword L = e >> 2 (L >= 1): bytes [0, e & 3)
-    const uint32_t L = e >> 2, y = e & 3u;
-    const bool lp = L >= 1 && y != 0;
-    const uint32_t v = L <= 1 ? w1 : L == 2 ? w2 : L == 3 ? w3 : w4;
-    const uint32_t D = (D0 + 4 * L) & RMASK;
-    st16(ring, lp && y >= 2 ? D : TR, v);
-    st8(ring, lp && (y & 1u) ? D + y - 1 : TR, v >> ((8 * (y - 1)) & 31));
+    uint8_t *ring = s.ring;
+    const int32_t ha = (int32_t)(da & 3u), e = ha + m;  // 1..19
+    const uint32_t D0 = da & ~3u;
+    lds_or(ring, D0, w0 & lomask(e) & ~lomask(ha));
+    lds_or(ring, (D0 + 4) & RMASK, w1 & lomask(e - 4));
+    lds_or(ring, (D0 + 8) & RMASK, w2 & lomask(e - 8));
+    lds_or(ring, (D0 + 12) & RMASK, w3 & lomask(e - 12));
+    lds_or(ring, (D0 + 16) & RMASK, w4 & lomask(e - 16));
+}
+
+// Zero ring bytes of output [O0, O1) (bytes below O0 in the first dword are kept).
+__device__ __forceinline__ void zero_span(Smem &s, const Ctx &c, int32_t O0, int32_t O1) {
+    const int l = lane_id();
+    const uint32_t a = slot(c, O0), h = a & 3u;
+    const int32_t A = O0 + (int32_t)((4u - h) & 3u);  // first dword-aligned position >= O0
+    if (l == 0 && h)
+        __hip_atomic_fetch_and(reinterpret_cast<uint32_t *>(s.ring) + (a >> 2), lomask((int32_t)h), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+    for (int32_t x = A + 4 * l; x < O1; x += 256) *(uint32_t *)(s.ring + slot(c, x)) = 0u;
 }
 
 // Copy m (1..16) bytes from LDS source byte address sa to ring slot da.
@@ -503,8 +503,11 @@ __device__ __forceinline__ uint32_t pick5(int32_t q, uint32_t a, uint32_t b, uin
 // output [O0, O1), O1 - O0 <= BSPAN, every ll/ml <= LMAX.
 __device__ __forceinline__ void batch(Smem &s, Ctx &c, bool act, int32_t o, uint32_t ll, uint32_t ml, uint32_t off,
                                       uint32_t litr, int32_t O0, int32_t O1 PROF_ARG) {
-    const int32_t hz = O1 - R;  // sources below hz come from HBM
+    // sources below hz come from HBM: the ring slots of [hz, O1) are intact
+    // (zero_span may clear up to 3 bytes past O1, i.e. the slots of O1 - R ..)
+    const int32_t hz = O1 + 4 - R;
     if (O0 - c.F >= FLUSH_T) flush_to_line(s, c, O0);
+    zero_span(s, c, O0, O1);
     const int32_t ms = o + (int32_t)ll, msrc = ms - (int32_t)off;
     const bool hasm = act && ml > 0;
     const bool zero = hasm && off == 0;
@@ -529,10 +532,10 @@ __device__ __forceinline__ void batch(Smem &s, Ctx &c, bool act, int32_t o, uint
         }
     }
     PSTAMP(4);
-    // far matches (and offset-0 matches, which write zeros)
-    if (__ballot(far || zero)) {
-        for (uint32_t k = 0; __ballot((far || zero) && k < ml); k += 16) {
-            if ((far || zero) && k < ml) {
+    // far matches (offset-0 matches write zeros: the span is already zero)
+    if (__ballot(far)) {
+        for (uint32_t k = 0; __ballot(far && k < ml); k += 16) {
+            if (far && k < ml) {
                 const int32_t m = ml - k < 16u ? (int32_t)(ml - k) : 16;
                 const uint32_t da = slot(c, ms + (int32_t)k);
                 uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0, w4 = 0;
