@@ -1,0 +1,36 @@
+"""HBM traffic per launch of one kernel from two rocprofv3 --pmc passes
+(FETCH_SIZE, WRITE_SIZE; KiB per dispatch), with the gfx950 FETCH_SIZE
+correction of MI355X_MICROARCH.md (HBM/rocprofv3 section).
+usage: traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> <kernel-substr> <blocks> <block_bytes> [out.json]"""
+import csv
+import json
+import sys
+
+
+def per_dispatch(path, kname, counter):
+    vals = {}
+    for r in csv.DictReader(open(path)):
+        if kname in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+    if not vals:
+        raise SystemExit(f"no {counter} rows for {kname} in {path}")
+    return sum(vals.values()) / len(vals), len(vals)
+
+
+fpath, wpath, kname, nblk, bb = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4]), int(sys.argv[5])
+f_kb, nf = per_dispatch(fpath, kname, "FETCH_SIZE")
+w_kb, nw = per_dispatch(wpath, kname, "WRITE_SIZE")
+out = {
+    "blocks": nblk, "block_bytes": bb, "kernel": kname,
+    "fetch_size_kb": f_kb, "write_size_kb": w_kb, "dispatches": [nf, nw],
+    "hbm_bytes_raw": (f_kb + w_kb) * 1024.0,
+    "hbm_bytes_per_launch": (2.0 * f_kb + w_kb) * 1024.0,
+    "correction": "MI355X_MICROARCH.md: on gfx950 FETCH_SIZE reads 1/2 of wide coalesced stream bytes -> "
+                  "hbm = (2*FETCH_SIZE + WRITE_SIZE)*1024; the x2 is exact only for the 16-B staging loads, "
+                  "so true traffic lies between hbm_bytes_raw and hbm_bytes_per_launch",
+    "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes ({fpath}, {wpath})",
+}
+s = json.dumps(out, indent=1)
+print(s)
+if len(sys.argv) > 6:
+    open(sys.argv[6], "w").write(s + "\n")
