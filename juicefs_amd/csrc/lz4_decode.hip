@@ -39,7 +39,11 @@
 namespace jfs {
 namespace lz4d {
 
-constexpr int P = 64;                  // bytes per lane piece (visited set = one u64)
+#ifndef JFS_LZ4_P
+#define JFS_LZ4_P 32
+#endif
+constexpr int P = JFS_LZ4_P;           // bytes per lane piece (visited set = one u64)
+static_assert(P <= 64, "visited set is one u64");
 constexpr int CW = 64 * P;             // compressed window bytes handled per pass
 constexpr int CWIN = CW + 80;          // LDS staging incl. lookahead (multiple of 16)
 #ifndef JFS_LZ4_RING
@@ -86,13 +90,24 @@ struct Prof {
 #define PROF_PASS
 #endif
 
+// Published by the parser wave for each window it stages (double-buffered).
+enum { W_NONE = 0, W_WIN = 1, W_SER = 2, W_BUG = 3 };
+struct Meta {
+    int32_t kind, wbase, cbase;
+    uint32_t T, efin;
+};
+// Published by the copier wave after each pipeline step.
+struct Ctl {
+    int32_t done, restart, rip;
+};
+
 struct Smem {
     alignas(16) uint8_t ring[R];
-    alignas(16) uint8_t cwin[CWIN];
-    alignas(16) uint16_t tab[TMAX];  // token positions relative to cbase, stream order
-    };
-
-static_assert(__builtin_offsetof(Smem, cwin) == R, "literal sources are addressed as ring + R");
+    alignas(16) uint8_t cwin[2][CWIN];
+    alignas(16) uint16_t tab[2][TMAX];  // token positions relative to cbase, stream order
+    Meta meta[2];
+    Ctl ctl;
+};
 
 struct Ctx {
     const gc_u8 *src;
@@ -102,8 +117,11 @@ struct Ctx {
     int32_t F;      // ring flushed up to (output position)
     int32_t Fw;     // flushed and waited for (HBM loads below this are safe)
     uint32_t dmis;  // dst address mod 16 (ring slots mirror HBM alignment)
-    int32_t cbase;  // input position of cwin[0]
+    int32_t cbase;  // input position of cw[0]
     int32_t bug;    // set when an internal bound trips (kernel bug guard; never expected)
+    uint8_t *cw;    // staged window (one of Smem::cwin)
+    uint32_t cwoff; // its byte offset in Smem (LDS address of cw[0])
+    uint16_t *tab;  // its token table
 };
 
 __device__ __forceinline__ uint32_t slot(const Ctx &c, int32_t pos) { return (uint32_t)(pos + (int32_t)c.dmis) & RMASK; }
@@ -113,7 +131,7 @@ __device__ __forceinline__ uint32_t slot(const Ctx &c, int32_t pos) { return (ui
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t cb(const Smem &s, const Ctx &c, int32_t p) {
     int32_t r = p - c.cbase;
-    if ((uint32_t)r < (uint32_t)CWIN) return s.cwin[r];
+    if ((uint32_t)r < (uint32_t)CWIN) return c.cw[r];
     return (p >= 0 && p < c.n) ? c.src[p] : 0u;
 }
 
@@ -126,13 +144,13 @@ __device__ __forceinline__ void stage_window(Smem &s, Ctx &c, int32_t wbase) {
         int32_t p = c.cbase + 16 * k;
         uint4 v = make_uint4(0, 0, 0, 0);
         if (p < c.n) v = *(const gc_u4 *)(c.src + p);  // chunk holds at least one valid byte: same page
-        *(uint4 *)(s.cwin + 16 * k) = v;
+        *(uint4 *)(c.cw + 16 * k) = v;
     }
     // bytes outside [0, n) must read as 0 (they are never part of a fast-path token)
     if (c.cbase < 0 || c.cbase + CWIN > c.n) {
         for (int k = l; k < CWIN; k += 64) {
             int32_t p = c.cbase + k;
-            if (p >= c.n || p < 0) s.cwin[k] = 0;
+            if (p >= c.n || p < 0) c.cw[k] = 0;
         }
     }
 }
@@ -199,13 +217,13 @@ struct FTok {
     bool slow, stop;
 };
 
-__device__ __forceinline__ uint32_t w8(const Smem &s, int32_t r) { return s.cwin[r < CWIN - 1 ? r : CWIN - 1]; }
+__device__ __forceinline__ uint32_t w8(const Ctx &c, int32_t r) { return c.cw[r < CWIN - 1 ? r : CWIN - 1]; }
 
 __device__ __forceinline__ FTok parse_fast(const Smem &s, const Ctx &c, int32_t p) {
     FTok t;
     const int32_t n = c.n, b0 = c.cbase;
     const int32_t r = p - b0;
-    const uint32_t tb = w8(s, r), e1 = w8(s, r + 1);
+    const uint32_t tb = w8(c, r), e1 = w8(c, r + 1);
     const bool llx = (tb >> 4) == 15;
     int32_t q = r + 1 + (llx ? 1 : 0);
     t.ll = (tb >> 4) + (llx ? e1 : 0u);
@@ -215,7 +233,7 @@ __device__ __forceinline__ FTok parse_fast(const Smem &s, const Ctx &c, int32_t 
     t.lit = b0 + q;
     q += (int32_t)t.ll;
     slow |= q + 3 > CWIN;  // offset and the first match-length extension byte must be staged
-    const uint32_t o0 = w8(s, q), o1 = w8(s, q + 1), e2 = w8(s, q + 2);
+    const uint32_t o0 = w8(c, q), o1 = w8(c, q + 1), e2 = w8(c, q + 2);
     q += 2;
     const bool mlx = (tb & 15) == 15;
     t.ml = (tb & 15) + (mlx ? e2 : 0u) + 4;
@@ -528,7 +546,7 @@ __device__ __forceinline__ void batch(Smem &s, Ctx &c, bool act, int32_t o, uint
     for (uint32_t k = 0; __ballot(act && k < ll); k += 16) {
         if (act && k < ll) {
             const int32_t m = ll - k < 16u ? (int32_t)(ll - k) : 16;
-            copy16<false>(s, (uint32_t)R + litr + k, slot(c, o + (int32_t)k), m);
+            copy16<false>(s, c.cwoff + litr + k, slot(c, o + (int32_t)k), m);
         }
     }
     PSTAMP(4);
@@ -632,7 +650,7 @@ __device__ __forceinline__ uint32_t copy_tokens(Smem &s, Ctx &c, uint32_t T, int
     for (uint32_t g0 = 0; g0 < T; g0 += 64) {
         const uint32_t n0 = T - g0 < 64u ? T - g0 : 64u;
         const bool in0 = (uint32_t)l < n0;
-        const int32_t p = c.cbase + (in0 ? (int32_t)s.tab[g0 + l] : 0);
+        const int32_t p = c.cbase + (in0 ? (int32_t)c.tab[g0 + l] : 0);
         FTok t = parse_fast(s, c, p);
         const bool sl = in0 && t.slow;
         if (__ballot(sl)) {
@@ -704,12 +722,11 @@ __device__ __forceinline__ uint32_t step_next(const Smem &s, const Ctx &c, int32
 }
 
 // ---------------------------------------------------------------------------
-// fast path: one window
+// parser wave: stage one window, find its true token chain, write the table
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void window(Smem &s, Ctx &c, Ser &st, int *stopped PROF_ARG) {
+__device__ __forceinline__ void parse_window(Smem &s, Ctx &c, int32_t wbase, uint32_t *T_out,
+                                             uint32_t *efin_out PROF_ARG) {
     const int l = lane_id();
-    const int32_t wbase = st.ip;
-    const int32_t op0 = st.op;
     stage_window(s, c, wbase);
     const int32_t cbase = c.cbase;
     __builtin_amdgcn_wave_barrier();
@@ -796,49 +813,172 @@ __device__ __forceinline__ void window(Smem &s, Ctx &c, Ser &st, int *stopped PR
             if (guard > P) { c.bug = 7; break; }
         }
     }
-    const uint32_t efin = readlane(ex, 63);
+    *efin_out = readlane(ex, 63);
     PSTAMP(1);
 
     // 3. token table: positions (relative to cbase) in stream order
     const uint32_t cnt = (uint32_t)__builtin_popcountll(vt);
     const uint32_t cinc = dpp_scan_add(cnt);
-    const uint32_t T = readlane(cinc, 63);
+    *T_out = readlane(cinc, 63);
     {
         uint32_t idx = cinc - cnt;
         uint64_t v = vt;
         while (__ballot(v != 0)) {
             if (v) {
                 const uint32_t b = (uint32_t)__builtin_ctzll(v);
-                s.tab[idx] = (uint16_t)((uint32_t)l * P + b);
+                c.tab[idx] = (uint16_t)((uint32_t)l * P + b);
                 idx++;
                 v &= v - 1;
             }
         }
     }
-    __builtin_amdgcn_wave_barrier();
     PSTAMP(2);
-
-    // 4. copy
-    int32_t end_op = op0, bad_ip = 0;
-    const uint32_t done = T > 0 ? copy_tokens(s, c, T, op0, &end_op, &bad_ip PROF_PASS) : 0u;
-    __builtin_amdgcn_wave_barrier();
-    PSTAMP(3);
-    if (done < T) {
-        st.ip = bad_ip;
-        *stopped = 1;
-    } else {
-        st.ip = (int32_t)(efin & ~STOP);
-        *stopped = (efin & STOP) ? 1 : 0;
-    }
-    st.op = end_op;
 }
 
-__global__ __launch_bounds__(64) void lz4_decode_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
-                                                       int32_t *__restrict__ ret) {
+// LDS-only workgroup barrier between the parser and copier waves
+__device__ __forceinline__ void wg_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__device__ __forceinline__ void use_buffer(Smem &s, Ctx &c, int buf) {
+    c.cw = s.cwin[buf];
+    c.cwoff = (uint32_t)((const uint8_t *)s.cwin[buf] - (const uint8_t *)&s);
+    c.tab = s.tab[buf];
+}
+
+// Pipeline: in step k the parser stages and parses window k into buffer k&1
+// while the copier copies window k-1 from the other buffer; two barriers per
+// step.  When the copier has to take tokens exactly (a stop token, an
+// output-side check, the end of the block) it runs the serial restatement
+// and, if the fast path applies again, restarts the parser at the new input
+// position (the window the parser produced meanwhile is skipped).
+__device__ __forceinline__ void parser_wave(Smem &s, Ctx &c PROF_ARG) {
+    int32_t pip = 0;
+    bool pstop = false;
+    for (uint32_t k = 0;; ++k) {
+        const int buf = (int)(k & 1u);
+        Meta m;
+        m.kind = W_NONE;
+        m.wbase = pip;
+        m.cbase = 0;
+        m.T = 0;
+        m.efin = 0;
+        if (!pstop) {
+            if (pip < c.n - 64) {
+                use_buffer(s, c, buf);
+                uint32_t T, efin;
+                parse_window(s, c, pip, &T, &efin PROF_PASS);
+                m.kind = c.bug ? W_BUG : W_WIN;
+                m.cbase = c.cbase;
+                m.T = T;
+                m.efin = efin;
+                if ((efin & STOP) || c.bug) pstop = true;
+                else pip = (int32_t)efin;
+            } else {
+                m.kind = W_SER;
+                pstop = true;
+            }
+        }
+        if (lane_id() == 0) s.meta[buf] = m;
+        wg_sync();
+        const int32_t done = (int32_t)uniform((uint32_t)s.ctl.done), restart = (int32_t)uniform((uint32_t)s.ctl.restart),
+                      rip = (int32_t)uniform((uint32_t)s.ctl.rip);
+        wg_sync();
+        PSTAMP(9);
+        if (done) break;
+        if (restart) {
+            pip = rip;
+            pstop = false;
+        }
+    }
+}
+
+__device__ __forceinline__ void copier_wave(Smem &s, Ctx &c, int32_t *retp PROF_ARG) {
+    Ser st;
+    st.ip = 0;
+    st.op = 0;
+    st.fast = c.cap >= 64;
+    st.ret = 0;
+    bool skip = false;
+    int32_t result = INT32_MIN;
+    int64_t nser = 0;
+    for (uint32_t k = 0;; ++k) {
+        int32_t done = 0, restart = 0, rip = 0;
+        if (k > 0 && !skip) {
+            const int buf = (int)((k - 1) & 1u);
+            Meta m;
+            m.kind = (int32_t)uniform((uint32_t)s.meta[buf].kind);
+            m.wbase = (int32_t)uniform((uint32_t)s.meta[buf].wbase);
+            m.cbase = (int32_t)uniform((uint32_t)s.meta[buf].cbase);
+            m.T = uniform(s.meta[buf].T);
+            m.efin = uniform(s.meta[buf].efin);
+            bool ser = false;
+            if (m.kind == W_BUG || m.kind == W_NONE || m.wbase != st.ip) {
+                c.bug |= 8;
+            } else if (m.kind == W_WIN && st.fast && st.ip < c.n - 64 && st.op < c.cap - 128) {
+                use_buffer(s, c, buf);
+                c.cbase = m.cbase;
+                int32_t end_op = st.op, bad_ip = 0;
+                const uint32_t dn = m.T > 0 ? copy_tokens(s, c, m.T, st.op, &end_op, &bad_ip PROF_PASS) : 0u;
+                st.op = end_op;
+                if (dn < m.T) {
+                    st.ip = bad_ip;
+                    ser = true;
+                } else {
+                    st.ip = (int32_t)(m.efin & ~STOP);
+                    ser = (m.efin & STOP) != 0;
+                }
+            } else {
+                ser = true;  // W_SER, or the window's start is not fast-path eligible
+            }
+            if (ser && !c.bug) {
+                // tokens the fast path declines: exact, wave-uniform liblz4 1.9.3 steps
+                c.cbase = 0x3fffffff;  // no staged window describes st.ip
+                for (;;) {
+                    const int status = ser_seq(s, c, st);
+                    if (status != SER_CONT) {
+                        if (status == SER_DONE) flush(s, c, st.op);
+                        result = st.ret;
+                        done = 1;
+                        break;
+                    }
+                    if (++nser > (int64_t)c.n + 64) { c.bug |= 16; break; }
+                    if (st.fast && st.ip < c.n - 64 && st.op < c.cap - 128) {
+                        restart = 1;
+                        rip = st.ip;
+                        break;
+                    }
+                }
+                PSTAMP(8);
+            }
+            if (c.bug) {
+                done = 1;
+                restart = 0;
+                result = INT32_MIN;
+            }
+        }
+        if (k > (uint32_t)c.n + 64) {  // every step consumes input or finishes the block
+            done = 1;
+            result = INT32_MIN;
+        }
+        if (lane_id() == 0) {
+            s.ctl.done = done;
+            s.ctl.restart = restart;
+            s.ctl.rip = rip;
+        }
+        wg_sync();
+        wg_sync();
+        PSTAMP(9);
+        if (done) break;
+        skip = restart != 0;
+    }
+    if (lane_id() == 0) *retp = result;
+}
+
+__global__ __launch_bounds__(128) void lz4_decode_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
+                                                        int32_t *__restrict__ ret) {
     __shared__ Smem s;
     const int b = blockIdx.x;
     if (b >= nblk) return;
-    const int l = lane_id();
+    const int wave = (int)uniform(threadIdx.x >> 6);
     jfs_dev_block d = ((const gc_blk *)blocks)[b];
     Ctx c;
     c.src = (const gc_u8 *)d.src;
@@ -850,50 +990,24 @@ __global__ __launch_bounds__(64) void lz4_decode_kernel(const jfs_dev_block *__r
     c.dmis = (uint32_t)((uintptr_t)d.dst & 15u);
     c.cbase = 0x3fffffff;
     c.bug = 0;
-    int32_t result;
+    use_buffer(s, c, 0);
 #ifdef JFS_PROF
     Prof pr;
     pr.start();
 #endif
-    (void)l;
-    if (d.src == nullptr || c.n < 0 || c.cap < 0) {
-        result = -1;
-    } else if (c.cap == 0) {
-        result = (c.n == 1 && c.src[0] == 0) ? 0 : -1;
-    } else if (c.n == 0) {
-        result = -1;
-    } else {
-        Ser st;
-        st.ip = 0;
-        st.op = 0;
-        st.fast = c.cap >= 64;
-        st.ret = 0;
-        int status = SER_CONT;
-        for (int64_t guard = 0;; ++guard) {
-            if (c.bug || guard > (int64_t)c.n + 64) { status = SER_ERR; st.ret = INT32_MIN; c.bug |= 1; break; }
-            int32_t ip_before = st.ip;
-            if (st.fast && st.ip < c.n - 64 && st.op < c.cap - 128) {
-                int stopped = 0;
-                window(s, c, st, &stopped PROF_PASS);
-                if (st.ip <= ip_before && !stopped) { c.bug = 2; continue; }
-                if (!stopped) continue;
-            }
-            // the token at st.ip is not a fast-path token: take it exactly
-            c.cbase = 0x3fffffff;  // staged window no longer describes st.ip
-            status = ser_seq(s, c, st);
-            PSTAMP(8);
-            if (status != SER_CONT) break;
-        }
-        if (status == SER_DONE) {
-            flush(s, c, st.op);
-            result = st.ret;
-        } else {
-            result = st.ret;
-        }
+    // inputs that never reach the decode loop (no barrier: both waves return)
+    int32_t early = 1, result = 0;
+    if (d.src == nullptr || c.n < 0 || c.cap < 0) result = -1;
+    else if (c.cap == 0) result = (c.n == 1 && c.src[0] == 0) ? 0 : -1;
+    else if (c.n == 0) result = -1;
+    else early = 0;
+    if (early) {
+        if (wave == 1 && lane_id() == 0) ret[b] = result;
+        return;
     }
-    if (lane_id() == 0) ret[b] = result;
+    if (wave == 0) parser_wave(s, c PROF_PASS);
+    else copier_wave(s, c, ret + b PROF_PASS);
 #ifdef JFS_PROF
-    pr.stamp(9);
     pr.flush_out();
 #endif
 }
@@ -913,6 +1027,6 @@ extern "C" int jfs_prof_reset() {
 
 extern "C" int jfs_launch_lz4_decode(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, hipStream_t stream) {
     if (nblk <= 0) return 0;
-    hipLaunchKernelGGL(jfs::lz4d::lz4_decode_kernel, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, d_ret);
+    hipLaunchKernelGGL(jfs::lz4d::lz4_decode_kernel, dim3(nblk), dim3(128), 0, stream, d_blocks, nblk, d_ret);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
