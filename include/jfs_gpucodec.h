@@ -40,7 +40,7 @@ extern "C" {
 #define JFS_ERR_EMPTY_INPUT (JFS_ERR_BASE - 2)   /* "decompress an empty input"   compress.go:122 / zstd ErrEmptySlice */
 #define JFS_ERR_CORRUPT (JFS_ERR_BASE - 3)       /* malformed Zstd frame (ZSTD_decompress error) */
 #define JFS_ERR_COMPRESS_FAIL (JFS_ERR_BASE - 4) /* LZ4_compress_default returned 0 */
-#define JFS_ERR_UNSUPPORTED (JFS_ERR_BASE - 5)   /* operation not available (e.g. Zstd encode on GPU) */
+#define JFS_ERR_UNSUPPORTED (JFS_ERR_BASE - 5)   /* operation not available in this build */
 #define JFS_ERR_NO_DEVICE (JFS_ERR_BASE - 6)     /* no usable gfx950 device; the library never falls back to CPU */
 #define JFS_ERR_INVALID (JFS_ERR_BASE - 7)       /* bad argument (unknown algo, negative size, ...) */
 #define JFS_ERR_HIP (JFS_ERR_BASE - 8)           /* HIP runtime failure */
@@ -63,7 +63,10 @@ int64_t jfs_compress_bound(int algo, int64_t n);
  * dst_cap is len(dst) for LZ4/none and cap(dst) for Zstd (DataDog/zstd writes
  * into dst[:cap]; compress.go:83-89).  LZ4 output is byte-identical to
  * LZ4_compress_default; a dst smaller than the compressed size fails
- * (JFS_ERR_COMPRESS_FAIL), like lz4.CompressDefault returning 0. */
+ * (JFS_ERR_COMPRESS_FAIL), like lz4.CompressDefault returning 0.  Zstd: one
+ * RFC 8878 frame (FCS present, no checksum), never larger than
+ * CompressBound; dst_cap < CompressBound(n) -> JFS_ERR_SHORT_BUFFER, the
+ * "buffer too short" of compress.go:86-89. */
 int64_t jfs_compress(int algo, uint8_t *dst, int64_t dst_cap, const uint8_t *src, int64_t n);
 
 /* Decompress(dst, src) -> bytes written (>=0) or <0.
@@ -104,6 +107,9 @@ typedef struct jfs_dev_block {
 int64_t jfs_lz4_decompress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream);
 int64_t jfs_lz4_compress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream);
 int64_t jfs_zstd_decompress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream);
+/* Zstd frame per block; ret[i] = frame size, or -2 when dst_cap < CompressBound(src_len).
+ * Synchronous with respect to `stream` (it uses per-device scratch). */
+int64_t jfs_zstd_compress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream);
 
 /* ---- Runtime / utilities ------------------------------------------------- */
 

@@ -28,7 +28,7 @@ JFS_ERR_HIP = JFS_ERR_BASE - 8
 EXPORTS = [
     "jfs_codec_from_name", "jfs_codec_name", "jfs_compress_bound", "jfs_compress", "jfs_decompress",
     "jfs_compress_batch", "jfs_decompress_batch", "jfs_lz4_decompress_device", "jfs_lz4_compress_device",
-    "jfs_zstd_decompress_device", "jfs_device_count", "jfs_version", "jfs_gen_blocks_device",
+    "jfs_zstd_decompress_device", "jfs_zstd_compress_device", "jfs_device_count", "jfs_version", "jfs_gen_blocks_device",
     "jfs_gen_block_host",
 ]
 
@@ -67,7 +67,8 @@ def load() -> ctypes.CDLL:
     for f in (lib.jfs_compress_batch, lib.jfs_decompress_batch):
         f.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(JfsIov), ctypes.POINTER(i64), u32]
         f.restype = i64
-    for f in (lib.jfs_lz4_decompress_device, lib.jfs_lz4_compress_device, lib.jfs_zstd_decompress_device):
+    for f in (lib.jfs_lz4_decompress_device, lib.jfs_lz4_compress_device, lib.jfs_zstd_decompress_device,
+              lib.jfs_zstd_compress_device):
         f.argtypes = [vp, ctypes.c_int, vp, vp]
         f.restype = i64
     lib.jfs_device_count.argtypes = []

@@ -127,6 +127,7 @@ int64_t finish_result(int algo, int dir, int32_t raw) {
     }
     if (algo == JFS_ALGO_ZSTD) {
         if (raw >= 0) return raw;
+        if (dir == COMPRESS) return raw == -2 ? JFS_ERR_SHORT_BUFFER : JFS_ERR_COMPRESS_FAIL;
         if (raw == -2) return JFS_ERR_SHORT_BUFFER;
         return JFS_ERR_CORRUPT;
     }
@@ -156,6 +157,7 @@ int64_t run_batch(DevCtx *dev, int algo, int dir, int nblk, const jfs_iov *iov, 
             // cap(dst) < hint: DataDog decodes into a new hint-sized buffer
             cap = std::max<int64_t>(cap, zstd_size_hint(iov[i].src, iov[i].src_len));
         }
+        if (algo == JFS_ALGO_ZSTD && dir == COMPRESS) cap = std::min<int64_t>(cap, jfs_compress_bound(JFS_ALGO_ZSTD, iov[i].src_len));
         tout += align16(std::max<int64_t>(cap, 0));
     }
     int64_t desc_bytes = align16((int64_t)nblk * (int64_t)sizeof(jfs_dev_block));
@@ -179,6 +181,7 @@ int64_t run_batch(DevCtx *dev, int algo, int dir, int nblk, const jfs_iov *iov, 
             cap = std::min<int64_t>(cap, iov[i].src_len + iov[i].src_len / 255 + 16);
         if (algo == JFS_ALGO_ZSTD && dir == DECOMPRESS)
             cap = std::max<int64_t>(cap, zstd_size_hint(iov[i].src, iov[i].src_len));
+        if (algo == JFS_ALGO_ZSTD && dir == COMPRESS) cap = std::min<int64_t>(cap, jfs_compress_bound(JFS_ALGO_ZSTD, iov[i].src_len));
         h_desc[i].dst_cap = (int32_t)std::min<int64_t>(cap, INT32_MAX);
     }
     hipStream_t st = dev->stream;
@@ -190,6 +193,7 @@ int64_t run_batch(DevCtx *dev, int algo, int dir, int nblk, const jfs_iov *iov, 
     if (algo == JFS_ALGO_LZ4 && dir == DECOMPRESS) rc = jfs_launch_lz4_decode(d_desc, nblk, d_ret, st);
     else if (algo == JFS_ALGO_LZ4 && dir == COMPRESS) rc = jfs_launch_lz4_encode(d_desc, nblk, d_ret, st);
     else if (algo == JFS_ALGO_ZSTD && dir == DECOMPRESS) rc = jfs_launch_zstd_decode(d_desc, nblk, d_ret, nullptr, st);
+    else if (algo == JFS_ALGO_ZSTD && dir == COMPRESS) rc = jfs_launch_zstd_encode(d_desc, nblk, d_ret, st);
     else return JFS_ERR_UNSUPPORTED;
     if (rc != 0) return JFS_ERR_HIP;
     if (hipMemcpyAsync(h_ret, d_ret, (size_t)nblk * 4, hipMemcpyDeviceToHost, st) != hipSuccess) return JFS_ERR_HIP;
@@ -298,7 +302,10 @@ bool pre_answer(int algo, int dir, const jfs_iov &v, int64_t *res) {
     if (v.src_len < 0 || v.dst_cap < 0) { *res = JFS_ERR_INVALID; return true; }
     if (dir == DECOMPRESS && v.src_len == 0) { *res = JFS_ERR_EMPTY_INPUT; return true; }  // compress.go:121, ErrEmptySlice
     if (algo == JFS_ALGO_LZ4 && dir == COMPRESS && v.src_len > LZ4_MAX_INPUT) { *res = JFS_ERR_COMPRESS_FAIL; return true; }
-    if (algo == JFS_ALGO_ZSTD && dir == COMPRESS) { *res = JFS_ERR_UNSUPPORTED; return true; }
+    if (algo == JFS_ALGO_ZSTD && dir == COMPRESS && v.dst_cap < jfs_compress_bound(JFS_ALGO_ZSTD, v.src_len)) {
+        *res = JFS_ERR_SHORT_BUFFER;  // compress.go:86-89 (DataDog checks cap(dst) against CompressBound)
+        return true;
+    }
     return false;
 }
 
@@ -425,6 +432,11 @@ int64_t jfs_lz4_decompress_device(const jfs_dev_block *d_blocks, int nblk, int32
 int64_t jfs_lz4_compress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream) {
     if (devices().empty()) return JFS_ERR_NO_DEVICE;
     return jfs_launch_lz4_encode(d_blocks, nblk, d_ret, (hipStream_t)stream) == 0 ? JFS_OK : JFS_ERR_HIP;
+}
+
+int64_t jfs_zstd_compress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream) {
+    if (devices().empty()) return JFS_ERR_NO_DEVICE;
+    return jfs_launch_zstd_encode(d_blocks, nblk, d_ret, (hipStream_t)stream) == 0 ? JFS_OK : JFS_ERR_HIP;
 }
 
 int64_t jfs_zstd_decompress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream) {

@@ -59,6 +59,12 @@ def zstd_decompress(desc: torch.Tensor, ret: torch.Tensor, stream=None):
            "jfs_zstd_decompress_device")
 
 
+def zstd_compress(desc: torch.Tensor, ret: torch.Tensor, stream=None):
+    n = desc.numel() // DESC_DTYPE.itemsize
+    _check(L.load().jfs_zstd_compress_device(desc.data_ptr(), n, ret.data_ptr(), _stream_ptr(stream)),
+           "jfs_zstd_compress_device")
+
+
 def gen_blocks(out: torch.Tensor, nblk: int, block_bytes: int, cls: str, seed_base: int, stream=None):
     """Fill out[0 : nblk*block_bytes] with synthetic blocks."""
     assert out.numel() >= nblk * block_bytes
