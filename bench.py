@@ -53,6 +53,8 @@ def parse():
     p.add_argument("--level", type=int, default=3, help="zstd level of the generated frames")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--host-path", action="store_true", help="also time the PCIe-inclusive batch path (extra launches)")
+    p.add_argument("--no-extras", action="store_true", help="skip the compress-side measurements")
+    p.add_argument("--extra-blocks", type=int, default=1024, help="blocks in the Zstd compress sample")
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="wall budget per CPU baseline leg")
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
     return p.parse_args()
@@ -311,6 +313,20 @@ def main():
                 lb = libzstd_baseline(comp_blocks, U, a.cpu_seconds / 2)
                 if lb:
                     out["cpu_libzstd"] = lb
+        if not a.no_extras:
+            ex = {}
+            if a.codec == "lz4":
+                ex["lz4_compress"] = {"value": nblk * U / (batch.enc_ms / 1e3) / 2**30, "unit": "GiB/s",
+                                      "kernel_ms": batch.enc_ms, "blocks": nblk,
+                                      "note": "one GPU LZ4 encode launch (byte-identical to LZ4_compress_default)"}
+            try:
+                zr, zratio, zms = D.zstd_compress_rate(min(a.extra_blocks, nblk), U, a.cls, seed_base=7, device=dev)
+                ex["zstd_compress"] = {"value": zr, "unit": "GiB/s", "ratio": zratio, "kernel_ms": zms,
+                                       "blocks": min(a.extra_blocks, nblk),
+                                       "note": "one GPU Zstd encode launch; frames verified by the GPU decoder"}
+            except Exception as e:  # report, never fake
+                ex["zstd_compress"] = {"error": str(e)}
+            out["compress"] = ex
         if a.host_path and a.codec == "lz4":
             try:
                 out["host_path"] = host_path_rate(comp_blocks * 8, U)

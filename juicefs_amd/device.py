@@ -94,8 +94,12 @@ class Lz4Batch:
         offs = np.arange(nblk, dtype=np.int64)
         self.enc_desc = make_desc(self.raw, offs * block_bytes, [block_bytes] * nblk, self.comp, offs * self.slot,
                                   [self.slot] * nblk)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
         lz4_compress(self.enc_desc, self.ret)
+        e1.record()
         torch.cuda.synchronize()
+        self.enc_ms = e0.elapsed_time(e1)  # one GPU LZ4 encode launch over the whole batch
         self.csize = self.ret.cpu().numpy().astype(np.int64)
         if (self.csize <= 0).any():
             raise RuntimeError("device LZ4 compression failed")
@@ -115,6 +119,41 @@ class Lz4Batch:
         torch.cuda.synchronize()
         ok = bool((self.dec_ret == self.U).all().item())
         return ok and bool(torch.equal(self.out, self.raw))
+
+
+def zstd_bound(n: int) -> int:
+    return n + (n >> 8) + (((128 << 10) - n) >> 11 if n < (128 << 10) else 0)
+
+
+def zstd_compress_rate(nblk: int, block_bytes: int, cls: str = "T", seed_base: int = 1, device="cuda"):
+    """Time one GPU Zstd encode launch over nblk synthetic blocks in HBM and
+    check every frame with the GPU decoder.  Returns (GiB/s, ratio, ms)."""
+    dev = torch.device(device)
+    raw = torch.empty(nblk * block_bytes, dtype=torch.uint8, device=dev)
+    gen_blocks(raw, nblk, block_bytes, cls, seed_base)
+    slot = (zstd_bound(block_bytes) + 255) // 256 * 256
+    comp = torch.empty(nblk * slot, dtype=torch.uint8, device=dev)
+    offs = np.arange(nblk, dtype=np.int64)
+    desc = make_desc(raw, offs * block_bytes, [block_bytes] * nblk, comp, offs * slot, [slot] * nblk)
+    ret = torch.empty(nblk, dtype=torch.int32, device=dev)
+    zstd_compress(desc, ret)  # warm-up (scratch allocation)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    zstd_compress(desc, ret)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1)
+    csize = ret.cpu().numpy().astype(np.int64)
+    if (csize <= 0).any():
+        raise RuntimeError("device Zstd compression failed")
+    out = torch.empty(nblk * block_bytes, dtype=torch.uint8, device=dev)
+    ddesc = make_desc(comp, offs * slot, csize, out, offs * block_bytes, [block_bytes] * nblk)
+    dret = torch.empty(nblk, dtype=torch.int32, device=dev)
+    zstd_decompress(ddesc, dret)
+    torch.cuda.synchronize()
+    if not (bool((dret == block_bytes).all().item()) and torch.equal(out, raw)):
+        raise RuntimeError("Zstd round trip mismatch")
+    return nblk * block_bytes / (ms / 1e3) / 2**30, nblk * block_bytes / float(csize.sum()), ms
 
 
 def _libzstd():
