@@ -202,3 +202,35 @@ def test_lz4_device_resident_roundtrip(gpu, oracle):
     assert (ret == b.U).all()
     for i in range(24):
         assert torch.equal(out[offs_d[i]:offs_d[i] + b.U], b.raw[i * b.U:(i + 1) * b.U])
+
+
+def _dense_tokens(seed, ntok):
+    """A valid LZ4 block made of 3..5-byte sequences (more tokens per input
+    window than the per-window table holds): exercises windows that end at the
+    table capacity and restart at the next token."""
+    rng = random.Random(seed)
+    out = bytearray([0x80]) + bytes(rng.randrange(256) for _ in range(8)) + (rng.randrange(1, 9)).to_bytes(2, "little")
+    for _ in range(ntok):
+        k = rng.randrange(10)
+        if k < 6:      # ll 0, ml 4: 3 bytes
+            out += bytes([0x00]) + rng.randrange(1, 9).to_bytes(2, "little")
+        elif k < 8:    # ll 1, ml 5: 4 bytes
+            out += bytes([0x11, rng.randrange(256)]) + rng.randrange(1, 9).to_bytes(2, "little")
+        else:          # ll 0, ml 15+4+e: 4 bytes
+            out += bytes([0x0F]) + rng.randrange(1, 9).to_bytes(2, "little") + bytes([rng.randrange(0, 40)])
+    out += bytes([0xF0, 1]) + bytes(rng.randrange(256) for _ in range(16))
+    return bytes(out)
+
+
+def test_lz4_decode_dense_tokens(gpu, oracle):
+    c = C.LZ4()
+    comps = [_dense_tokens(70 + i, n) for i, n in enumerate((10, 700, 5000, 60000, 250000))]
+    pairs, want = [], []
+    for comp in comps:
+        r, out = oracle.lz4_decompress(comp, 8 << 20)
+        assert r > 0
+        pairs.append((bytearray(r), comp))
+        want.append((r, out[:r]))
+    res = c.DecompressBatch(pairs)
+    for (dst, _), (r, out), (n, err) in zip(pairs, want, res):
+        assert err is None and n == r and bytes(dst[:n]) == out
