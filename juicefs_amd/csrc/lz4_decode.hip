@@ -51,6 +51,10 @@ constexpr int CWIN = CW + 80;          // LDS staging incl. lookahead (multiple 
 #endif
 constexpr int R = JFS_LZ4_RING;        // output ring bytes (power of two)
 constexpr int RMASK = R - 1;
+#ifndef JFS_LZ4_OV
+#define JFS_LZ4_OV 32
+#endif
+constexpr int OV = JFS_LZ4_OV;           // speculative-walk pre-roll (bytes before the piece)
 constexpr int TMAX = CW / 3 + 2;       // max tokens in a window (interior token >= 3 bytes)
 // Table capacity per window.  Windows with more tokens (only runs of 3..5-byte
 // tokens) end at token TCAP and the next window starts there; the cap keeps the
@@ -70,7 +74,7 @@ static_assert(R - BSPAN >= LMAX + 16, "far sources must lie below the flushed pr
 
 #ifdef JFS_PROF
 // diagnostic build only: per-phase cycle sums (s_memtime), never in the product .so
-#define NPROF 10
+#define NPROF 16  // 0..9 phase cycles, 10..15 event counts
 __device__ uint64_t g_prof[NPROF];
 struct Prof {
     uint64_t t, acc[NPROF];
@@ -89,10 +93,12 @@ struct Prof {
     }
 };
 #define PSTAMP(k) pr.stamp(k)
+#define PCOUNT(k, n) (pr.acc[k] += (n))
 #define PROF_ARG , Prof &pr
 #define PROF_PASS , pr
 #else
 #define PSTAMP(k)
+#define PCOUNT(k, n)
 #define PROF_ARG
 #define PROF_PASS
 #endif
@@ -531,6 +537,7 @@ __device__ __forceinline__ void batch(Smem &s, Ctx &c, bool act, int32_t o, uint
     // sources below hz come from HBM: the ring slots of [hz, O1) are intact
     // (zero_span may clear up to 3 bytes past O1, i.e. the slots of O1 - R ..)
     const int32_t hz = O1 + 4 - R;
+    PCOUNT(14, 1);
     if (O0 - c.F >= FLUSH_T) flush_to_line(s, c, O0);
     zero_span(s, c, O0, O1);
     const int32_t ms = o + (int32_t)ll, msrc = ms - (int32_t)off;
@@ -632,6 +639,7 @@ __device__ __forceinline__ void batch(Smem &s, Ctx &c, bool act, int32_t o, uint
         const int32_t front = (int32_t)dwave_min(pend ? (uint32_t)ms : 0x7FFFFFFFu);
         bool go = pend && send <= front;
         while (__ballot(go)) {
+            PCOUNT(15, 1);
             if (go) {
                 const int32_t m = rem < 16 ? (rem < D ? rem : D) : (D < 16 ? D : 16);
                 copy16<true>(s, slot(c, pos - D), slot(c, pos), m);
@@ -736,25 +744,30 @@ __device__ __forceinline__ void parse_window(Smem &s, Ctx &c, int32_t wbase, uin
     const int l = lane_id();
     stage_window(s, c, wbase);
     const int32_t cbase = c.cbase;
+    PCOUNT(10, 1);
     __builtin_amdgcn_wave_barrier();
     PSTAMP(0);
 
     // 1. speculative walk of this lane's piece: visited positions + exit
     const int32_t plo = cbase + l * P, phi = plo + P;
-    uint32_t cur = l == 0 ? (uint32_t)wbase : (uint32_t)plo;
+    // The walk starts OV bytes before the piece (a pre-roll whose positions are
+    // not recorded): by the time it reaches the piece it has usually fallen into
+    // the true chain, so few pieces need a second fix-up round.
+    uint32_t cur = l == 0 ? (uint32_t)wbase : (uint32_t)(plo - OV);
     uint64_t vs = 0;  // positions the speculative chain visited (bit = position - plo)
     uint32_t sx = 0;  // its exit: first position >= phi, or STOP | p
     {
         int32_t q = (int32_t)cur;
         bool act = true;
         for (int guard = 0; __ballot(act); ++guard) {
+            PCOUNT(11, 1);
             if (act) {
                 const uint32_t x = step_next(s, c, q, act);
                 if (x & STOP) {
                     sx = x;
                     act = false;
                 } else {
-                    vs |= 1ull << (uint32_t)(q - plo);
+                    if (q >= plo) vs |= 1ull << (uint32_t)(q - plo);
                     q = (int32_t)x;
                     if (q >= phi) {
                         sx = (uint32_t)q;
@@ -762,7 +775,7 @@ __device__ __forceinline__ void parse_window(Smem &s, Ctx &c, int32_t wbase, uin
                     }
                 }
             }
-            if (guard > P) { c.bug = 6; break; }
+            if (guard > P + OV) { c.bug = 6; break; }
         }
     }
     // 2. fix-up: true entry of piece k = exit of piece k-1.  An entry on the
@@ -775,6 +788,7 @@ __device__ __forceinline__ void parse_window(Smem &s, Ctx &c, int32_t wbase, uin
         const bool ch = In != cur;
         if (!__ballot(ch)) break;
         if (r > 64) { c.bug = 3; break; }
+        PCOUNT(12, 1);
         bool part = false;
         if (ch) {
             cur = In;
@@ -794,6 +808,7 @@ __device__ __forceinline__ void parse_window(Smem &s, Ctx &c, int32_t wbase, uin
         int32_t q = (int32_t)In;
         uint64_t vp = 0;
         for (int guard = 0; __ballot(part); ++guard) {
+            PCOUNT(13, 1);
             if (part) {
                 const uint32_t d = (uint32_t)(q - plo);
                 if ((vs >> d) & 1ull) {  // joined the speculative chain

@@ -88,19 +88,10 @@ __device__ __forceinline__ uint32_t dpp_scan_min(uint32_t v) {  // inclusive, id
     v = umin32(v, __builtin_amdgcn_update_dpp(~0u, v, 0x143, 0xC, 0xF, false));
     return v;
 }
-// value of lane l-1 (lane 0 gets `first`): row_shr:1 within each 16-lane row,
-// then patch the three row heads with v_readlane/v_writelane
+// value of lane l-1 (lane 0 gets `first`): one DPP wave_shr:1 (GFX9 DPP;
+// lane 0 has no source and keeps `old`)
 __device__ __forceinline__ uint32_t dpp_shift_up(uint32_t v, uint32_t first) {
-    uint32_t t = __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xF, 0xF, true);
-    const int l = (int)__lane_id();
-    uint32_t r15 = (uint32_t)__builtin_amdgcn_readlane((int)v, 15);
-    uint32_t r31 = (uint32_t)__builtin_amdgcn_readlane((int)v, 31);
-    uint32_t r47 = (uint32_t)__builtin_amdgcn_readlane((int)v, 47);
-    t = l == 16 ? r15 : t;
-    t = l == 32 ? r31 : t;
-    t = l == 48 ? r47 : t;
-    t = l == 0 ? first : t;
-    return t;
+    return __builtin_amdgcn_update_dpp(first, v, 0x138, 0xF, 0xF, false);
 }
 __device__ __forceinline__ uint32_t readlane(uint32_t v, int l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, l); }
 __device__ __forceinline__ uint32_t dwave_min(uint32_t v) { return readlane(dpp_scan_min(v), 63); }
