@@ -21,6 +21,8 @@ from __future__ import annotations
 
 import ctypes
 
+import numpy as np
+
 from . import _lib as L
 
 ZSTD_LEVEL = 1
@@ -48,10 +50,10 @@ def _addr(buf, writable: bool):
             raise ValueError("dst must be writable")
         c = (ctypes.c_char * n).from_buffer(mv)
     else:
-        if mv.readonly:
-            c = ctypes.create_string_buffer(bytes(mv), n)  # copy of read-only input
-        else:
-            c = (ctypes.c_char * n).from_buffer(mv)
+        if mv.readonly:  # read-only input (bytes): address it in place, no copy
+            a = np.frombuffer(mv, dtype=np.uint8)
+            return ctypes.c_void_p(a.ctypes.data), n, (mv, a)
+        c = (ctypes.c_char * n).from_buffer(mv)
     return ctypes.cast(c, ctypes.c_void_p), n, (mv, c)
 
 

@@ -10,13 +10,17 @@
 // at once, cmd/flags.go:133-139): single-block calls enqueue on a per-process
 // coalescer; one worker thread per device drains the queue, so calls that
 // arrive while a batch is running ride the next batch (no artificial delay).
-// Batches go host -> pinned staging -> HBM -> kernel -> HBM -> pinned -> host.
+// Batches go host -> pinned staging -> HBM -> kernel -> HBM -> pinned -> host,
+// pipelined in chunks over two streams (run_batch).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <mutex>
@@ -35,40 +39,50 @@ constexpr int64_t LZ4_MAX_INPUT = 0x7E000000;
 
 inline int64_t align16(int64_t x) { return (x + 15) & ~(int64_t)15; }
 
-struct DevCtx {
-    int id = -1;
-    hipStream_t stream = nullptr;
-    std::mutex mu;  // serialises use of the staging buffers below
-    uint8_t *h_pin = nullptr;
+// One pinned host + device staging area with its own kernel stream: chunk k
+// of a batch uses slot k % NSLOT, so chunk k+1's H2D and chunk k-1's D2H run
+// while chunk k's kernel runs (and kernels of neighbouring chunks overlap).
+constexpr int NSLOT = 3;
+struct Slot {
+    hipStream_t st = nullptr;  // this slot's kernels
+    hipEvent_t ev_in = nullptr, ev_k = nullptr, ev = nullptr;  // H2D done, kernel done, D2H done
+    uint8_t *h = nullptr;
     int64_t h_cap = 0;
-    uint8_t *d_buf = nullptr;
+    uint8_t *d = nullptr;
     int64_t d_cap = 0;
-    uint8_t *d_vocab = nullptr;
 
-    bool ensure(int64_t host_bytes, int64_t dev_bytes) {
-        (void)hipSetDevice(id);
-        if (host_bytes > h_cap) {
-            if (h_pin) (void)hipHostFree(h_pin);
-            int64_t c = std::max<int64_t>(host_bytes, h_cap * 2);
-            if (hipHostMalloc((void **)&h_pin, (size_t)c, hipHostMallocDefault) != hipSuccess) {
-                h_pin = nullptr;
+    bool ensure(int64_t bytes) {
+        const int64_t want = (bytes + (64ll << 20) - 1) & ~((64ll << 20) - 1);  // grow in 64 MiB steps
+        if (bytes > h_cap) {
+            if (h) (void)hipHostFree(h);
+            if (hipHostMalloc((void **)&h, (size_t)want, hipHostMallocDefault) != hipSuccess) {
+                h = nullptr;
                 h_cap = 0;
                 return false;
             }
-            h_cap = c;
+            h_cap = want;
         }
-        if (dev_bytes > d_cap) {
-            if (d_buf) (void)hipFree(d_buf);
-            int64_t c = std::max<int64_t>(dev_bytes, d_cap * 2);
-            if (hipMalloc((void **)&d_buf, (size_t)c) != hipSuccess) {
-                d_buf = nullptr;
+        if (bytes > d_cap) {
+            if (d) (void)hipFree(d);
+            if (hipMalloc((void **)&d, (size_t)want) != hipSuccess) {
+                d = nullptr;
                 d_cap = 0;
                 return false;
             }
-            d_cap = c;
+            d_cap = want;
         }
         return true;
     }
+};
+
+struct DevCtx {
+    int id = -1;
+    std::mutex mu;  // serialises use of the staging slots below
+    Slot slot[NSLOT];
+    // All H2D copies go on s_in and all D2H copies on s_out, ordered by events:
+    // a D2H waiting for its kernel must not hold up the next chunk's H2D.
+    hipStream_t s_in = nullptr, s_out = nullptr;
+    uint8_t *d_vocab = nullptr;
 };
 
 std::once_flag g_once;
@@ -84,7 +98,16 @@ void init_devices() {
         DevCtx *d = new DevCtx();
         d->id = i;
         (void)hipSetDevice(i);
-        if (hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking) != hipSuccess) {
+        bool ok = true;
+        ok = ok && hipStreamCreateWithFlags(&d->s_in, hipStreamNonBlocking) == hipSuccess;
+        ok = ok && hipStreamCreateWithFlags(&d->s_out, hipStreamNonBlocking) == hipSuccess;
+        for (Slot &sl : d->slot) {
+            ok = ok && hipStreamCreateWithFlags(&sl.st, hipStreamNonBlocking) == hipSuccess;
+            ok = ok && hipEventCreateWithFlags(&sl.ev_in, hipEventDisableTiming) == hipSuccess;
+            ok = ok && hipEventCreateWithFlags(&sl.ev_k, hipEventDisableTiming) == hipSuccess;
+            ok = ok && hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming) == hipSuccess;
+        }
+        if (!ok) {
             delete d;
             continue;
         }
@@ -134,82 +157,201 @@ int64_t finish_result(int algo, int dir, int32_t raw) {
     return JFS_ERR_INVALID;
 }
 
-// Run blocks [0,nblk) of iov on one device, synchronously.  Blocks that the
-// C-ABI answers without a kernel (empty input, noOp) are handled by the caller.
+// Staged output capacity of one block (what the kernel may write).
+int64_t staged_cap(int algo, int dir, const jfs_iov &v) {
+    int64_t cap = v.dst_cap;
+    // LZ4 compress: the kernel never writes at/after cap; stage at most the bound
+    if (algo == JFS_ALGO_LZ4 && dir == COMPRESS) cap = std::min<int64_t>(cap, v.src_len + v.src_len / 255 + 16);
+    // Zstd decompress, cap(dst) < hint: DataDog decodes into a new hint-sized buffer
+    if (algo == JFS_ALGO_ZSTD && dir == DECOMPRESS) cap = std::max<int64_t>(cap, zstd_size_hint(v.src, v.src_len));
+    if (algo == JFS_ALGO_ZSTD && dir == COMPRESS) cap = std::min<int64_t>(cap, jfs_compress_bound(JFS_ALGO_ZSTD, v.src_len));
+    return std::max<int64_t>(cap, 0);
+}
+
+// Host staging chunk (input + output bytes per pipeline stage); default 2 GiB,
+// JFS_HOST_CHUNK_MB overrides.  The decode kernel needs many blocks in flight
+// (one workgroup per block), so chunks stay large.
+int64_t chunk_limit() {
+    static int64_t v = [] {
+        const char *e = getenv("JFS_HOST_CHUNK_MB");
+        long long mb = e ? atoll(e) : 2048;
+        return (int64_t)std::max(mb, 16ll) << 20;
+    }();
+    return v;
+}
+
+// memcpy jobs spread over host threads (pageable <-> pinned is CPU-bound)
+struct CopyJob {
+    uint8_t *dst;
+    const uint8_t *src;
+    int64_t n;
+};
+void par_copy(std::vector<CopyJob> &jobs) {
+    int64_t total = 0;
+    for (const CopyJob &j : jobs) total += j.n;
+    int T = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
+    if (total < (16ll << 20) || T == 1) {
+        for (const CopyJob &j : jobs) memcpy(j.dst, j.src, (size_t)j.n);
+        return;
+    }
+    // cut into <= 8 MiB pieces, deal them out in byte-balanced stripes
+    constexpr int64_t PIECE = 8ll << 20;
+    std::vector<CopyJob> pc;
+    for (const CopyJob &j : jobs)
+        for (int64_t o = 0; o < j.n; o += PIECE) pc.push_back({j.dst + o, j.src + o, std::min(PIECE, j.n - o)});
+    std::atomic<size_t> next{0};
+    auto work = [&] {
+        for (size_t i; (i = next.fetch_add(1)) < pc.size();) memcpy(pc[i].dst, pc[i].src, (size_t)pc[i].n);
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < T; t++) th.emplace_back(work);
+    work();
+    for (auto &t : th) t.join();
+}
+
+// JFS_HOST_TRACE=1: per-chunk host timings on stderr (diagnostics)
+bool host_trace() {
+    static bool v = getenv("JFS_HOST_TRACE") != nullptr;
+    return v;
+}
+double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int launch_kernel(int algo, int dir, const jfs_dev_block *d_desc, int nblk, int32_t *d_ret, hipStream_t st) {
+    if (algo == JFS_ALGO_LZ4 && dir == DECOMPRESS) return jfs_launch_lz4_decode(d_desc, nblk, d_ret, st);
+    if (algo == JFS_ALGO_LZ4 && dir == COMPRESS) return jfs_launch_lz4_encode(d_desc, nblk, d_ret, st);
+    if (algo == JFS_ALGO_ZSTD && dir == DECOMPRESS) return jfs_launch_zstd_decode(d_desc, nblk, d_ret, nullptr, st);
+    if (algo == JFS_ALGO_ZSTD && dir == COMPRESS) return jfs_launch_zstd_encode(d_desc, nblk, d_ret, st);
+    return -1;
+}
+
+// Run blocks [0,nblk) of iov on one device; returns when every result is in
+// out[].  Blocks that the C-ABI answers without a kernel (empty input, noOp)
+// are handled by the caller.  The batch is cut into chunks of about
+// chunk_limit() staging bytes, pipelined over NSLOT (stream, pinned, HBM)
+// slots: host copy-in of chunk k (threads) | H2D k+1, kernel k, D2H k-1
+// (streams) | host copy-out of chunk k-NSLOT.
 int64_t run_batch(DevCtx *dev, int algo, int dir, int nblk, const jfs_iov *iov, int64_t *out) {
     if (nblk <= 0) return JFS_OK;
     std::lock_guard<std::mutex> lk(dev->mu);
     (void)hipSetDevice(dev->id);
-    // layout: [inputs][outputs][descs][rets]
-    std::vector<int64_t> in_off(nblk), out_off(nblk);
-    int64_t tin = 0, tout = 0;
-    for (int i = 0; i < nblk; i++) {
-        in_off[i] = tin;
-        tin += align16(iov[i].src_len);
-        out_off[i] = tout;
-        int64_t cap = iov[i].dst_cap;
-        if (algo == JFS_ALGO_LZ4 && dir == COMPRESS) {
-            // the kernel never writes at/after cap; stage the full bound so the
-            // result can be copied out exactly
-            cap = std::min<int64_t>(cap, iov[i].src_len + iov[i].src_len / 255 + 16);
+    std::vector<int64_t> cap(nblk), in_off(nblk), out_off(nblk);
+    struct Chunk {
+        int s, e, slot;
+        int64_t tin, tout;
+    };
+    std::vector<Chunk> ch;
+    {
+        const int64_t limit = chunk_limit();
+        int s = 0;
+        while (s < nblk) {
+            Chunk c{s, s, (int)(ch.size() % NSLOT), 0, 0};
+            while (c.e < nblk) {
+                const int64_t ci = staged_cap(algo, dir, iov[c.e]);
+                const int64_t ib = align16(iov[c.e].src_len), ob = align16(ci);
+                if (c.e > s && c.tin + c.tout + ib + ob > limit) break;
+                cap[c.e] = ci;
+                in_off[c.e] = c.tin;
+                out_off[c.e] = c.tout;
+                c.tin += ib;
+                c.tout += ob;
+                c.e++;
+            }
+            ch.push_back(c);
+            s = c.e;
         }
-        if (algo == JFS_ALGO_ZSTD && dir == DECOMPRESS) {
-            // cap(dst) < hint: DataDog decodes into a new hint-sized buffer
-            cap = std::max<int64_t>(cap, zstd_size_hint(iov[i].src, iov[i].src_len));
+    }
+    auto layout = [&](const Chunk &c, uint8_t *base, uint8_t **in, uint8_t **outp, jfs_dev_block **desc, int32_t **ret) {
+        const int64_t desc_bytes = align16((int64_t)(c.e - c.s) * (int64_t)sizeof(jfs_dev_block));
+        *in = base;
+        *outp = base + c.tin;
+        *desc = (jfs_dev_block *)(base + c.tin + c.tout);
+        *ret = (int32_t *)(base + c.tin + c.tout + desc_bytes);
+    };
+    auto chunk_bytes = [&](const Chunk &c) {
+        return c.tin + c.tout + align16((int64_t)(c.e - c.s) * (int64_t)sizeof(jfs_dev_block)) +
+               align16((int64_t)(c.e - c.s) * 4);
+    };
+    auto launch = [&](const Chunk &c) -> int64_t {
+        Slot &sl = dev->slot[c.slot];
+        if (!sl.ensure(chunk_bytes(c))) return JFS_ERR_HIP;
+        uint8_t *h_in, *h_out, *d_in, *d_out;
+        jfs_dev_block *h_desc, *d_desc;
+        int32_t *h_ret, *d_ret;
+        layout(c, sl.h, &h_in, &h_out, &h_desc, &h_ret);
+        layout(c, sl.d, &d_in, &d_out, &d_desc, &d_ret);
+        std::vector<CopyJob> jobs;
+        for (int i = c.s; i < c.e; i++) {
+            const int k = i - c.s;
+            if (iov[i].src_len > 0) jobs.push_back({h_in + in_off[i], iov[i].src, iov[i].src_len});
+            h_desc[k].src = d_in + in_off[i];
+            h_desc[k].dst = d_out + out_off[i];
+            h_desc[k].src_len = (int32_t)iov[i].src_len;
+            h_desc[k].dst_cap = (int32_t)std::min<int64_t>(cap[i], INT32_MAX);
         }
-        if (algo == JFS_ALGO_ZSTD && dir == COMPRESS) cap = std::min<int64_t>(cap, jfs_compress_bound(JFS_ALGO_ZSTD, iov[i].src_len));
-        tout += align16(std::max<int64_t>(cap, 0));
-    }
-    int64_t desc_bytes = align16((int64_t)nblk * (int64_t)sizeof(jfs_dev_block));
-    int64_t ret_bytes = align16((int64_t)nblk * 4);
-    int64_t host_bytes = tin + tout + desc_bytes + ret_bytes;
-    if (!dev->ensure(host_bytes, host_bytes)) return JFS_ERR_HIP;
-    uint8_t *h = dev->h_pin, *d = dev->d_buf;
-    uint8_t *h_in = h, *h_out = h + tin;
-    jfs_dev_block *h_desc = (jfs_dev_block *)(h + tin + tout);
-    int32_t *h_ret = (int32_t *)(h + tin + tout + desc_bytes);
-    uint8_t *d_in = d, *d_out = d + tin;
-    jfs_dev_block *d_desc = (jfs_dev_block *)(d + tin + tout);
-    int32_t *d_ret = (int32_t *)(d + tin + tout + desc_bytes);
-    for (int i = 0; i < nblk; i++) {
-        if (iov[i].src_len > 0) memcpy(h_in + in_off[i], iov[i].src, (size_t)iov[i].src_len);
-        h_desc[i].src = d_in + in_off[i];
-        h_desc[i].dst = d_out + out_off[i];
-        h_desc[i].src_len = (int32_t)iov[i].src_len;
-        int64_t cap = iov[i].dst_cap;
-        if (algo == JFS_ALGO_LZ4 && dir == COMPRESS)
-            cap = std::min<int64_t>(cap, iov[i].src_len + iov[i].src_len / 255 + 16);
-        if (algo == JFS_ALGO_ZSTD && dir == DECOMPRESS)
-            cap = std::max<int64_t>(cap, zstd_size_hint(iov[i].src, iov[i].src_len));
-        if (algo == JFS_ALGO_ZSTD && dir == COMPRESS) cap = std::min<int64_t>(cap, jfs_compress_bound(JFS_ALGO_ZSTD, iov[i].src_len));
-        h_desc[i].dst_cap = (int32_t)std::min<int64_t>(cap, INT32_MAX);
-    }
-    hipStream_t st = dev->stream;
-    if (hipMemcpyAsync(d_in, h_in, (size_t)tin, hipMemcpyHostToDevice, st) != hipSuccess) return JFS_ERR_HIP;
-    if (hipMemcpyAsync(d_desc, h_desc, (size_t)nblk * sizeof(jfs_dev_block), hipMemcpyHostToDevice, st) !=
-        hipSuccess)
-        return JFS_ERR_HIP;
-    int rc = -1;
-    if (algo == JFS_ALGO_LZ4 && dir == DECOMPRESS) rc = jfs_launch_lz4_decode(d_desc, nblk, d_ret, st);
-    else if (algo == JFS_ALGO_LZ4 && dir == COMPRESS) rc = jfs_launch_lz4_encode(d_desc, nblk, d_ret, st);
-    else if (algo == JFS_ALGO_ZSTD && dir == DECOMPRESS) rc = jfs_launch_zstd_decode(d_desc, nblk, d_ret, nullptr, st);
-    else if (algo == JFS_ALGO_ZSTD && dir == COMPRESS) rc = jfs_launch_zstd_encode(d_desc, nblk, d_ret, st);
-    else return JFS_ERR_UNSUPPORTED;
-    if (rc != 0) return JFS_ERR_HIP;
-    if (hipMemcpyAsync(h_ret, d_ret, (size_t)nblk * 4, hipMemcpyDeviceToHost, st) != hipSuccess) return JFS_ERR_HIP;
-    if (hipMemcpyAsync(h_out, d_out, (size_t)tout, hipMemcpyDeviceToHost, st) != hipSuccess) return JFS_ERR_HIP;
-    if (hipStreamSynchronize(st) != hipSuccess) return JFS_ERR_HIP;
-    for (int i = 0; i < nblk; i++) {
-        int64_t r = finish_result(algo, dir, h_ret[i]);
-        if (algo == JFS_ALGO_ZSTD && dir == DECOMPRESS && r > 0 &&
-            iov[i].dst_cap < zstd_size_hint(iov[i].src, iov[i].src_len)) {
-            // decoded into DataDog's own buffer: compress.go:99-101 "buffer too short"
-            r = JFS_ERR_SHORT_BUFFER;
+        const double t0 = host_trace() ? now_ms() : 0.0;
+        par_copy(jobs);
+        if (host_trace())
+            fprintf(stderr, "[jfs host] chunk %d-%d stage-in %.1f MiB %.2f ms\n", c.s, c.e, c.tin / 1048576.0, now_ms() - t0);
+        const int n = c.e - c.s;
+        if (algo != JFS_ALGO_LZ4 && algo != JFS_ALGO_ZSTD) return JFS_ERR_UNSUPPORTED;
+        if (hipMemcpyAsync(d_in, h_in, (size_t)c.tin, hipMemcpyHostToDevice, dev->s_in) != hipSuccess) return JFS_ERR_HIP;
+        if (hipMemcpyAsync(d_desc, h_desc, (size_t)n * sizeof(jfs_dev_block), hipMemcpyHostToDevice, dev->s_in) !=
+            hipSuccess)
+            return JFS_ERR_HIP;
+        if (hipEventRecord(sl.ev_in, dev->s_in) != hipSuccess) return JFS_ERR_HIP;
+        if (hipStreamWaitEvent(sl.st, sl.ev_in, 0) != hipSuccess) return JFS_ERR_HIP;
+        if (launch_kernel(algo, dir, d_desc, n, d_ret, sl.st) != 0) return JFS_ERR_HIP;
+        if (hipEventRecord(sl.ev_k, sl.st) != hipSuccess) return JFS_ERR_HIP;
+        if (hipStreamWaitEvent(dev->s_out, sl.ev_k, 0) != hipSuccess) return JFS_ERR_HIP;
+        if (hipMemcpyAsync(h_ret, d_ret, (size_t)n * 4, hipMemcpyDeviceToHost, dev->s_out) != hipSuccess)
+            return JFS_ERR_HIP;
+        if (hipMemcpyAsync(h_out, d_out, (size_t)c.tout, hipMemcpyDeviceToHost, dev->s_out) != hipSuccess)
+            return JFS_ERR_HIP;
+        if (hipEventRecord(sl.ev, dev->s_out) != hipSuccess) return JFS_ERR_HIP;
+        return JFS_OK;
+    };
+    auto finish = [&](const Chunk &c) -> int64_t {
+        Slot &sl = dev->slot[c.slot];
+        const double t0 = host_trace() ? now_ms() : 0.0;
+        if (hipEventSynchronize(sl.ev) != hipSuccess) return JFS_ERR_HIP;
+        const double t1 = host_trace() ? now_ms() : 0.0;
+        uint8_t *h_in, *h_out;
+        jfs_dev_block *h_desc;
+        int32_t *h_ret;
+        layout(c, sl.h, &h_in, &h_out, &h_desc, &h_ret);
+        std::vector<CopyJob> jobs;
+        for (int i = c.s; i < c.e; i++) {
+            int64_t r = finish_result(algo, dir, h_ret[i - c.s]);
+            if (algo == JFS_ALGO_ZSTD && dir == DECOMPRESS && r > 0 &&
+                iov[i].dst_cap < zstd_size_hint(iov[i].src, iov[i].src_len)) {
+                // decoded into DataDog's own buffer: compress.go:99-101 "buffer too short"
+                r = JFS_ERR_SHORT_BUFFER;
+            }
+            if (r > 0) jobs.push_back({iov[i].dst, h_out + out_off[i], r});
+            out[i] = r;
         }
-        if (r > 0) memcpy(iov[i].dst, h_out + out_off[i], (size_t)r);
-        out[i] = r;
+        par_copy(jobs);
+        if (host_trace())
+            fprintf(stderr, "[jfs host] chunk %d-%d wait %.2f ms copy-out %.1f MiB %.2f ms\n", c.s, c.e, t1 - t0,
+                    c.tout / 1048576.0, now_ms() - t1);
+        return JFS_OK;
+    };
+    const int nch = (int)ch.size();
+    int64_t rc = JFS_OK;
+    int done = 0;  // chunks [0, done) finished
+    for (int k = 0; k < nch && rc == JFS_OK; k++) {
+        if (k >= NSLOT) rc = finish(ch[done++]);
+        if (rc == JFS_OK) rc = launch(ch[k]);
     }
-    return JFS_OK;
+    while (done < nch && rc == JFS_OK) rc = finish(ch[done++]);
+    if (rc != JFS_OK) {  // leave no copy in flight into the staging slots
+        (void)hipStreamSynchronize(dev->s_in);
+        for (Slot &sl : dev->slot) (void)hipStreamSynchronize(sl.st);
+        (void)hipStreamSynchronize(dev->s_out);
+    }
+    return rc;
 }
 
 // ---------------------------------------------------------------------------
@@ -334,18 +476,7 @@ int64_t batch_common(int algo, int dir, int nblk, const jfs_iov *iov, int64_t *o
     std::vector<std::vector<int64_t>> res(G);
     auto work = [&](size_t g) {
         res[g].assign(part[g].size(), 0);
-        // bound each device batch to ~1 GiB of staging
-        size_t s = 0;
-        while (s < part[g].size() && rc[g] == JFS_OK) {
-            size_t e = s;
-            int64_t bytes = 0;
-            while (e < part[g].size() && (e == s || bytes + part[g][e].src_len + part[g][e].dst_cap <= (1ll << 30))) {
-                bytes += part[g][e].src_len + part[g][e].dst_cap;
-                e++;
-            }
-            rc[g] = run_batch(ds[g], algo, dir, (int)(e - s), part[g].data() + s, res[g].data() + s);
-            s = e;
-        }
+        rc[g] = run_batch(ds[g], algo, dir, (int)part[g].size(), part[g].data(), res[g].data());
     };
     if (G == 1) work(0);
     else {
