@@ -736,20 +736,34 @@ __device__ __forceinline__ uint32_t step_next(const Smem &s, const Ctx &c, int32
     return x;
 }
 
-// ---------------------------------------------------------------------------
-// parser wave: stage one window, find its true token chain, write the table
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ void parse_window(Smem &s, Ctx &c, int32_t wbase, uint32_t *T_out,
-                                             uint32_t *efin_out PROF_ARG) {
-    const int l = lane_id();
-    stage_window(s, c, wbase);
-    const int32_t cbase = c.cbase;
-    PCOUNT(10, 1);
-    __builtin_amdgcn_wave_barrier();
-    PSTAMP(0);
+// Next-token step for windows far from the input end (no end-of-input rule
+// can apply to a token that starts and whose match-length byte lies in the
+// window): two LDS byte reads and a dozen VALU ops.  Tokens with a literal-
+// length extension or a 255 match-length byte take step_next.
+template <bool LEAN>
+__device__ __forceinline__ uint32_t walk_step(const Smem &s, const Ctx &c, int32_t p, bool act) {
+    if (!LEAN) return step_next(s, c, p, act);
+    const int32_t r = p - c.cbase;  // p in [cbase, cbase + CW + OV): r + 17 < CWIN
+    const uint32_t tb = c.cw[r];
+    const uint32_t ll = tb >> 4;
+    const uint32_t e2 = c.cw[r + 3 + (int32_t)ll];
+    const bool mlx = (tb & 15u) == 15u;
+    const bool slow = act && (ll == 15u || (mlx && e2 == 255u));
+    uint32_t x = (uint32_t)(p + 3 + (int32_t)ll + (mlx ? 1 : 0));
+    if (__ballot(slow)) {
+        if (slow) x = step_next(s, c, p, true);
+    }
+    return x;
+}
 
+// Chain of one 32-byte piece: a speculative walk from OV bytes before the
+// piece records the positions it visits; fix-up rounds take the true entry
+// (exit of the previous piece) and walk only until they meet that chain.
+template <bool LEAN>
+__device__ __forceinline__ void piece_chain(Smem &s, Ctx &c, int32_t wbase, int32_t plo, int32_t phi, uint64_t &vt,
+                                            uint32_t &ex PROF_ARG) {
+    const int l = lane_id();
     // 1. speculative walk of this lane's piece: visited positions + exit
-    const int32_t plo = cbase + l * P, phi = plo + P;
     // The walk starts OV bytes before the piece (a pre-roll whose positions are
     // not recorded): by the time it reaches the piece it has usually fallen into
     // the true chain, so few pieces need a second fix-up round.
@@ -762,7 +776,7 @@ __device__ __forceinline__ void parse_window(Smem &s, Ctx &c, int32_t wbase, uin
         for (int guard = 0; __ballot(act); ++guard) {
             PCOUNT(11, 1);
             if (act) {
-                const uint32_t x = step_next(s, c, q, act);
+                const uint32_t x = walk_step<LEAN>(s, c, q, act);
                 if (x & STOP) {
                     sx = x;
                     act = false;
@@ -781,8 +795,8 @@ __device__ __forceinline__ void parse_window(Smem &s, Ctx &c, int32_t wbase, uin
     // 2. fix-up: true entry of piece k = exit of piece k-1.  An entry on the
     //    speculative chain keeps its suffix; otherwise walk from the entry until
     //    the chain meets the speculative one (or leaves the piece).
-    uint64_t vt = vs;  // true chain positions in this piece
-    uint32_t ex = sx;  // true exit
+    vt = vs;  // true chain positions in this piece
+    ex = sx;  // true exit
     for (int r = 0;; ++r) {
         const uint32_t In = dpp_shift_up(ex, (uint32_t)wbase);
         const bool ch = In != cur;
@@ -816,7 +830,7 @@ __device__ __forceinline__ void parse_window(Smem &s, Ctx &c, int32_t wbase, uin
                     ex = sx;
                     part = false;
                 } else {
-                    const uint32_t x = step_next(s, c, q, part);
+                    const uint32_t x = walk_step<LEAN>(s, c, q, part);
                     if (x & STOP) {
                         vt = vp;
                         ex = x;
@@ -835,6 +849,25 @@ __device__ __forceinline__ void parse_window(Smem &s, Ctx &c, int32_t wbase, uin
             if (guard > P) { c.bug = 7; break; }
         }
     }
+}
+
+// ---------------------------------------------------------------------------
+// parser wave: stage one window, find its true token chain, write the table
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void parse_window(Smem &s, Ctx &c, int32_t wbase, uint32_t *T_out,
+                                             uint32_t *efin_out PROF_ARG) {
+    const int l = lane_id();
+    stage_window(s, c, wbase);
+    const int32_t cbase = c.cbase;
+    PCOUNT(10, 1);
+    __builtin_amdgcn_wave_barrier();
+    PSTAMP(0);
+
+    const int32_t plo = cbase + l * P, phi = plo + P;
+    uint64_t vt;  // true chain positions in this piece (bit = position - plo)
+    uint32_t ex;  // true exit: first position >= phi, or STOP | p
+    if (cbase + CWIN + 32 < c.n) piece_chain<true>(s, c, wbase, plo, phi, vt, ex PROF_PASS);
+    else piece_chain<false>(s, c, wbase, plo, phi, vt, ex PROF_PASS);
     *efin_out = readlane(ex, 63);
     PSTAMP(1);
 
