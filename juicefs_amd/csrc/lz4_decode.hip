@@ -488,13 +488,18 @@ __device__ __forceinline__ void lds_or(uint8_t *ring, uint32_t a, uint32_t v) { 
 __device__ __forceinline__ void put16(Smem &s, uint32_t da, int32_t m, uint32_t w0, uint32_t w1, uint32_t w2,
                                       uint32_t w3, uint32_t w4) {
     uint8_t *ring = s.ring;
-    const int32_t ha = (int32_t)(da & 3u), e = ha + m;  // 1..19
+    const int32_t ha = (int32_t)(da & 3u), e8 = 8 * (ha + m);  // byte span [ha, ha + m) of the 20 bytes, in bits
     const uint32_t D0 = da & ~3u;
-    lds_or(ring, D0, w0 & lomask(e) & ~lomask(ha));
-    lds_or(ring, (D0 + 4) & RMASK, w1 & lomask(e - 4));
-    lds_or(ring, (D0 + 8) & RMASK, w2 & lomask(e - 8));
-    lds_or(ring, (D0 + 12) & RMASK, w3 & lomask(e - 12));
-    lds_or(ring, (D0 + 16) & RMASK, w4 & lomask(e - 16));
+    // lomask(k) = high half of 0x00000000FFFFFFFF << 8k (k clamped to [0, 4])
+    auto lm = [](int32_t b) -> uint32_t {
+        const uint32_t sh = (uint32_t)(b < 0 ? 0 : b > 32 ? 32 : b);
+        return (uint32_t)((0xFFFFFFFFull << sh) >> 32);
+    };
+    lds_or(ring, D0, w0 & lm(e8) & ~lm(8 * ha));
+    lds_or(ring, (D0 + 4) & RMASK, w1 & lm(e8 - 32));
+    lds_or(ring, (D0 + 8) & RMASK, w2 & lm(e8 - 64));
+    lds_or(ring, (D0 + 12) & RMASK, w3 & lm(e8 - 96));
+    lds_or(ring, (D0 + 16) & RMASK, w4 & lm(e8 - 128));
 }
 
 // Zero ring bytes of output [O0, O1) (bytes below O0 in the first dword are kept).
@@ -539,7 +544,9 @@ __device__ __forceinline__ void batch(Smem &s, Ctx &c, bool act, int32_t o, uint
     const int32_t hz = O1 + 4 - R;
     PCOUNT(14, 1);
     if (O0 - c.F >= FLUSH_T) flush_to_line(s, c, O0);
+#ifndef JFS_SKIP_ZERO
     zero_span(s, c, O0, O1);
+#endif
     const int32_t ms = o + (int32_t)ll, msrc = ms - (int32_t)off;
     const bool hasm = act && ml > 0;
     const bool zero = hasm && off == 0;
@@ -557,6 +564,9 @@ __device__ __forceinline__ void batch(Smem &s, Ctx &c, bool act, int32_t o, uint
         f1 = q[1];
     }
     // literal runs (source: staged window, addressed as ring + R + litr)
+#ifdef JFS_SKIP_LIT
+    if (0)
+#endif
     for (uint32_t k = 0; __ballot(act && k < ll); k += 16) {
         if (act && k < ll) {
             const int32_t m = ll - k < 16u ? (int32_t)(ll - k) : 16;
@@ -565,6 +575,9 @@ __device__ __forceinline__ void batch(Smem &s, Ctx &c, bool act, int32_t o, uint
     }
     PSTAMP(4);
     // far matches (offset-0 matches write zeros: the span is already zero)
+#ifdef JFS_SKIP_FAR
+    if (0)
+#endif
     if (__ballot(far)) {
         for (uint32_t k = 0; __ballot(far && k < ml); k += 16) {
             if (far && k < ml) {
@@ -613,6 +626,9 @@ __device__ __forceinline__ void batch(Smem &s, Ctx &c, bool act, int32_t o, uint
         const uint32_t key = act ? (uint32_t)ms : (lane_id() < first ? 0u : 0xFFFFFFFFu);  // non-decreasing
         const uint32_t mek = pend ? (uint32_t)(ms + (int32_t)ml) : 0u;
         bool cand = pend && off >= ml;
+#ifdef JFS_SKIP_SUBST
+        if (0)
+#endif
         for (int it = 0; it < 3; ++it) {
             const bool want = cand && src >= O0;
             if (!__ballot(want)) break;
@@ -634,6 +650,9 @@ __device__ __forceinline__ void batch(Smem &s, Ctx &c, bool act, int32_t o, uint
     // near matches in rounds
     int32_t pos = ms, rem = (int32_t)ml, D = ms - src;
     const int32_t send = src + (int32_t)ml < ms ? src + (int32_t)ml : ms;
+#ifdef JFS_SKIP_NEAR
+    if (0)
+#endif
     for (int guard = 0; __ballot(pend); ++guard) {
         if (guard > 64) { c.bug = 5; break; }
         const int32_t front = (int32_t)dwave_min(pend ? (uint32_t)ms : 0x7FFFFFFFu);
@@ -710,7 +729,9 @@ __device__ __forceinline__ uint32_t copy_tokens(Smem &s, Ctx &c, uint32_t T, int
             const bool act = (uint32_t)l >= j && (uint32_t)l < eb;
             const int32_t O1 = (int32_t)readlane((uint32_t)endo, (int)eb - 1);
             PSTAMP(3);
+#ifndef JFS_LZ4_NOCOPY  // diagnostics: parse-only variant (wrong output)
             batch(s, c, act, o, ll, ml, off, litr, oj, O1 PROF_PASS);
+#endif
             j = eb;
         }
         if (bm) {
