@@ -54,6 +54,9 @@ constexpr int RMASK = R - 1;
 #ifndef JFS_LZ4_OV
 #define JFS_LZ4_OV 32
 #endif
+#ifndef JFS_LZ4_DP
+#define JFS_LZ4_DP 1  // exit-table parser for windows away from the input end
+#endif
 constexpr int OV = JFS_LZ4_OV;           // speculative-walk pre-roll (bytes before the piece)
 constexpr int TMAX = CW / 3 + 2;       // max tokens in a window (interior token >= 3 bytes)
 // Table capacity per window.  Windows with more tokens (only runs of 3..5-byte
@@ -872,6 +875,134 @@ __device__ __forceinline__ void piece_chain(Smem &s, Ctx &c, int32_t wbase, int3
     }
 }
 
+#if JFS_LZ4_DP
+__device__ __forceinline__ uint32_t pick2(uint32_t a, uint32_t b, uint32_t m) { return a ^ ((a ^ b) & m); }
+
+// Exit table of one 32-byte piece, built backwards over its offsets i:
+//   XT byte i = offset of the first position >= 32 on the chain from i
+//   (3..49), or 255 when that chain meets a token the lean step cannot take.
+// Bytes come from the staged window (two LDS byte reads per offset); the
+// table lives in 8 VGPRs, indexed only with compile-time dword numbers
+// (mask selects, so it stays in registers).
+template <int I>
+__device__ __forceinline__ void dp_step(const uint8_t *pc, int32_t lim, uint32_t (&XT)[8]) {
+    if constexpr (I >= 0) {
+        const uint32_t tb = pc[I], e1 = pc[I + 1];
+        const uint32_t ll = tb >> 4;
+        const bool llx = ll == 15u;
+        // q: offset of the first match-length extension byte (after the offset)
+        const uint32_t q = (uint32_t)I + 3u + (llx ? 16u + e1 : ll);
+        const bool oob = (int32_t)q >= lim;  // not staged: exact walk
+        const uint32_t e2 = pc[oob ? 0u : q];
+        const bool mlx = (tb & 15u) == 15u;
+        const uint32_t nx = q + (mlx ? 1u : 0u);
+        // long literal runs land past the piece (else: exact walk)
+        const bool slow = (llx && (e1 == 255u || nx < 32u)) || oob || (mlx && e2 == 255u);
+        uint32_t xi = nx;
+        if constexpr (I + 3 < 32) {
+            constexpr int bq = (I + 3) >> 2;
+            const uint32_t kx = (nx >> 2) - (uint32_t)bq;  // 0..4 when nx < 32 and !llx
+            uint32_t xw = XT[bq];
+            if constexpr (bq + 1 < 8) xw = pick2(xw, XT[bq + 1], 0u - (uint32_t)(kx == 1));
+            if constexpr (bq + 2 < 8) xw = pick2(xw, XT[bq + 2], 0u - (uint32_t)(kx == 2));
+            if constexpr (bq + 3 < 8) xw = pick2(xw, XT[bq + 3], 0u - (uint32_t)(kx == 3));
+            if constexpr (bq + 4 < 8) xw = pick2(xw, XT[bq + 4], 0u - (uint32_t)(kx == 4));
+            const uint32_t xj = (xw >> (8u * (nx & 3u))) & 0xFFu;
+            xi = nx >= 32u ? nx : xj;
+        }
+        xi = slow || xi > 254u ? 255u : xi;
+        XT[I >> 2] |= xi << (8 * (I & 3));
+        dp_step<I - 1>(pc, lim, XT);
+    }
+}
+
+__device__ __forceinline__ uint32_t byte_of8(const uint32_t (&V)[8], uint32_t i) {
+    const uint32_t d = i >> 2;
+    const uint32_t m0 = 0u - (d & 1u), m1 = 0u - ((d >> 1) & 1u), m2 = 0u - ((d >> 2) & 1u);
+    const uint32_t ab = pick2(pick2(V[0], V[1], m0), pick2(V[2], V[3], m0), m1);
+    const uint32_t ce = pick2(pick2(V[4], V[5], m0), pick2(V[6], V[7], m0), m1);
+    return (pick2(ab, ce, m2) >> (8u * (i & 3u))) & 0xFFu;
+}
+
+// Chain of one 32-byte piece (lean windows) from the exit table: fix-up rounds
+// are one register lookup per lane (an exact walk for table entries 255), then
+// one walk from the true entry records the chain positions.
+__device__ __forceinline__ void table_chain(Smem &s, Ctx &c, int32_t wbase, int32_t plo, int32_t phi, uint64_t &vt,
+                                            uint32_t &ex PROF_ARG) {
+    const int l = lane_id();
+    uint32_t XT[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    dp_step<31>(c.cw + l * P, CWIN - 1 - l * P, XT);
+    uint32_t Ea = l == 0 ? (uint32_t)wbase : (uint32_t)plo;
+    uint32_t cur = 0xFFFFFFFFu;
+    ex = 0;
+    for (int r = 0;; ++r) {
+        const bool ch = Ea != cur;
+        if (!__ballot(ch)) break;
+        if (r > 70) { c.bug = 3; break; }
+        PCOUNT(12, 1);
+        cur = Ea;
+        bool walk = false;
+        if (ch) {
+            if ((Ea & STOP) || (int32_t)Ea >= phi) {
+                ex = Ea;
+            } else {
+                const uint32_t x = byte_of8(XT, Ea - (uint32_t)plo);
+                if (x == 255u) walk = true;
+                else ex = (uint32_t)plo + x;
+            }
+        }
+        if (__ballot(walk)) {
+            // exact step over the token the table cannot take, then back to the table
+            int32_t q = (int32_t)Ea;
+            for (int g = 0; __ballot(walk); ++g) {
+                PCOUNT(13, 1);
+                if (walk) {
+                    const uint32_t x = walk_step<true>(s, c, q, walk);
+                    if (x & STOP) {
+                        ex = x;
+                        walk = false;
+                    } else {
+                        q = (int32_t)x;
+                        if (q >= phi) {
+                            ex = (uint32_t)q;
+                            walk = false;
+                        } else {
+                            const uint32_t y = byte_of8(XT, (uint32_t)(q - plo));
+                            if (y != 255u) {
+                                ex = (uint32_t)plo + y;
+                                walk = false;
+                            }
+                        }
+                    }
+                }
+                if (g > P) { c.bug = 7; break; }
+            }
+        }
+        Ea = dpp_shift_up(ex, (uint32_t)wbase);
+    }
+    // true chain positions in the piece
+    vt = 0;
+    {
+        int32_t q = (int32_t)cur;
+        bool act = !(cur & STOP) && q < phi;
+        for (int g = 0; __ballot(act); ++g) {
+            PCOUNT(11, 1);
+            if (act) {
+                const uint32_t x = walk_step<true>(s, c, q, act);
+                if (x & STOP) {  // a stop token ends the chain (it is not a token)
+                    act = false;
+                } else {
+                    vt |= 1ull << (uint32_t)(q - plo);
+                    if ((int32_t)x >= phi) act = false;
+                    else q = (int32_t)x;
+                }
+            }
+            if (g > P) { c.bug = 9; break; }
+        }
+    }
+}
+#endif
+
 // ---------------------------------------------------------------------------
 // parser wave: stage one window, find its true token chain, write the table
 // ---------------------------------------------------------------------------
@@ -887,7 +1018,12 @@ __device__ __forceinline__ void parse_window(Smem &s, Ctx &c, int32_t wbase, uin
     const int32_t plo = cbase + l * P, phi = plo + P;
     uint64_t vt;  // true chain positions in this piece (bit = position - plo)
     uint32_t ex;  // true exit: first position >= phi, or STOP | p
+#if JFS_LZ4_DP
+    if (cbase + CWIN + 400 < c.n) table_chain(s, c, wbase, plo, phi, vt, ex PROF_PASS);
+    else if (cbase + CWIN + 32 < c.n) piece_chain<true>(s, c, wbase, plo, phi, vt, ex PROF_PASS);
+#else
     if (cbase + CWIN + 32 < c.n) piece_chain<true>(s, c, wbase, plo, phi, vt, ex PROF_PASS);
+#endif
     else piece_chain<false>(s, c, wbase, plo, phi, vt, ex PROF_PASS);
     *efin_out = readlane(ex, 63);
     PSTAMP(1);
@@ -1062,7 +1198,7 @@ __device__ __forceinline__ void copier_wave(Smem &s, Ctx &c, int32_t *retp PROF_
 #ifndef JFS_LZ4_NSGPR
 #define JFS_LZ4_NSGPR 80
 #endif
-#define JFS_LZ4_ATTR __attribute__((amdgpu_num_sgpr(JFS_LZ4_NSGPR)))
+#define JFS_LZ4_ATTR __attribute__((amdgpu_num_sgpr(JFS_LZ4_NSGPR), amdgpu_waves_per_eu(8)))
 __global__ __launch_bounds__(128) JFS_LZ4_ATTR void lz4_decode_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
                                                         int32_t *__restrict__ ret) {
     __shared__ Smem s;
