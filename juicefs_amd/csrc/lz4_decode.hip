@@ -57,6 +57,9 @@ constexpr int RMASK = R - 1;
 #ifndef JFS_LZ4_DP
 #define JFS_LZ4_DP 1  // exit-table parser for windows away from the input end
 #endif
+#ifndef JFS_LZ4_NEARPM
+#define JFS_LZ4_NEARPM 1  // exact near-match readiness (prefix max of pending ends)
+#endif
 constexpr int OV = JFS_LZ4_OV;           // speculative-walk pre-roll (bytes before the piece)
 constexpr int TMAX = CW / 3 + 2;       // max tokens in a window (interior token >= 3 bytes)
 // Table capacity per window.  Windows with more tokens (only runs of 3..5-byte
@@ -77,7 +80,7 @@ static_assert(R - BSPAN >= LMAX + 16, "far sources must lie below the flushed pr
 
 #ifdef JFS_PROF
 // diagnostic build only: per-phase cycle sums (s_memtime), never in the product .so
-#define NPROF 16  // 0..9 phase cycles, 10..15 event counts
+#define NPROF 20  // 0..9 phase cycles, 10..19 event counts
 __device__ uint64_t g_prof[NPROF];
 struct Prof {
     uint64_t t, acc[NPROF];
@@ -571,6 +574,7 @@ __device__ __forceinline__ void batch(Smem &s, Ctx &c, bool act, int32_t o, uint
     if (0)
 #endif
     for (uint32_t k = 0; __ballot(act && k < ll); k += 16) {
+        PCOUNT(16, 1);
         if (act && k < ll) {
             const int32_t m = ll - k < 16u ? (int32_t)(ll - k) : 16;
             copy16<false>(s, c.cwoff + litr + k, slot(c, o + (int32_t)k), m);
@@ -583,6 +587,7 @@ __device__ __forceinline__ void batch(Smem &s, Ctx &c, bool act, int32_t o, uint
 #endif
     if (__ballot(far)) {
         for (uint32_t k = 0; __ballot(far && k < ml); k += 16) {
+            PCOUNT(17, 1);
             if (far && k < ml) {
                 const int32_t m = ml - k < 16u ? (int32_t)(ml - k) : 16;
                 const uint32_t da = slot(c, ms + (int32_t)k);
@@ -623,10 +628,10 @@ __device__ __forceinline__ void batch(Smem &s, Ctx &c, bool act, int32_t o, uint
     // This shortens the dependency chains the rounds below must walk.
     bool pend = hasm && !far && !zero;
     int32_t src = msrc;
+    const uint64_t am = __ballot(act);
+    const int first = am ? (int)__builtin_ctzll(am) : 0;
+    const uint32_t key = act ? (uint32_t)ms : (lane_id() < first ? 0u : 0xFFFFFFFFu);  // non-decreasing
     {
-        const uint64_t am = __ballot(act);
-        const int first = am ? (int)__builtin_ctzll(am) : 0;
-        const uint32_t key = act ? (uint32_t)ms : (lane_id() < first ? 0u : 0xFFFFFFFFu);  // non-decreasing
         const uint32_t mek = pend ? (uint32_t)(ms + (int32_t)ml) : 0u;
         bool cand = pend && off >= ml;
 #ifdef JFS_SKIP_SUBST
@@ -653,13 +658,32 @@ __device__ __forceinline__ void batch(Smem &s, Ctx &c, bool act, int32_t o, uint
     // near matches in rounds
     int32_t pos = ms, rem = (int32_t)ml, D = ms - src;
     const int32_t send = src + (int32_t)ml < ms ? src + (int32_t)ml : ms;
+#if JFS_LZ4_NEARPM
+    int jl = 0;  // last lane with key < send (jv: such a lane exists)
+#pragma unroll
+    for (int stp = 32; stp; stp >>= 1) {
+        const uint32_t v = (uint32_t)__shfl((int)key, jl + stp, 64);
+        jl = v < (uint32_t)send ? jl + stp : jl;
+    }
+    const bool jv = (uint32_t)__shfl((int)key, jl, 64) < (uint32_t)send;
+#endif
 #ifdef JFS_SKIP_NEAR
     if (0)
 #endif
     for (int guard = 0; __ballot(pend); ++guard) {
         if (guard > 64) { c.bug = 5; break; }
+        PCOUNT(18, 1);
+#if JFS_LZ4_NEARPM
+        // ready: no still-pending destination [ms_j, ms_j + ml_j) meets the source
+        // [src, send).  Destinations are disjoint and in lane order, so that is the
+        // prefix max of pending ends at the last lane jl with ms_jl < send.
+        const uint32_t pm = dpp_scan_max(pend ? (uint32_t)(ms + (int32_t)ml) : 0u);
+        const uint32_t pmj = (uint32_t)__shfl((int)pm, jl, 64);
+        bool go = pend && (!jv || pmj <= (uint32_t)src);
+#else
         const int32_t front = (int32_t)dwave_min(pend ? (uint32_t)ms : 0x7FFFFFFFu);
         bool go = pend && send <= front;
+#endif
         while (__ballot(go)) {
             PCOUNT(15, 1);
             if (go) {

@@ -15,7 +15,7 @@ b.decompress(); torch.cuda.synchronize()
 lib.jfs_prof_reset()
 t0 = time.perf_counter(); b.decompress(); torch.cuda.synchronize(); dt = time.perf_counter() - t0
 assert b.verify()
-buf = (ctypes.c_uint64 * 16)()
+buf = (ctypes.c_uint64 * 20)()
 lib.jfs_prof_read(buf)
 names = ["stage", "walk+fixup", "table+tokparse", "batching", "lits+pref", "far", "near", "long", "serial", "tail"]
 tot = sum(buf[:10])
@@ -25,3 +25,5 @@ for n, v in zip(names, buf[:10]):
 w = max(buf[10], 1)
 print(f"windows/block {buf[10]/nblk:.1f}  per window: walk iters {buf[11]/w:.2f}  fix-up rounds {buf[12]/w:.2f}  "
       f"partial iters {buf[13]/w:.2f}  batches {buf[14]/w:.2f}  near copy iters {buf[15]/w:.2f}")
+b = max(buf[14], 1)
+print(f"per batch: literal iters {buf[16]/b:.2f}  far iters {buf[17]/b:.2f}  near rounds {buf[18]/b:.2f}  near copy iters {buf[15]/b:.2f}")
