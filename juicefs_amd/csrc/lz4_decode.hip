@@ -562,12 +562,13 @@ __device__ __forceinline__ void batch(Smem &s, Ctx &c, bool act, int32_t o, uint
         c.Fw = c.F;
         if (hz + LMAX > c.Fw) c.bug = 4;
     }
-    // far prefetch: 32 bytes from the 16-byte line holding the source start
+    // far prefetch: the 16-byte line holding the source start, and the next
+    // one only when the first 16 source bytes cross into it
     uint4 f0 = make_uint4(0, 0, 0, 0), f1 = f0;
     if (far) {
         const gc_u4 *q = (const gc_u4 *)((uintptr_t)(c.dst + msrc) & ~(uintptr_t)15);
         f0 = q[0];
-        f1 = q[1];
+        if ((int32_t)(((uintptr_t)(c.dst + msrc)) & 15u) + (ml < 16u ? (int32_t)ml : 16) > 16) f1 = q[1];
     }
     // literal runs (source: staged window, addressed as ring + R + litr)
 #ifdef JFS_SKIP_LIT
@@ -614,9 +615,11 @@ __device__ __forceinline__ void batch(Smem &s, Ctx &c, bool act, int32_t o, uint
             const bool more = far && k + 16 < ml;
             if (__ballot(more)) {
                 if (more) {
-                    const gc_u4 *q = (const gc_u4 *)((uintptr_t)(c.dst + msrc + (int32_t)k + 16) & ~(uintptr_t)15);
+                    const g_u8 *sp = c.dst + msrc + (int32_t)k + 16;
+                    const gc_u4 *q = (const gc_u4 *)((uintptr_t)sp & ~(uintptr_t)15);
+                    const uint32_t rest = ml - k - 16;
                     f0 = q[0];
-                    f1 = q[1];
+                    if ((int32_t)((uintptr_t)sp & 15u) + (rest < 16u ? (int32_t)rest : 16) > 16) f1 = q[1];
                 }
             }
         }
