@@ -1,35 +1,30 @@
-// LZ4 block decoder for gfx950 -- one wavefront per block.
+// LZ4 block decoder for gfx950 -- one workgroup of two wavefronts per block.
 //
 // Replaces LZ4_decompress_safe reached from pkg/compress/compress.go:120-125
 // (LZ4.Decompress -> lz4.DecompressSafe).  Result semantics (decoded size, or
 // the same negative error value liblz4 1.9.3 returns) are restated in
 // oracle/lz4_oracle.c; parity is tested in tests/test_lz4_gpu.py.
 //
-// Design (DESIGN.md "LZ4 decode"):
-//   The compressed stream is processed in windows of CW bytes staged in LDS.
-//   1. Speculative parse: lane k owns the k-th P-byte piece of the window and
-//      walks the token chain that starts at the piece start, keeping every
-//      token's fields in registers and a bitmask of the positions it visited.
-//      Chains started at arbitrary bytes fall into the true chain within a few
-//      tokens, so after one fix-up round (entry of piece k = exit of piece k-1;
-//      a lane whose true entry is in its visited mask just drops the prefix)
-//      almost every lane already holds its true tokens; the rest re-walk.
-//      Tokens that need the exact liblz4 end-of-buffer rules, or whose length
-//      fields are very long, stop the window.
-//   2. DPP prefix sums give token indices and output offsets; the output-side
-//      fast-loop checks run; tokens go to an LDS table (8 bytes each).
-//   3. Copy, lane per token, 64 consecutive tokens per batch: literal runs
-//      first (source: the staged window), then far matches (source older than
-//      the LDS output ring: HBM, prefetched before the literal pass), then
-//      near matches in rounds -- a match is ready once its source ends at or
-//      below the earliest still-pending match start.  Copies move up to 16
-//      bytes per step (aligned LDS dword reads + v_alignbyte, byte-exact ring
-//      writes); overlapping matches (offset < 16) double their step distance.
-//      Tokens longer than LMAX are copied by the whole wave.
-//   4. The ring streams to HBM with 16-byte stores at 128-byte lines.
-//   5. Everything the fast path does not cover (the last bytes of input /
-//      output, malformed input, very long length fields) runs through an
-//      exact, wave-uniform restatement of the liblz4 1.9.3 state machine.
+// Design:
+//   The compressed stream is processed in windows of CW bytes staged in LDS,
+//   double-buffered: the parser wave finds window k's token chain while the
+//   copier wave produces window k-1's output (two barriers per window).
+//   Parser: lane k owns the k-th P-byte piece; an exit table built backwards
+//   over the piece (8 VGPRs) gives, for every entry offset, where the chain
+//   leaves the piece; fix-up rounds propagate the true entry (exit of the
+//   previous piece, DPP wave shift) until nothing changes; the chain
+//   positions go to a u16 table in LDS.  Near the input end a speculative
+//   walk with the exact end-of-input rules is used instead.
+//   Copier: lane per token, 64 consecutive tokens per batch; DPP prefix sums
+//   give output offsets and the liblz4 output-side checks; literal runs,
+//   far matches (source older than the LDS output ring, read from HBM),
+//   source substitution, then near matches in rounds (ready once no pending
+//   destination overlaps the source).  Every ring write is an LDS atomic OR of
+//   whole dwords into a zeroed span.  The ring streams to HBM in 128-byte
+//   lines.  Tokens longer than LMAX are copied by the whole wave.
+//   Everything the fast path does not cover (the last bytes of input /
+//   output, malformed input, very long length fields) runs through an
+//   exact, wave-uniform restatement of the liblz4 1.9.3 state machine.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
