@@ -52,6 +52,9 @@ constexpr int RMASK = R - 1;
 #ifndef JFS_LZ4_DP
 #define JFS_LZ4_DP 1  // exit-table parser for windows away from the input end
 #endif
+#ifndef JFS_LZ4_SUBST
+#define JFS_LZ4_SUBST 3  // source-substitution hops per batch
+#endif
 #ifndef JFS_LZ4_NEARPM
 #define JFS_LZ4_NEARPM 1  // exact near-match readiness (prefix max of pending ends)
 #endif
@@ -154,11 +157,20 @@ __device__ __forceinline__ void stage_window(Smem &s, Ctx &c, int32_t wbase) {
     const int l = lane_id();
     const uint32_t mis = (uint32_t)(((uintptr_t)c.src + (uint32_t)wbase) & 15u);
     c.cbase = wbase - (int32_t)mis;
-    for (int k = l; k < CWIN / 16; k += 64) {
-        int32_t p = c.cbase + 16 * k;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (p < c.n) v = *(const gc_u4 *)(c.src + p);  // chunk holds at least one valid byte: same page
-        *(uint4 *)(c.cw + 16 * k) = v;
+    // all loads first, then the LDS writes: one HBM latency per window, not three
+    constexpr int NCH = (CWIN / 16 + 63) / 64;
+    uint4 v[NCH];
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+        const int k = l + 64 * j;
+        const int32_t p = c.cbase + 16 * k;
+        v[j] = make_uint4(0, 0, 0, 0);
+        if (k < CWIN / 16 && p < c.n) v[j] = *(const gc_u4 *)(c.src + p);  // chunk holds a valid byte: same page
+    }
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+        const int k = l + 64 * j;
+        if (k < CWIN / 16) *(uint4 *)(c.cw + 16 * k) = v[j];
     }
     // bytes outside [0, n) must read as 0 (they are never part of a fast-path token)
     if (c.cbase < 0 || c.cbase + CWIN > c.n) {
@@ -635,7 +647,7 @@ __device__ __forceinline__ void batch(Smem &s, Ctx &c, bool act, int32_t o, uint
 #ifdef JFS_SKIP_SUBST
         if (0)
 #endif
-        for (int it = 0; it < 3; ++it) {
+        for (int it = 0; it < JFS_LZ4_SUBST; ++it) {
             const bool want = cand && src >= O0;
             if (!__ballot(want)) break;
             int lo = 0;  // last lane with key <= src
