@@ -53,7 +53,7 @@ constexpr int RMASK = R - 1;
 #define JFS_LZ4_DP 1  // exit-table parser for windows away from the input end
 #endif
 #ifndef JFS_LZ4_SUBST
-#define JFS_LZ4_SUBST 3  // source-substitution hops per batch
+#define JFS_LZ4_SUBST 2  // source-substitution hops per batch (2 measured best: 323 vs 317 GiB/s for 3)
 #endif
 #ifndef JFS_LZ4_NEARPM
 #define JFS_LZ4_NEARPM 1  // exact near-match readiness (prefix max of pending ends)
