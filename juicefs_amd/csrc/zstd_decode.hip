@@ -957,11 +957,16 @@ typedef JFS_GLOBAL const uint16_t gc_u16;
 
 struct GBlk {
     const gc_u8 *bs;   // sequence bitstream
+    const gc_u8 *in;   // start of the input holding it
+    g_u4 *ib;          // the input's item array
     int32_t bsz, nseq;
     uint32_t item;     // BSTART item index (relative to the input)
-    uint32_t tll, tof, tml;
+    uint64_t tll, tof, tml;  // table cells (absolute index into the table scratch)
     uint32_t al;       // al_ll | al_of << 8 | al_ml << 16 | frame-first << 24
 };
+// Inputs per sequence workgroup: a 4 MiB frame has 32 compressed blocks, so
+// two inputs fill the 64 lanes of phase B.
+constexpr int ZSEQ_INPUTS = 2;
 struct SeqSmem {
     uint8_t stage[256];
     int16_t norm[64];
@@ -1076,8 +1081,8 @@ __device__ __forceinline__ uint32_t rep_res(uint32_t v, uint32_t e0, uint32_t e1
 }
 
 // phases B and C for the collected group
-__device__ __forceinline__ void seq_group(SeqSmem &sm, int gn, const gc_u8 *in, const gc_u16 *tabs, g_u4 *items,
-                                          uint32_t *e0, uint32_t *e1, uint32_t *e2) {
+__device__ __forceinline__ void seq_group(SeqSmem &sm, int gn, const gc_u16 *tabs, uint32_t *e0, uint32_t *e1,
+                                          uint32_t *e2) {
     const int l = lane_id();
     __builtin_amdgcn_wave_barrier();
     wait_vm();  // table cells written in phase A are complete before they are gathered
@@ -1087,14 +1092,14 @@ __device__ __forceinline__ void seq_group(SeqSmem &sm, int gn, const gc_u8 *in, 
         const GBlk d = sm.g[l];
         const int32_t all = d.al & 0xFF, alof = (d.al >> 8) & 0xFF, alml = (d.al >> 16) & 0xFF;
         const gc_u16 *tl = tabs + d.tll, *to = tabs + d.tof, *tm = tabs + d.tml;
-        g_u4 *it = items + d.item;
+        g_u4 *it = d.ib + d.item;
         if (d.nseq == 0) {
             it[1] = make_uint4(0, 0, 0, IT_BREP);
             it[2] = make_uint4(0, 0, 0, IT_BEND);
             brep = 1;
         } else {
             BR r;
-            if (!br_init(r, in, d.bs, d.bsz)) {
+            if (!br_init(r, d.in, d.bs, d.bsz)) {
                 it[1] = make_uint4(0, 0, (uint32_t)E_CORRUPT, IT_ERR);
             } else {
                 brep = 1;
@@ -1143,9 +1148,10 @@ __device__ __forceinline__ void seq_group(SeqSmem &sm, int gn, const gc_u8 *in, 
     // phase C: entry states in stream order
     for (int g = 0; g < gn; g++) {
         const uint32_t al = sm.g[g].al, item = sm.g[g].item;
+        g_u4 *ib = sm.g[g].ib;
         if (al >> 24) { *e0 = 1; *e1 = 4; *e2 = 8; }
         const uint32_t x0 = readlane(r0, g), x1 = readlane(r1, g), x2 = readlane(r2, g);
-        if (readlane(brep, g) && l == 0) items[item + 1] = make_uint4(*e0, *e1, *e2, IT_BREP);
+        if (readlane(brep, g) && l == 0) ib[item + 1] = make_uint4(*e0, *e1, *e2, IT_BREP);
         const uint32_t n0 = rep_res(x0, *e0, *e1, *e2), n1 = rep_res(x1, *e0, *e1, *e2), n2 = rep_res(x2, *e0, *e1, *e2);
         *e0 = n0; *e1 = n1; *e2 = n2;
     }
@@ -1156,99 +1162,104 @@ __global__ __launch_bounds__(64) void zseq_kernel(const jfs_dev_block *__restric
                                                   ZInfo *__restrict__ info, uint16_t *__restrict__ tabs_all,
                                                   uint4 *__restrict__ items_all, int strict_reserved) {
     __shared__ SeqSmem sm;
-    const int bi = blockIdx.x;
-    if (bi >= nblk) return;
     const int l = lane_id();
-    const jfs_dev_block b = blocks[bi];
-    ZInfo &zi = info[bi];
-    const gc_u8 *s = (const gc_u8 *)b.src;
-    g_u16 *tabs = (g_u16 *)tabs_all + zi.tab_off;
-    g_u4 *items = (g_u4 *)items_all + zi.item_off;
     for (int i = l; i < 36; i += 64) sm.lut_ll[i] = LL_BASE[i] | ((uint32_t)LL_BITS[i] << 24);
     for (int i = l; i < 53; i += 64) sm.lut_ml[i] = ML_BASE[i] | ((uint32_t)ML_BITS[i] << 24);
-    Walk w;
-    walk_init(w, s, b.src_len, b.dst_cap);
-    const uint32_t cap_items = zi.n_items, cap_cblk = zi.n_cblk;
-    uint32_t cur = 0, cblk = 0;  // next item slot, next table area
-    int gn = 0, first = 0, bug = 0;
-    uint32_t e0 = 1, e1 = 4, e2 = 8;
-    uint32_t t_ll = 0, t_of = 0, t_ml = 0;
-    int32_t al_ll = 0, al_of = 0, al_ml = 0, hv_ll = 0, hv_of = 0, hv_ml = 0;
-    auto put = [&](uint32_t x, uint32_t y, uint32_t z, uint32_t kind) {
-        if (cur >= cap_items) { bug = 1; return; }
-        if (l == 0) items[cur] = make_uint4(x, y, z, kind);
-        cur++;
-    };
-    for (;;) {
-        int32_t err = 0;
-        uint32_t fl = 0, chk = 0;
-        int ev = walk_next(w, &err, &fl, &chk);
-        if (ev == EV_DONE) break;
-        if (ev == EV_ERROR) { put(0, 0, (uint32_t)err, IT_ERR); break; }
-        if (ev == EV_FSTART) {
-            hv_ll = hv_of = hv_ml = 0;
-            first = 1;
-            put(0, 0, 0, IT_FSTART);
-            continue;
+    int gn = 0;
+    uint32_t e0 = 1, e1 = 4, e2 = 8;  // repeat offsets carried through phase C (reset at each frame)
+    for (int f = 0; f < ZSEQ_INPUTS; ++f) {
+        const int bi = blockIdx.x * ZSEQ_INPUTS + f;
+        if (bi >= nblk) break;
+        const jfs_dev_block b = blocks[bi];
+        ZInfo &zi = info[bi];
+        const gc_u8 *s = (const gc_u8 *)b.src;
+        g_u16 *tabs = (g_u16 *)tabs_all + zi.tab_off;
+        g_u4 *items = (g_u4 *)items_all + zi.item_off;
+        Walk w;
+        walk_init(w, s, b.src_len, b.dst_cap);
+        const uint32_t cap_items = zi.n_items, cap_cblk = zi.n_cblk;
+        uint32_t cur = 0, cblk = 0;  // next item slot, next table area
+        int first = 0, bug = 0;
+        uint32_t t_ll = 0, t_of = 0, t_ml = 0;
+        int32_t al_ll = 0, al_of = 0, al_ml = 0, hv_ll = 0, hv_of = 0, hv_ml = 0;
+        auto put = [&](uint32_t x, uint32_t y, uint32_t z, uint32_t kind) {
+            if (cur >= cap_items) { bug = 1; return; }
+            if (l == 0) items[cur] = make_uint4(x, y, z, kind);
+            cur++;
+        };
+        for (;;) {
+            int32_t err = 0;
+            uint32_t fl = 0, chk = 0;
+            int ev = walk_next(w, &err, &fl, &chk);
+            if (ev == EV_DONE) break;
+            if (ev == EV_ERROR) { put(0, 0, (uint32_t)err, IT_ERR); break; }
+            if (ev == EV_FSTART) {
+                hv_ll = hv_of = hv_ml = 0;
+                first = 1;
+                put(0, 0, 0, IT_FSTART);
+                continue;
+            }
+            if (ev == EV_FEND) {
+                put((uint32_t)w.fcs, (uint32_t)(w.fcs >> 32), chk, IT_FEND | (fl << 8));
+                if (fl & FE_MISSING) break;
+                continue;
+            }
+            const uint32_t ord = w.ordinal - 1;
+            if (w.btype != 2) {
+                put(ord, (uint32_t)w.bsize, 0, IT_BSTART);
+                put((uint32_t)w.bsize, 0, 0, IT_SEQ);
+                put(0, 0, 0, IT_BEND);
+                w.lb += w.bsize;
+                continue;
+            }
+            LitHdr h;
+            int32_t e = lit_header(s, w.bpos, w.bsize, h);
+            const uint32_t slot = cur;
+            put(ord, e ? 0u : (uint32_t)h.regen, 0, IT_BSTART);
+            if (e) { put(0, 0, (uint32_t)e, IT_ERR); break; }
+            const int32_t end = w.bpos + w.bsize;
+            int32_t ip = w.bpos + h.sec;
+            int32_t nseq = 0, used = 0;
+            e = nbseq_header(s, ip, end, &nseq, &used);
+            if (e) { put(0, 0, (uint32_t)e, IT_ERR); break; }
+            ip += used;
+            w.lb += (int64_t)h.regen + 3 * (int64_t)nseq;
+            if (cblk >= cap_cblk || slot + 3 + (uint32_t)nseq > cap_items) { bug = 1; break; }
+            const uint32_t area = cblk * TAB_CELLS;
+            cblk++;
+            if (nseq > 0) {
+                if (ip + 1 > end) { put(0, 0, (uint32_t)E_SRCSIZE, IT_ERR); break; }
+                uint32_t modes = rd8(s, ip++);
+                if ((modes & 3) && strict_reserved) { put(0, 0, (uint32_t)E_CORRUPT, IT_ERR); break; }
+                int32_t c = seq_table_g(sm, tabs, area, &t_ll, &al_ll, &hv_ll, modes >> 6, s, ip, end - ip, 0);
+                if (c >= 0) { ip += c; c = seq_table_g(sm, tabs, area + 512, &t_of, &al_of, &hv_of, (modes >> 4) & 3, s, ip, end - ip, 1); }
+                if (c >= 0) { ip += c; c = seq_table_g(sm, tabs, area + 768, &t_ml, &al_ml, &hv_ml, (modes >> 2) & 3, s, ip, end - ip, 2); }
+                if (c < 0) { put(0, 0, (uint32_t)E_CORRUPT, IT_ERR); break; }
+                ip += c;
+            }
+            if (l == 0) {
+                GBlk &d = sm.g[gn];
+                d.bs = s + ip;
+                d.in = s;
+                d.ib = items;
+                d.bsz = end - ip;
+                d.nseq = nseq;
+                d.item = slot;
+                d.tll = zi.tab_off + t_ll; d.tof = zi.tab_off + t_of; d.tml = zi.tab_off + t_ml;
+                d.al = (uint32_t)al_ll | ((uint32_t)al_of << 8) | ((uint32_t)al_ml << 16) | ((uint32_t)first << 24);
+            }
+            first = 0;
+            cur = slot + 3 + (uint32_t)nseq;
+            gn++;
+            if (gn == 64) {
+                seq_group(sm, gn, (const gc_u16 *)tabs_all, &e0, &e1, &e2);
+                gn = 0;
+            }
         }
-        if (ev == EV_FEND) {
-            put((uint32_t)w.fcs, (uint32_t)(w.fcs >> 32), chk, IT_FEND | (fl << 8));
-            if (fl & FE_MISSING) break;
-            continue;
-        }
-        const uint32_t ord = w.ordinal - 1;
-        if (w.btype != 2) {
-            put(ord, (uint32_t)w.bsize, 0, IT_BSTART);
-            put((uint32_t)w.bsize, 0, 0, IT_SEQ);
-            put(0, 0, 0, IT_BEND);
-            w.lb += w.bsize;
-            continue;
-        }
-        LitHdr h;
-        int32_t e = lit_header(s, w.bpos, w.bsize, h);
-        const uint32_t slot = cur;
-        put(ord, e ? 0u : (uint32_t)h.regen, 0, IT_BSTART);
-        if (e) { put(0, 0, (uint32_t)e, IT_ERR); break; }
-        const int32_t end = w.bpos + w.bsize;
-        int32_t ip = w.bpos + h.sec;
-        int32_t nseq = 0, used = 0;
-        e = nbseq_header(s, ip, end, &nseq, &used);
-        if (e) { put(0, 0, (uint32_t)e, IT_ERR); break; }
-        ip += used;
-        w.lb += (int64_t)h.regen + 3 * (int64_t)nseq;
-        if (cblk >= cap_cblk || slot + 3 + (uint32_t)nseq > cap_items) { bug = 1; break; }
-        const uint32_t area = cblk * TAB_CELLS;
-        cblk++;
-        if (nseq > 0) {
-            if (ip + 1 > end) { put(0, 0, (uint32_t)E_SRCSIZE, IT_ERR); break; }
-            uint32_t modes = rd8(s, ip++);
-            if ((modes & 3) && strict_reserved) { put(0, 0, (uint32_t)E_CORRUPT, IT_ERR); break; }
-            int32_t c = seq_table_g(sm, tabs, area, &t_ll, &al_ll, &hv_ll, modes >> 6, s, ip, end - ip, 0);
-            if (c >= 0) { ip += c; c = seq_table_g(sm, tabs, area + 512, &t_of, &al_of, &hv_of, (modes >> 4) & 3, s, ip, end - ip, 1); }
-            if (c >= 0) { ip += c; c = seq_table_g(sm, tabs, area + 768, &t_ml, &al_ml, &hv_ml, (modes >> 2) & 3, s, ip, end - ip, 2); }
-            if (c < 0) { put(0, 0, (uint32_t)E_CORRUPT, IT_ERR); break; }
-            ip += c;
-        }
-        if (l == 0) {
-            GBlk &d = sm.g[gn];
-            d.bs = s + ip;
-            d.bsz = end - ip;
-            d.nseq = nseq;
-            d.item = slot;
-            d.tll = t_ll; d.tof = t_of; d.tml = t_ml;
-            d.al = (uint32_t)al_ll | ((uint32_t)al_of << 8) | ((uint32_t)al_ml << 16) | ((uint32_t)first << 24);
-        }
-        first = 0;
-        cur = slot + 3 + (uint32_t)nseq;
-        gn++;
-        if (gn == 64) {
-            seq_group(sm, gn, s, tabs, items, &e0, &e1, &e2);
-            gn = 0;
-        }
+        if (l == 0) zi.n_items = bug ? 0xFFFFFFFFu : cur;
     }
-    if (gn) seq_group(sm, gn, s, tabs, items, &e0, &e1, &e2);
+    if (gn) seq_group(sm, gn, (const gc_u16 *)tabs_all, &e0, &e1, &e2);
     wait_vm();
-    if (l == 0) zi.n_items = bug ? 0xFFFFFFFFu : cur;
 }
 
 // ---------------------------------------------------------------------------
@@ -1801,7 +1812,8 @@ extern "C" int jfs_launch_zstd_decode(const jfs_dev_block *d_blocks, int nblk, i
         return -1;
     hipLaunchKernelGGL(zlit_kernel, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, z.d_info, z.d_lit);
     if (hipGetLastError() != hipSuccess) return -1;
-    hipLaunchKernelGGL(zseq_kernel, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, z.d_info, z.d_tabs, z.d_items,
+    hipLaunchKernelGGL(zseq_kernel, dim3((nblk + ZSEQ_INPUTS - 1) / ZSEQ_INPUTS), dim3(64), 0, stream, d_blocks, nblk,
+                       z.d_info, z.d_tabs, z.d_items,
                        g_strict_reserved);
     if (hipGetLastError() != hipSuccess) return -1;
     hipLaunchKernelGGL(zexec_kernel, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, z.d_info, z.d_lit, z.d_items,
