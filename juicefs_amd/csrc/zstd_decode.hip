@@ -1107,7 +1107,11 @@ __device__ __forceinline__ void seq_group(SeqSmem &sm, int gn, const gc_u16 *tab
                 const uint32_t szl = 1u << all, szo = 1u << alof, szm = 1u << alml;
                 for (int32_t i = 0; i < d.nseq; i++) {
                     if (br_overflow(r)) { it[2 + i] = make_uint4(0, 0, (uint32_t)E_CORRUPT, IT_ERR); break; }
+#ifdef JFS_ZSEQ_NOTAB  // diagnostics only: wrong output
+                    const uint32_t cl = (sll & 63) | (64u << 6), co = (sof & 31) | (32u << 6), cm = (sml & 63) | (64u << 6);
+#else
                     const uint32_t cl = tl[sll], co = to[sof], cm = tm[sml];
+#endif
                     const uint32_t lv = sm.lut_ll[cl & 63], mv = sm.lut_ml[cm & 63], ofc = co & 63;
                     uint32_t ofv = (1u << ofc) + br_read(r, (int)ofc);
                     uint32_t ml = (mv & 0xFFFFFFu) + br_read(r, (int)(mv >> 24));
@@ -1137,7 +1141,9 @@ __device__ __forceinline__ void seq_group(SeqSmem &sm, int gn, const gc_u16 *tab
                         sml = ((nsm << nbm) - szm) + br_read(r, nbm);
                         sof = ((nso << nbo) - szo) + br_read(r, nbo);
                     }
+#ifndef JFS_ZSEQ_NOSTORE  // diagnostics only: wrong output
                     it[2 + i] = make_uint4(ll, ml, off, IT_SEQ);
+#endif
                     if (i + 1 == d.nseq)
                         it[2 + d.nseq] = br_done(r) ? make_uint4(0, 0, 0, IT_BEND)
                                                     : make_uint4(0, 0, (uint32_t)E_CORRUPT, IT_ERR);
