@@ -141,7 +141,29 @@ struct Ctx {
     uint16_t *tab;  // its token table
 };
 
+// dword vectors that are only 4-byte aligned (global_load_dwordx4 / x2 at any dword address)
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2), aligned(4)));
+typedef JFS_GLOBAL const u32x4 gc_x4;
+typedef JFS_GLOBAL const u32x2 gc_x2;
+
 __device__ __forceinline__ uint32_t slot(const Ctx &c, int32_t pos) { return (uint32_t)(pos + (int32_t)c.dmis) & RMASK; }
+
+// Far-match source bytes: the 6 dwords from the dword holding HBM address a.
+// A dword that lies wholly below dst's first dword holds no source byte (only
+// bytes the write mask drops) and is not read: it reads as 0.
+__device__ __forceinline__ void far_load(const Ctx &c, uintptr_t a, uint32_t &d0, uint32_t &d1, uint32_t &d2,
+                                         uint32_t &d3, uint32_t &d4, uint32_t &d5) {
+    const uintptr_t b = a & ~(uintptr_t)3, lo = (uintptr_t)c.dst & ~(uintptr_t)3;
+    const bool under = b < lo;
+    const gc_x4 *q = (const gc_x4 *)(under ? lo : b);
+    const u32x4 v = q[0];
+    const u32x2 w = *(const gc_x2 *)(q + 1);
+    d0 = v.x; d1 = v.y; d2 = v.z; d3 = v.w; d4 = w.x; d5 = w.y;
+    if (__ballot(under)) {
+        if (under) { d5 = d4; d4 = d3; d3 = d2; d2 = d1; d1 = d0; d0 = 0; }
+    }
+}
 
 // ---------------------------------------------------------------------------
 // staging and byte access
@@ -544,9 +566,6 @@ __device__ __forceinline__ void copy16(Smem &s, uint32_t sa, uint32_t da, int32_
           __builtin_amdgcn_alignbyte(r[5], r[4], sh));
 }
 
-__device__ __forceinline__ uint32_t pick5(int32_t q, uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t e) {
-    return q < 0 ? a : q == 0 ? b : q == 1 ? c : q == 2 ? d : e;
-}
 
 // One lane-parallel batch: lanes with act hold consecutive tokens producing
 // output [O0, O1), O1 - O0 <= BSPAN, every ll/ml <= LMAX.
@@ -569,13 +588,13 @@ __device__ __forceinline__ void batch(Smem &s, Ctx &c, bool act, int32_t o, uint
         c.Fw = c.F;
         if (hz + LMAX > c.Fw) c.bug = 4;
     }
-    // far prefetch: the 16-byte line holding the source start, and the next
-    // one only when the first 16 source bytes cross into it
-    uint4 f0 = make_uint4(0, 0, 0, 0), f1 = f0;
-    if (far) {
-        const gc_u4 *q = (const gc_u4 *)((uintptr_t)(c.dst + msrc) & ~(uintptr_t)15);
-        f0 = q[0];
-        if ((int32_t)(((uintptr_t)(c.dst + msrc)) & 15u) + (ml < 16u ? (int32_t)ml : 16) > 16) f1 = q[1];
+    // far prefetch: the 24 bytes from the dword holding source byte (src - ha),
+    // ha = the destination's offset in its dword, so that output dword j is
+    // alignbyte(d[j+1], d[j], sh) with no dword selection
+    uint32_t fd0 = 0, fd1 = 0, fd2 = 0, fd3 = 0, fd4 = 0, fd5 = 0;
+    const uint32_t fha = slot(c, ms) & 3u;
+    if (__ballot(far)) {
+        if (far) far_load(c, (uintptr_t)(c.dst + msrc) - fha, fd0, fd1, fd2, fd3, fd4, fd5);
     }
     // literal runs (source: staged window, addressed as ring + R + litr)
 #ifdef JFS_SKIP_LIT
@@ -598,36 +617,15 @@ __device__ __forceinline__ void batch(Smem &s, Ctx &c, bool act, int32_t o, uint
             PCOUNT(17, 1);
             if (far && k < ml) {
                 const int32_t m = ml - k < 16u ? (int32_t)(ml - k) : 16;
-                const uint32_t da = slot(c, ms + (int32_t)k);
-                uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = 0, w4 = 0;
-                if (far) {
-                    const uintptr_t sA = (uintptr_t)(c.dst + msrc + (int32_t)k) - (da & 3u);
-                    const uintptr_t B = (uintptr_t)(c.dst + msrc + (int32_t)k) & ~(uintptr_t)15;
-                    const int32_t rel = (int32_t)((intptr_t)sA - (intptr_t)B);  // -3..15
-                    const int32_t q = rel >> 2;                                   // -1..3
-                    const uint32_t sh = (uint32_t)rel & 3u;
-                    const uint32_t d0 = f0.x, d1 = f0.y, d2 = f0.z, d3 = f0.w, d4 = f1.x, d5 = f1.y, d6 = f1.z,
-                                   d7 = f1.w;
-                    const uint32_t e0 = pick5(q, 0u, d0, d1, d2, d3), e1 = pick5(q, d0, d1, d2, d3, d4),
-                                   e2 = pick5(q, d1, d2, d3, d4, d5), e3 = pick5(q, d2, d3, d4, d5, d6),
-                                   e4 = pick5(q, d3, d4, d5, d6, d7), e5 = pick5(q, d4, d5, d6, d7, 0u);
-                    w0 = __builtin_amdgcn_alignbyte(e1, e0, sh);
-                    w1 = __builtin_amdgcn_alignbyte(e2, e1, sh);
-                    w2 = __builtin_amdgcn_alignbyte(e3, e2, sh);
-                    w3 = __builtin_amdgcn_alignbyte(e4, e3, sh);
-                    w4 = __builtin_amdgcn_alignbyte(e5, e4, sh);
-                }
-                put16(s, da, m, w0, w1, w2, w3, w4);
+                const uint32_t da = slot(c, ms + (int32_t)k);  // da & 3 == fha
+                const uint32_t sh = (uint32_t)((uintptr_t)(c.dst + msrc + (int32_t)k) - fha) & 3u;
+                put16(s, da, m, __builtin_amdgcn_alignbyte(fd1, fd0, sh), __builtin_amdgcn_alignbyte(fd2, fd1, sh),
+                      __builtin_amdgcn_alignbyte(fd3, fd2, sh), __builtin_amdgcn_alignbyte(fd4, fd3, sh),
+                      __builtin_amdgcn_alignbyte(fd5, fd4, sh));
             }
             const bool more = far && k + 16 < ml;
             if (__ballot(more)) {
-                if (more) {
-                    const g_u8 *sp = c.dst + msrc + (int32_t)k + 16;
-                    const gc_u4 *q = (const gc_u4 *)((uintptr_t)sp & ~(uintptr_t)15);
-                    const uint32_t rest = ml - k - 16;
-                    f0 = q[0];
-                    if ((int32_t)((uintptr_t)sp & 15u) + (rest < 16u ? (int32_t)rest : 16) > 16) f1 = q[1];
-                }
+                if (more) far_load(c, (uintptr_t)(c.dst + msrc + (int32_t)k + 16) - fha, fd0, fd1, fd2, fd3, fd4, fd5);
             }
         }
     }

@@ -234,3 +234,83 @@ def test_lz4_decode_dense_tokens(gpu, oracle):
     res = c.DecompressBatch(pairs)
     for (dst, _), (r, out), (n, err) in zip(pairs, want, res):
         assert err is None and n == r and bytes(dst[:n]) == out
+
+
+def _far_head_stream(rng, pre, src_pos, ml):
+    """Filler tokens up to output `pre`, then one token whose match reads from
+    output position src_pos (0..3) -- a far source in the first dword of dst
+    once the output passes the 4 KiB LDS ring -- then filler and a literal tail."""
+    out = bytearray()
+    produced = 0
+
+    def tok(lits, off, mlen):
+        nonlocal produced
+        ll = len(lits)
+        mcode = mlen - 4
+        t = (min(ll, 15) << 4) | min(mcode, 15)
+        b = bytearray([t])
+        if ll >= 15:
+            r = ll - 15
+            while r >= 255:
+                b.append(255)
+                r -= 255
+            b.append(r)
+        b += lits + off.to_bytes(2, "little")
+        if mcode >= 15:
+            r = mcode - 15
+            while r >= 255:
+                b.append(255)
+                r -= 255
+            b.append(r)
+        produced += ll + mlen
+        return b
+
+    lits = bytes(rng.randrange(256) for _ in range(12))
+    out += tok(lits, 5, 4)
+    while produced + 14 + 40 < pre:
+        out += tok(bytes(rng.randrange(256) for _ in range(10)), rng.randrange(1, 9), 4)
+    ll = max(1, pre - produced)
+    ms = produced + ll
+    out += tok(bytes(rng.randrange(256) for _ in range(ll)), ms - src_pos, ml)
+    for _ in range(20):
+        out += tok(bytes(rng.randrange(256) for _ in range(10)), rng.randrange(1, 9), 4)
+    out += bytes([0xF0, 1]) + bytes(rng.randrange(256) for _ in range(16))
+    return bytes(out)
+
+
+def test_lz4_far_source_at_block_start(gpu, oracle):
+    """Far matches whose source starts in dst's first dword (the far loads must
+    not read below the block's first dword), every dst alignment."""
+    import torch
+    from juicefs_amd import device as D
+    rng = random.Random(5)
+    streams = []
+    for pre in range(4070, 4112, 3):
+        for sp in range(4):
+            streams.append(_far_head_stream(rng, pre, sp, 4 + rng.randrange(40)))
+    want = []
+    for st in streams:
+        r, o = oracle.lz4_decompress(st, 1 << 16)
+        assert r > 0
+        want.append(o[:r])
+    n = len(streams)
+    cap = max(len(w) for w in want)
+    src = torch.zeros(n * (len(max(streams, key=len)) + 32), dtype=torch.uint8, device=gpu)
+    slot_s = len(max(streams, key=len)) + 32
+    offs_s = [i * slot_s for i in range(n)]
+    host = np.zeros(src.numel(), dtype=np.uint8)
+    for i, st in enumerate(streams):
+        host[offs_s[i]:offs_s[i] + len(st)] = np.frombuffer(st, dtype=np.uint8)
+    src.copy_(torch.from_numpy(host))
+    for mis in (0, 1, 2, 3, 5, 13):
+        out = torch.full((n * (cap + 64) + 64,), 0xEE, dtype=torch.uint8, device=gpu)
+        offs_d = [i * (cap + 64) + mis for i in range(n)]
+        desc = D.make_desc(src, offs_s, [len(s) for s in streams], out, offs_d, [len(w) for w in want])
+        ret = torch.empty(n, dtype=torch.int32, device=gpu)
+        D.lz4_decompress(desc, ret)
+        torch.cuda.synchronize()
+        r = ret.cpu().tolist()
+        oh = out.cpu().numpy()
+        for i, w in enumerate(want):
+            assert r[i] == len(w), (mis, i, r[i], len(w))
+            assert oh[offs_d[i]:offs_d[i] + len(w)].tobytes() == w, (mis, i)
