@@ -300,12 +300,12 @@ __device__ __forceinline__ FTok parse_fast(const Smem &s, const Ctx &c, int32_t 
 // output ring <-> HBM
 // ---------------------------------------------------------------------------
 // Write ring[F, to) to dst[F, to).  `to` is a 128-byte aligned HBM boundary
-// (or the block end).  The previous flush is waited for first; Fw tracks the
-// prefix whose stores are known complete.
+// (or the block end).  The stores are not waited for here: Fw (the prefix
+// whose stores are known complete) only advances where an HBM read of the
+// output needs it (far matches, need_flushed), so the copier does not stall
+// on every flush.
 __device__ __forceinline__ void flush(Smem &s, Ctx &c, int32_t to) {
     const int l = lane_id();
-    wait_vm();
-    c.Fw = c.F;
     int32_t F = c.F;
     if (to <= F) return;
     int32_t a = F + (int32_t)((16u - ((c.dmis + (uint32_t)F) & 15u)) & 15u);
