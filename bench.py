@@ -37,6 +37,8 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from juicefs_amd import shard as S  # noqa: E402
+
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
@@ -218,9 +220,8 @@ def host_path_rate(comp_blocks, raw_blocks, U, nblk, reps=2):
 
 def main():
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    env = S.rank_env()
+    world, rank, local = env.world, env.rank, env.local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -231,44 +232,36 @@ def main():
     U, nblk = a.block_bytes, a.blocks
     t_setup = time.perf_counter()
     if a.codec == "lz4":
-        batch = D.Lz4Batch(nblk, U, a.cls, seed_base=1 + rank * nblk, device=dev)
+        batch = D.Lz4Batch(nblk, U, a.cls, seed_base=S.seed_base(rank, nblk), device=dev)
     else:
-        batch = D.ZstdBatch(nblk, U, a.cls, level=a.level, distinct=16, seed_base=1 + rank * 16, device=dev)
+        batch = D.ZstdBatch(nblk, U, a.cls, level=a.level, distinct=16, seed_base=S.seed_base(rank, 16), device=dev)
     C = batch.comp_bytes
     setup_s = time.perf_counter() - t_setup
 
     stream = torch.cuda.current_stream()
-    for _ in range(a.warmup):
-        batch.decompress(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
-    t0 = time.perf_counter()
-    for i in range(a.steps):
-        ev[i][0].record(stream)
-        batch.decompress(stream)
-        ev[i][1].record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    elapsed = float(elapsed.item())
+    k = [0]
+
+    def step():
+        if k[0] >= a.warmup:  # HIP events on the launch stream, timed steps only
+            i = k[0] - a.warmup
+            ev[i][0].record(stream)
+            batch.decompress(stream)
+            ev[i][1].record(stream)
+        else:
+            batch.decompress(stream)
+        k[0] += 1
+
+    # barrier + synchronize on both sides of exactly a.steps steps; max over ranks
+    elapsed = S.timed_steps(step, a.steps, a.warmup, torch.cuda.synchronize, world)
+    elapsed = S.max_over_ranks(elapsed, world, dev)
     kms = [s.elapsed_time(e) for s, e in ev]
     kern_s = float(np.mean(kms)) / 1e3
-    ok = batch.verify()
-    okt = torch.tensor([1 if ok else 0], device=dev)
-    if world > 1:
-        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-    if int(okt.item()) != 1:
+    if not S.all_ranks_ok(batch.verify(), world, dev):
         raise SystemExit("decoded output mismatch: benchmark invalid")
 
     ms_per_step = elapsed / a.steps * 1e3
-    value = world * nblk * U * a.steps / elapsed / 2**30
+    value = S.whole_job_gib_s(world, nblk, U, a.steps, elapsed)
     achieved = (C + nblk * U) / kern_s / 1e9
     traffic = None
     if a.codec == "lz4" and os.path.exists(a.traffic_file):
