@@ -5,6 +5,10 @@ decompression, 4 MiB blocks, 4096 blocks in HBM per GPU (configs[1]).
   python bench.py [--gpus N] [--steps K] [--warmup W]
   torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
 
+`python bench.py --gpus N` with N > 1 and no torchrun environment starts the N
+ranks itself (torch.distributed.run as a child process, before anything here
+touches a GPU) and exits with its status.
+
 A step = one launch of the LZ4 decode kernel over the rank's whole batch.
 Blocks are independent, so ranks shard them with no data-path collective
 (weak scaling: every rank decodes its own 4096 blocks); torch.distributed is
@@ -13,33 +17,50 @@ text-like blocks generated on the GPU and compressed by the GPU
 encoder (byte-identical to LZ4_compress_default) before timing; the decoded
 output is checked against the original on the device after timing.
 
-Extra fields: roofline (HIP-event timed kernel, algorithmic bytes C+U per
-launch vs 8 TB/s; traffic from profiles/traffic.json), cpu_baseline (the CPU
-oracle on this host's cores, bounded sample), cpu_liblz4 (the C library
-pkg/compress wraps, same sample), and with --host-path the PCIe-inclusive rate
-through the C ABI's batch API (kept out of the default run so that every
-decode launch in a default run is the headline launch).
+Sub-records of the same JSON line (each names its BASELINE config):
+  configs_3        Zstd level-3 decode, 4096 x 4 MiB frames in HBM, every rank
+  configs_2        LZ4 compress + decompress, 512 blocks per GPU, block i on
+                   rank i % N (round robin), every block verified, every rank
+  configs_0        LZ4 round trip of 1024 x 4 MiB host blocks through the C ABI
+                   batch entry points (rank 0, N = 1)
+  host_path        PCIe-inclusive LZ4 decompress/compress (rank 0, N = 1)
+  mixed_host_path  configs[4] shape on one GPU (rank 0, N = 1)
+  roofline         HIP-event timed decode kernel vs 8 TB/s; `traffic` from
+                   profiles/traffic.json only while its kernel-source stamp
+                   matches the sources built here
+  cpu_baseline     liblz4 LZ4_decompress_safe (the C code pkg/compress's
+                   go-lz4 wraps) on this host's cores; 1-core figure and the
+                   CPU oracle beside it
 """
 from __future__ import annotations
 
 import argparse
 import ctypes
+import hashlib
 import json
 import os
+import subprocess
 import sys
 import threading
 import time
 
 import numpy as np
-import torch
-import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from juicefs_amd import shard as S  # noqa: E402
-
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+METRIC = "device-resident GiB/s (de)compress, 4 MiB blocks, LZ4+Zstd, 1/2/4/8 MI355X"
+KERNEL_SOURCES = ("juicefs_amd/csrc/lz4_decode.hip", "juicefs_amd/csrc/wave.cuh", "juicefs_amd/csrc/jfs_internal.h")
+
+
+def kernel_src_sha256() -> str:
+    """Stamp of the LZ4 decode kernel sources (profiles/traffic.json carries it)."""
+    h = hashlib.sha256()
+    for p in KERNEL_SOURCES:
+        with open(os.path.join(ROOT, p), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
 
 
 def parse():
@@ -51,15 +72,17 @@ def parse():
     p.add_argument("--block-bytes", type=int, default=4 << 20)
     p.add_argument("--cls", default="T")
     p.add_argument("--codec", default="lz4", choices=["lz4", "zstd"],
-                   help="lz4 = headline (configs[1]); zstd = level-3 decode (configs[3])")
+                   help="headline codec: lz4 = configs[1] (default); zstd = level-3 decode (configs[3])")
     p.add_argument("--level", type=int, default=3, help="zstd level of the generated frames")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--host-path", action="store_true", help="(default) time the PCIe-inclusive batch path")
-    p.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive batch path")
-    p.add_argument("--host-blocks", type=int, default=2048, help="blocks in the --host-path sample")
-    p.add_argument("--no-extras", action="store_true", help="skip the compress-side measurements")
+    p.add_argument("--no-host-path", action="store_true", help="skip the PCIe-inclusive legs (host_path, mixed, configs_0)")
+    p.add_argument("--host-blocks", type=int, default=2048, help="blocks in the host_path sample")
+    p.add_argument("--no-extras", action="store_true", help="skip every sub-record (headline only)")
     p.add_argument("--no-mixed", action="store_true", help="skip configs[4] (mixed LZ4/Zstd 64 KiB-4 MiB, host path)")
     p.add_argument("--mixed-blocks", type=int, default=4096)
+    p.add_argument("--c0-blocks", type=int, default=1024, help="configs[0] blocks (host round trip)")
+    p.add_argument("--c2-blocks", type=int, default=512, help="configs[2] blocks per GPU")
+    p.add_argument("--zstd-steps", type=int, default=3, help="timed launches of the configs[3] sub-record")
     p.add_argument("--extra-blocks", type=int, default=1024, help="blocks in the Zstd compress sample")
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="wall budget per CPU baseline leg")
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
@@ -74,9 +97,78 @@ def host_threads() -> int:
     return max(1, min(16, n))  # the GPU box's CPU share is 16
 
 
-def cpu_baseline(comp_blocks, U, seconds, codec="lz4"):
-    """Time the CPU oracle (test infrastructure, kind "port") decompressing a
-    bounded sample of the same compressed blocks on this host's cores."""
+def _spawn_ranks(n: int) -> int:
+    """`--gpus N` without a torchrun environment: run N ranks (one per GPU)
+    under torch.distributed.run as a child process; nothing in this process has
+    touched a GPU yet."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd, env=dict(os.environ)).returncode
+
+
+# ---------------------------------------------------------------------------
+# CPU legs (bounded samples, rank 0 at N = 1)
+# ---------------------------------------------------------------------------
+def _timed_threads(work_one, T, seconds):
+    """Run work_one(t, k) on T threads until `seconds` elapse; returns (calls, wall)."""
+    counts = [0] * T
+    stop = [False]
+
+    def work(t):
+        k = t
+        while not stop[0]:
+            work_one(t, k)
+            counts[t] += 1
+            k += T
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(T)]
+    t0 = time.perf_counter()
+    [x.start() for x in th]
+    time.sleep(seconds)
+    stop[0] = True
+    [x.join() for x in th]
+    return sum(counts), time.perf_counter() - t0
+
+
+def _liblz4():
+    for path in ("/opt/conda/lib/liblz4.so.1", "/usr/lib/x86_64-linux-gnu/liblz4.so.1"):
+        if os.path.exists(path):
+            lz = ctypes.CDLL(path)
+            lz.path = path
+            return lz
+    return None
+
+
+def liblz4_baseline(comp_blocks, U, seconds, threads):
+    """LZ4_decompress_safe from the host's liblz4 -- the C routine pkg/compress
+    reaches through go-lz4 (compress.go:120-125; this image has 1.9.3, the
+    reference vendors a 2017 copy).  ctypes releases the GIL, so the threads
+    decode in parallel; one block stream per thread."""
+    lz = _liblz4()
+    if lz is None:
+        return None
+    bufs = [ctypes.create_string_buffer(c, len(c)) for c in comp_blocks]
+    outs = [ctypes.create_string_buffer(U) for _ in range(threads)]
+
+    def one(t, k):
+        c = bufs[k % len(bufs)]
+        r = lz.LZ4_decompress_safe(c, outs[t], len(c), U)
+        assert r == U
+
+    nb, dt = _timed_threads(one, threads, seconds)
+    return {"value": nb * U / dt / 2**30, "unit": "GiB/s", "cores": threads, "kind": "reference",
+            "library": f"{lz.path} v{lz.LZ4_versionNumber()}",
+            "sample": f"{nb} LZ4_decompress_safe calls over {len(bufs)} distinct 4 MiB text blocks (the headline's "
+                      f"own compressed blocks), {threads} threads, {dt:.1f} s wall"}
+
+
+def oracle_baseline(comp_blocks, U, seconds, codec="lz4"):
+    """The CPU oracle (test infrastructure, oracle/*.c at -O2) on the same
+    sample: reported beside the library, never the thing measured."""
     from tests.oracle_ctypes import Oracle
     so = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
     if not os.path.exists(so):
@@ -84,69 +176,19 @@ def cpu_baseline(comp_blocks, U, seconds, codec="lz4"):
     orc = Oracle(so)
     T = host_threads()
     bufs = [ctypes.create_string_buffer(c, len(c)) for c in comp_blocks]
-    counts = [0] * T
-    stop = [False]
+    outs = [ctypes.create_string_buffer(U) for _ in range(T)]
 
-    def work(t):
-        out = ctypes.create_string_buffer(U)
-        k = t
-        while not stop[0]:
-            c = bufs[k % len(bufs)]
-            if codec == "lz4":
-                r = orc.lib.oracle_lz4_decompress_safe(c, out, len(c), U)
-            else:
-                r = orc.lib.oracle_zstd_decompress(c, len(c), out, U)
-            assert r == U
-            counts[t] += 1
-            k += T
+    def one(t, k):
+        c = bufs[k % len(bufs)]
+        if codec == "lz4":
+            r = orc.lib.oracle_lz4_decompress_safe(c, outs[t], len(c), U)
+        else:
+            r = orc.lib.oracle_zstd_decompress(c, len(c), outs[t], U)
+        assert r == U
 
-    # size the run: each thread loops over the sample until the time budget ends
-    th = [threading.Thread(target=work, args=(t,)) for t in range(T)]
-    t0 = time.perf_counter()
-    [x.start() for x in th]
-    time.sleep(seconds)
-    stop[0] = True
-    [x.join() for x in th]
-    dt = time.perf_counter() - t0
-    nb = sum(counts)
+    nb, dt = _timed_threads(one, T, seconds)
     return {"value": nb * U / dt / 2**30, "unit": "GiB/s", "cores": T, "kind": "port",
-            "sample": f"{nb} decodes of {len(bufs)} distinct 4 MiB text blocks (oracle/{codec}_oracle.c, -O2), "
-                      f"{T} threads, {dt:.1f} s wall"}
-
-
-def liblz4_baseline(comp_blocks, U, seconds):
-    """The C library pkg/compress reaches through cgo (LZ4_decompress_safe), if
-    the host has one; reported beside the oracle."""
-    for path in ("/opt/conda/lib/liblz4.so.1", "/usr/lib/x86_64-linux-gnu/liblz4.so.1"):
-        if os.path.exists(path):
-            break
-    else:
-        return None
-    lz = ctypes.CDLL(path)
-    T = host_threads()
-    bufs = [ctypes.create_string_buffer(c, len(c)) for c in comp_blocks]
-    counts = [0] * T
-    stop = [False]
-
-    def work(t):
-        out = ctypes.create_string_buffer(U)
-        k = t
-        while not stop[0]:
-            c = bufs[k % len(bufs)]
-            r = lz.LZ4_decompress_safe(c, out, len(c), U)
-            assert r == U
-            counts[t] += 1
-            k += T
-
-    th = [threading.Thread(target=work, args=(t,)) for t in range(T)]
-    t0 = time.perf_counter()
-    [x.start() for x in th]
-    time.sleep(seconds)
-    stop[0] = True
-    [x.join() for x in th]
-    dt = time.perf_counter() - t0
-    return {"value": sum(counts) * U / dt / 2**30, "unit": "GiB/s", "cores": T,
-            "library": f"{path} v{lz.LZ4_versionNumber()}"}
+            "sample": f"{nb} decodes of {len(bufs)} distinct 4 MiB text blocks (oracle/{codec}_oracle.c), {T} threads"}
 
 
 def libzstd_baseline(comp_blocks, U, seconds):
@@ -159,35 +201,25 @@ def libzstd_baseline(comp_blocks, U, seconds):
     z.ZSTD_versionNumber.restype = ctypes.c_uint
     T = host_threads()
     bufs = [ctypes.create_string_buffer(c, len(c)) for c in comp_blocks]
-    counts = [0] * T
-    stop = [False]
+    outs = [ctypes.create_string_buffer(U) for _ in range(T)]
 
-    def work(t):
-        out = ctypes.create_string_buffer(U)
-        k = t
-        while not stop[0]:
-            c = bufs[k % len(bufs)]
-            r = z.ZSTD_decompress(out, U, c, len(c))
-            assert r == U
-            counts[t] += 1
-            k += T
+    def one(t, k):
+        c = bufs[k % len(bufs)]
+        assert z.ZSTD_decompress(outs[t], U, c, len(c)) == U
 
-    th = [threading.Thread(target=work, args=(t,)) for t in range(T)]
-    t0 = time.perf_counter()
-    [x.start() for x in th]
-    time.sleep(seconds)
-    stop[0] = True
-    [x.join() for x in th]
-    dt = time.perf_counter() - t0
-    return {"value": sum(counts) * U / dt / 2**30, "unit": "GiB/s", "cores": T,
+    nb, dt = _timed_threads(one, T, seconds)
+    return {"value": nb * U / dt / 2**30, "unit": "GiB/s", "cores": T, "kind": "reference",
             "library": f"{z.path} v{z.ZSTD_versionNumber()}"}
 
 
+# ---------------------------------------------------------------------------
+# host-buffer legs (C ABI batch entry points: what the cgo drop-in calls)
+# ---------------------------------------------------------------------------
 def host_path_rate(comp_blocks, raw_blocks, U, nblk, reps=2):
     """PCIe-inclusive: Go-heap-like host buffers -> pinned -> HBM -> kernel ->
-    pinned -> host buffers, via the C ABI batch entry points (what the cgo
-    drop-in calls), chunked and pipelined over two streams (capi.hip run_batch).
-    Timed with the host clock around the whole call; best of `reps`."""
+    pinned -> host buffers, via the C ABI batch entry points, chunked and
+    pipelined over two streams (capi.hip run_batch).  Host clock around the
+    whole call; best of `reps`."""
     from juicefs_amd import compress as C
     c = C.LZ4()
     k = max(1, nblk // len(comp_blocks))
@@ -203,31 +235,77 @@ def host_path_rate(comp_blocks, raw_blocks, U, nblk, reps=2):
         res_d = max(res_d, len(pairs) * U / dt / 2**30)
     del pairs
     bound = c.CompressBound(U)
-    ncb = min(nblk, 512)  # the encoder is latency-bound per block: a smaller sample
+    ncb = min(nblk, 1024)
     raws = (raw_blocks * (ncb // len(raw_blocks) + 1))[:ncb]
     cpairs = [(bytearray(bound), rb) for rb in raws]
-    res_c = 0.0
-    for _ in range(1):
-        t0 = time.perf_counter()
-        res = c.CompressBatch(cpairs)
-        dt = time.perf_counter() - t0
-        assert all(n > 0 and e is None for n, e in res)
-        res_c = max(res_c, len(cpairs) * U / dt / 2**30)
+    t0 = time.perf_counter()
+    res = c.CompressBatch(cpairs)
+    dt = time.perf_counter() - t0
+    assert all(n > 0 and e is None for n, e in res)
     return {"lz4_decompress": {"value": res_d, "unit": "GiB/s"},
-            "lz4_compress": {"value": res_c, "unit": "GiB/s"},
+            "lz4_compress": {"value": len(cpairs) * U / dt / 2**30, "unit": "GiB/s"},
             "blocks": nblk, "compress_blocks": ncb, "chunk_mb": int(os.environ.get("JFS_HOST_CHUNK_MB", "2048")),
             "path": "jfs_{de,}compress_batch: host buffers -> pinned (16 threads) -> H2D -> kernel -> D2H -> "
                     "host buffers, 2-stream chunk pipeline, 1 GPU, GiB/s of uncompressed bytes"}
 
 
+def configs0_roundtrip(dev, nblk, U, seed_base=90001):
+    """BASELINE configs[0]: LZ4 round trip of nblk x 4 MiB synthetic host
+    blocks through the pkg/compress-shaped C ABI (jfs_compress_batch then
+    jfs_decompress_batch; the cgo drop-in's batch form).  Every decoded block
+    is compared with its source; the compressed bytes of every block are
+    compared with the device-resident encoder's output for the same block."""
+    import torch
+    from juicefs_amd import compress as C
+    from juicefs_amd import device as D
+    raw = np.empty(nblk * U, dtype=np.uint8)
+    per = 256
+    dbuf = torch.empty(per * U, dtype=torch.uint8, device=dev)
+    for s in range(0, nblk, per):
+        k = min(per, nblk - s)
+        D.gen_blocks(dbuf, k, U, "T", seed_base + s)
+        raw[s * U:(s + k) * U] = dbuf[:k * U].cpu().numpy()
+    del dbuf
+    c = C.LZ4()
+    bound = c.CompressBound(U)
+    comp = np.zeros(nblk * bound, dtype=np.uint8)
+    pairs = [(comp[i * bound:(i + 1) * bound], raw[i * U:(i + 1) * U]) for i in range(nblk)]
+    t0 = time.perf_counter()
+    res = c.CompressBatch(pairs)
+    tc = time.perf_counter() - t0
+    sizes = [n for n, e in res]
+    if any(e is not None or n <= 0 for n, e in res):
+        raise RuntimeError("configs[0] compress failed")
+    out = np.zeros(nblk * U, dtype=np.uint8)
+    dpairs = [(out[i * U:(i + 1) * U], comp[i * bound:i * bound + sizes[i]]) for i in range(nblk)]
+    t0 = time.perf_counter()
+    res = c.DecompressBatch(dpairs)
+    td = time.perf_counter() - t0
+    if any(e is not None or n != U for n, e in res) or not np.array_equal(out, raw):
+        raise RuntimeError("configs[0] round trip mismatch")
+    # compressed bytes == the device-resident encoder's (a sample of 64 blocks)
+    ns = min(64, nblk)
+    b = D.Lz4Batch(ns, U, "T", seed_base=seed_base, device=dev)
+    dcomp = b.comp.cpu().numpy()
+    same = all(int(b.csize[i]) == sizes[i] and
+               np.array_equal(dcomp[i * b.slot:i * b.slot + sizes[i]], comp[i * bound:i * bound + sizes[i]])
+               for i in range(ns))
+    if not same:
+        raise RuntimeError("configs[0] host-path bytes differ from the device encoder")
+    total = nblk * U
+    return {"value": total / (tc + td) / 2**30, "unit": "GiB/s",
+            "compress": {"value": total / tc / 2**30, "unit": "GiB/s", "s": tc},
+            "decompress": {"value": total / td / 2**30, "unit": "GiB/s", "s": td},
+            "blocks": nblk, "ratio": total / float(sum(sizes)),
+            "verified": "every block decoded == source; compressed bytes == device encoder on 64 blocks",
+            "path": "BASELINE configs[0] through the C ABI batch surface (host buffers, pinned staging, GPU kernels); "
+                    "value = uncompressed bytes / (compress s + decompress s)"}
+
+
 def mixed_host_path(raw_src, nblk=4096, seed=11):
     """BASELINE configs[4] on one GPU: mixed LZ4/Zstd blocks of 64 KiB-4 MiB
     (log-uniform sizes, codec alternating), host buffers in and out through the
-    C-ABI batch entry points (pinned staging, async H2D/D2H, capi.hip
-    run_batch).  Compress = the GPU encoders (LZ4 byte-identical to
-    LZ4_compress_default; Zstd level-1-style frames); decompress = the GPU
-    decoders; every block is checked against its source.  GiB/s of
-    uncompressed bytes over the whole mixed job (both codecs, host clock)."""
+    C ABI batch entry points.  Every block is checked against its source."""
     from juicefs_amd import compress as C
     rng = np.random.default_rng(seed)
     lo, hi = 64 << 10, 4 << 20
@@ -266,10 +344,105 @@ def mixed_host_path(raw_src, nblk=4096, seed=11):
                     "GPU encoders and decoders, every block verified"}
 
 
+# ---------------------------------------------------------------------------
+# device-resident sub-records (every rank)
+# ---------------------------------------------------------------------------
+def timed_launches(fn, steps, warmup, S, world, dev):
+    """warmup + exactly `steps` launches between barriers; (max wall over
+    ranks, mean HIP-event ms per launch on the launch stream)."""
+    import torch
+    stream = torch.cuda.current_stream()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    k = [0]
+
+    def step():
+        if k[0] >= warmup:
+            i = k[0] - warmup
+            ev[i][0].record(stream)
+            fn(stream)
+            ev[i][1].record(stream)
+        else:
+            fn(stream)
+        k[0] += 1
+
+    el = S.timed_steps(step, steps, warmup, torch.cuda.synchronize, world)
+    el = S.max_over_ranks(el, world, dev)
+    return el, float(np.mean([s.elapsed_time(e) for s, e in ev]))
+
+
+def configs3_zstd(a, S, world, rank, dev):
+    """BASELINE configs[3]: Zstd level-3 decode of 4096 x 4 MiB frames in HBM."""
+    from juicefs_amd import device as D
+    zb = D.ZstdBatch(a.blocks, a.block_bytes, a.cls, level=a.level, distinct=16, seed_base=S.seed_base(rank, 16),
+                     device=dev)
+    el, kms = timed_launches(zb.decompress, a.zstd_steps, 1, S, world, dev)
+    if not S.all_ranks_ok(zb.verify(), world, dev):
+        raise RuntimeError("configs[3] decoded output mismatch")
+    U = a.block_bytes
+    return {"config": f"Zstd level-{a.level} decode, {a.blocks}x4MiB frames in HBM per GPU (BASELINE configs[3])",
+            "value": S.whole_job_gib_s(world, a.blocks, U, a.zstd_steps, el), "unit": "GiB/s",
+            "ms_per_step": el / a.zstd_steps * 1e3, "steps": a.zstd_steps, "n_gpus": world,
+            "kernel_ms": kms, "ratio": a.blocks * U / zb.comp_bytes,
+            "roofline": {"bound": "hbm", "achieved": (zb.comp_bytes + a.blocks * U) / (kms / 1e3) / 1e9,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": (zb.comp_bytes + a.blocks * U) / (kms / 1e3) / 1e9 / HBM_PEAK_GBS},
+            "data": "synthetic text-like, 16 distinct blocks compressed by the host libzstd, replicated",
+            "verified": "every frame's output compared with its source"}
+
+
+def configs2_roundtrip(a, S, world, rank, dev):
+    """BASELINE configs[2]: LZ4 compress + decompress of 4 MiB blocks dealt
+    round-robin over the GPUs (block i -> rank i % N); a step = one encode
+    launch + one decode launch over the rank's share, device-resident."""
+    from juicefs_amd import device as D
+    nb = a.c2_blocks
+    # global block i = rank + N*j: the rank's share of a round-robin deal
+    b = D.Lz4Batch(nb, a.block_bytes, a.cls, seed_base=700001 + rank * nb, device=dev)
+
+    def step(stream):
+        b.compress(stream)
+        b.decompress(stream)
+
+    el, kms = timed_launches(step, 3, 1, S, world, dev)
+    if not S.all_ranks_ok(b.verify(), world, dev):
+        raise RuntimeError("configs[2] round trip mismatch")
+    U = a.block_bytes
+    return {"config": f"LZ4 compress + decompress, {nb} x 4 MiB blocks per GPU, round-robin over {world} GPU(s) "
+                      f"(BASELINE configs[2])",
+            "value": S.whole_job_gib_s(world, nb, U, 3, el), "unit": "GiB/s",
+            "ms_per_step": el / 3 * 1e3, "n_gpus": world, "blocks_per_gpu": nb,
+            "step_kernel_ms": kms,
+            "note": "value = uncompressed bytes / (encode + decode time) over all ranks; every block's compressed "
+                    "size and decoded bytes verified"}
+
+
+def measured_traffic(path, nblk, U):
+    """HBM bytes per launch from profiles/traffic.json, only if it was
+    measured on these kernel sources at this workload."""
+    try:
+        tj = json.load(open(path))
+    except Exception:
+        return None, "no traffic file"
+    if tj.get("blocks") != nblk or tj.get("block_bytes") != U:
+        return None, "traffic file is for another workload"
+    if tj.get("kernel_src_sha256") != kernel_src_sha256():
+        return None, "traffic file is stale (kernel sources changed since it was measured)"
+    return tj.get("hbm_bytes_per_launch"), f"rocprofv3 PMC at {tj.get('git_head')}"
+
+
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(_spawn_ranks(a.gpus))
+
+    import torch
+    import torch.distributed as dist
+
+    from juicefs_amd import shard as S
     env = S.rank_env()
     world, rank, local = env.world, env.rank, env.local
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -286,51 +459,28 @@ def main():
     C = batch.comp_bytes
     setup_s = time.perf_counter() - t_setup
 
-    stream = torch.cuda.current_stream()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
-    k = [0]
-
-    def step():
-        if k[0] >= a.warmup:  # HIP events on the launch stream, timed steps only
-            i = k[0] - a.warmup
-            ev[i][0].record(stream)
-            batch.decompress(stream)
-            ev[i][1].record(stream)
-        else:
-            batch.decompress(stream)
-        k[0] += 1
-
     # barrier + synchronize on both sides of exactly a.steps steps; max over ranks
-    elapsed = S.timed_steps(step, a.steps, a.warmup, torch.cuda.synchronize, world)
-    elapsed = S.max_over_ranks(elapsed, world, dev)
-    kms = [s.elapsed_time(e) for s, e in ev]
-    kern_s = float(np.mean(kms)) / 1e3
+    elapsed, kms = timed_launches(batch.decompress, a.steps, a.warmup, S, world, dev)
+    kern_s = kms / 1e3
     if not S.all_ranks_ok(batch.verify(), world, dev):
         raise SystemExit("decoded output mismatch: benchmark invalid")
 
     ms_per_step = elapsed / a.steps * 1e3
     value = S.whole_job_gib_s(world, nblk, U, a.steps, elapsed)
     achieved = (C + nblk * U) / kern_s / 1e9
-    traffic = None
-    if a.codec == "lz4" and os.path.exists(a.traffic_file):
-        try:
-            tj = json.load(open(a.traffic_file))
-            if tj.get("blocks") == nblk and tj.get("block_bytes") == U:
-                traffic = tj.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    traffic, traffic_src = (None, "not measured for zstd")
     if a.codec == "lz4":
+        traffic, traffic_src = measured_traffic(a.traffic_file, nblk, U)
         workload = "LZ4 decompress, 4096x4MiB blocks already in HBM (BASELINE configs[1])"
         kernel = "jfs::lz4d::lz4_decode_kernel"
         data = "synthetic (text-like blocks generated on GPU, SURVEY.md 8d; LZ4-compressed on GPU)"
     else:
         workload = f"Zstd level-{a.level} decompress, {nblk}x4MiB frames already in HBM (BASELINE configs[3])"
-        kernel = "zscan + zentropy + zexec (whole jfs_zstd_decompress_device call)"
+        kernel = "zscan + zlit + zseq + zexec (whole jfs_zstd_decompress_device call)"
         data = (f"synthetic text-like blocks (SURVEY.md 8d), {batch.distinct} distinct, compressed on the host by "
                 f"libzstd level {a.level}, replicated to {nblk} frames")
-        traffic = None
     out = {
-        "metric": "device-resident GiB/s (de)compress, 4 MiB blocks, LZ4+Zstd, 1/2/4/8 MI355X",
+        "metric": METRIC,
         "value": value,
         "unit": "GiB/s",
         "n_gpus": world,
@@ -350,56 +500,67 @@ def main():
         },
         "roofline": {
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-            "kernel": kernel, "kernel_ms": kern_s * 1e3,
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+            "kernel": kernel, "kernel_ms": kms,
             "algorithmic_bytes_per_launch": C + nblk * U,
             "u_only_TBps": nblk * U / kern_s / 1e12,
         },
         "setup_s": setup_s,
     }
+    extras = not a.no_extras
+    if extras and a.codec == "lz4":
+        try:
+            out["configs_3"] = configs3_zstd(a, S, world, rank, dev)
+        except Exception as e:  # report, never fake
+            out["configs_3"] = {"error": repr(e)}
+        try:
+            out["configs_2"] = configs2_roundtrip(a, S, world, rank, dev)
+        except Exception as e:
+            out["configs_2"] = {"error": repr(e)}
     if rank == 0 and world == 1:
-        # bounded sample for the CPU legs: 32 distinct blocks
+        # bounded sample for the CPU legs: 32 distinct blocks of the headline batch
         ns = min(32, nblk)
-        comp_blocks = []
-        for i in range(ns):
-            s0 = i * batch.slot
-            comp_blocks.append(batch.comp[s0:s0 + int(batch.csize[i])].cpu().numpy().tobytes())
+        comp_blocks = [batch.comp[i * batch.slot:i * batch.slot + int(batch.csize[i])].cpu().numpy().tobytes()
+                       for i in range(ns)]
         if not a.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(comp_blocks, U, a.cpu_seconds, a.codec)
+            T = host_threads()
             if a.codec == "lz4":
-                lb = liblz4_baseline(comp_blocks, U, a.cpu_seconds / 2)
-                if lb:
-                    out["cpu_liblz4"] = lb
+                cb = liblz4_baseline(comp_blocks, U, a.cpu_seconds, T)
+                if cb is not None:
+                    one = liblz4_baseline(comp_blocks, U, a.cpu_seconds / 3, 1)
+                    cb["one_core"] = {"value": one["value"], "unit": "GiB/s"} if one else None
+                    out["cpu_baseline"] = cb
+                out["cpu_oracle"] = oracle_baseline(comp_blocks, U, a.cpu_seconds / 3, a.codec)
             else:
-                lb = libzstd_baseline(comp_blocks, U, a.cpu_seconds / 2)
-                if lb:
-                    out["cpu_libzstd"] = lb
-        if not a.no_extras:
-            ex = {}
-            if a.codec == "lz4":
-                ex["lz4_compress"] = {"value": nblk * U / (batch.enc_ms / 1e3) / 2**30, "unit": "GiB/s",
-                                      "kernel_ms": batch.enc_ms, "blocks": nblk,
-                                      "note": "one GPU LZ4 encode launch (byte-identical to LZ4_compress_default)"}
+                out["cpu_baseline"] = libzstd_baseline(comp_blocks, U, a.cpu_seconds)
+                out["cpu_oracle"] = oracle_baseline(comp_blocks, U, a.cpu_seconds / 3, a.codec)
+        if extras and a.codec == "lz4":
+            ex = {"lz4_compress": {"value": nblk * U / (batch.enc_ms / 1e3) / 2**30, "unit": "GiB/s",
+                                   "kernel_ms": batch.enc_ms, "blocks": nblk,
+                                   "note": "one GPU LZ4 encode launch (byte-identical to LZ4_compress_default)"}}
             try:
                 zr, zratio, zms = D.zstd_compress_rate(min(a.extra_blocks, nblk), U, a.cls, seed_base=7, device=dev)
                 ex["zstd_compress"] = {"value": zr, "unit": "GiB/s", "ratio": zratio, "kernel_ms": zms,
                                        "blocks": min(a.extra_blocks, nblk),
                                        "note": "one GPU Zstd encode launch; frames verified by the GPU decoder"}
             except Exception as e:  # report, never fake
-                ex["zstd_compress"] = {"error": str(e)}
+                ex["zstd_compress"] = {"error": repr(e)}
             out["compress"] = ex
-        if not a.no_host_path and a.codec == "lz4" and rank == 0:
-            try:
-                raw_blocks = [batch.raw[i * U:(i + 1) * U].cpu().numpy().tobytes() for i in range(len(comp_blocks))]
-                out["host_path"] = host_path_rate(comp_blocks, raw_blocks, U, a.host_blocks)
-            except Exception as e:  # report, never fake
-                out["host_path"] = {"error": str(e)}
-        if not a.no_mixed and not a.no_host_path and a.codec == "lz4" and rank == 0:
-            try:
-                src = [batch.raw[i * U:(i + 1) * U].cpu().numpy().tobytes() for i in range(min(32, nblk))]
-                out["mixed_host_path"] = mixed_host_path(src, a.mixed_blocks)
-            except Exception as e:  # report, never fake
-                out["mixed_host_path"] = {"error": str(e)}
+            if not a.no_host_path:
+                raw_blocks = [batch.raw[i * U:(i + 1) * U].cpu().numpy().tobytes() for i in range(ns)]
+                try:
+                    out["configs_0"] = configs0_roundtrip(dev, a.c0_blocks, U)
+                except Exception as e:
+                    out["configs_0"] = {"error": repr(e)}
+                try:
+                    out["host_path"] = host_path_rate(comp_blocks, raw_blocks, U, a.host_blocks)
+                except Exception as e:
+                    out["host_path"] = {"error": repr(e)}
+                if not a.no_mixed:
+                    try:
+                        out["mixed_host_path"] = mixed_host_path(raw_blocks, a.mixed_blocks)
+                    except Exception as e:
+                        out["mixed_host_path"] = {"error": repr(e)}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -44,6 +44,7 @@ extern "C" {
 #define JFS_ERR_NO_DEVICE (JFS_ERR_BASE - 6)     /* no usable gfx950 device; the library never falls back to CPU */
 #define JFS_ERR_INVALID (JFS_ERR_BASE - 7)       /* bad argument (unknown algo, negative size, ...) */
 #define JFS_ERR_HIP (JFS_ERR_BASE - 8)           /* HIP runtime failure */
+#define JFS_ERR_NO_MEMORY (JFS_ERR_BASE - 9)     /* pinned/HBM staging for this block could not be allocated */
 
 /* ---- Compressor surface (one synchronous call per block) ---------------- */
 
@@ -80,8 +81,12 @@ int64_t jfs_decompress(int algo, uint8_t *dst, int64_t dst_cap, const uint8_t *s
  * Blocks are independent; they are dealt round-robin over the devices in
  * device_mask (bit d = device d; 0 = all visible devices) and staged through
  * pinned host memory with async copies.  out_n[i] receives what the
- * single-block call would have returned for block i.  Returns JFS_OK or a
- * JFS_ERR_* code for failures that are not per-block. */
+ * single-block call would have returned for block i.  Errors are per block: a
+ * batch that fails as a whole (staging allocation, copy or launch failure) is
+ * re-run block by block, so only the blocks that fail on their own report
+ * JFS_ERR_NO_MEMORY / JFS_ERR_HIP.  Returns JFS_OK, or JFS_ERR_INVALID /
+ * JFS_ERR_NO_DEVICE for a call that cannot run at all.  The calling thread's
+ * current HIP device is unchanged on return. */
 typedef struct jfs_iov {
     const uint8_t *src;
     int64_t src_len;
@@ -93,10 +98,11 @@ int64_t jfs_compress_batch(int algo, int nblk, const jfs_iov *iov, int64_t *out_
 int64_t jfs_decompress_batch(int algo, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t device_mask);
 
 /* ---- Device-resident surface (inputs/outputs already in HBM) ------------
- * One descriptor per block; all pointers are device pointers on the current
- * device.  ret[i] is written with the single-block result.  Asynchronous on
- * `stream`.  `scratch`/`scratch_bytes` as returned by jfs_*_scratch_size (may
- * be 0 when that returns 0). */
+ * One descriptor per block; all pointers are device pointers on the calling
+ * thread's current device, and `stream` (0 = the null stream) belongs to it.
+ * ret[i] is written with the single-block result.  The LZ4 calls and the Zstd
+ * decompress call are asynchronous on `stream` (they only enqueue work);
+ * jfs_zstd_compress_device is host-synchronous (per-device scratch, locked). */
 typedef struct jfs_dev_block {
     const uint8_t *src;
     uint8_t *dst;
@@ -111,10 +117,25 @@ int64_t jfs_zstd_decompress_device(const jfs_dev_block *d_blocks, int nblk, int3
  * Synchronous with respect to `stream` (it uses per-device scratch). */
 int64_t jfs_zstd_compress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream);
 
+/* CRC-32C (Castagnoli) of device-resident blocks.
+ * d_blocks[i].src / src_len: the data.  d_crc[i] (if d_crc != NULL) receives
+ * crc32.Update(0, crc32c, data), the object checksum of
+ * pkg/object/checksum.go:30-45.  If seg_bytes > 0 (a multiple of 4096; JuiceFS
+ * uses 32768), d_blocks[i].dst receives the disk-cache checksum layout of
+ * pkg/chunk/disk_cache_file.go:139-152: the big-endian CRC-32C of every
+ * seg_bytes piece, ((len-1)/seg_bytes+1)*4 bytes (4 zero bytes for len 0);
+ * dst_cap must hold them.  d_ret[i] (if non-NULL) = bytes written to dst, or
+ * -1 for a bad descriptor.  Asynchronous on `stream`. */
+int64_t jfs_crc32c_device(const jfs_dev_block *d_blocks, int nblk, int32_t seg_bytes, uint32_t *d_crc,
+                          int32_t *d_ret, void *stream);
+
 /* ---- Runtime / utilities ------------------------------------------------- */
 
 /* Number of usable gfx950 devices (0 when none; never an error). */
 int jfs_device_count(void);
+/* Free the batch path's pinned host + HBM staging now (it is also released
+ * after JFS_STAGING_IDLE_MS, default 15000, of no batch activity). */
+void jfs_release_staging(void);
 /* Library version string. */
 const char *jfs_version(void);
 

@@ -23,13 +23,14 @@ JFS_ERR_UNSUPPORTED = JFS_ERR_BASE - 5
 JFS_ERR_NO_DEVICE = JFS_ERR_BASE - 6
 JFS_ERR_INVALID = JFS_ERR_BASE - 7
 JFS_ERR_HIP = JFS_ERR_BASE - 8
+JFS_ERR_NO_MEMORY = JFS_ERR_BASE - 9
 
 # every symbol include/jfs_gpucodec.h declares
 EXPORTS = [
     "jfs_codec_from_name", "jfs_codec_name", "jfs_compress_bound", "jfs_compress", "jfs_decompress",
     "jfs_compress_batch", "jfs_decompress_batch", "jfs_lz4_decompress_device", "jfs_lz4_compress_device",
     "jfs_zstd_decompress_device", "jfs_zstd_compress_device", "jfs_device_count", "jfs_version", "jfs_gen_blocks_device",
-    "jfs_gen_block_host",
+    "jfs_gen_block_host", "jfs_release_staging", "jfs_crc32c_device",
 ]
 
 
@@ -71,6 +72,10 @@ def load() -> ctypes.CDLL:
               lib.jfs_zstd_compress_device):
         f.argtypes = [vp, ctypes.c_int, vp, vp]
         f.restype = i64
+    lib.jfs_crc32c_device.argtypes = [vp, ctypes.c_int, ctypes.c_int32, vp, vp, vp]
+    lib.jfs_crc32c_device.restype = i64
+    lib.jfs_release_staging.argtypes = []
+    lib.jfs_release_staging.restype = None
     lib.jfs_device_count.argtypes = []
     lib.jfs_device_count.restype = ctypes.c_int
     lib.jfs_version.argtypes = []

@@ -43,6 +43,17 @@ inline int64_t align16(int64_t x) { return (x + 15) & ~(int64_t)15; }
 // of a batch uses slot k % NSLOT, so chunk k+1's H2D and chunk k-1's D2H run
 // while chunk k's kernel runs (and kernels of neighbouring chunks overlap).
 constexpr int NSLOT = 3;
+
+// Upper bound on one slot's staging (JFS_STAGING_MAX_MB; default none): a
+// request that needs more fails alone with JFS_ERR_NO_MEMORY.
+int64_t staging_max_bytes() {
+    static int64_t v = [] {
+        const char *e = getenv("JFS_STAGING_MAX_MB");
+        return e ? (int64_t)atoll(e) << 20 : INT64_MAX;
+    }();
+    return v;
+}
+
 struct Slot {
     hipStream_t st = nullptr;  // this slot's kernels
     hipEvent_t ev_in = nullptr, ev_k = nullptr, ev = nullptr;  // H2D done, kernel done, D2H done
@@ -53,6 +64,7 @@ struct Slot {
 
     bool ensure(int64_t bytes) {
         const int64_t want = (bytes + (64ll << 20) - 1) & ~((64ll << 20) - 1);  // grow in 64 MiB steps
+        if (bytes > staging_max_bytes()) return false;
         if (bytes > h_cap) {
             if (h) (void)hipHostFree(h);
             if (hipHostMalloc((void **)&h, (size_t)want, hipHostMallocDefault) != hipSuccess) {
@@ -83,12 +95,38 @@ struct DevCtx {
     // a D2H waiting for its kernel must not hold up the next chunk's H2D.
     hipStream_t s_in = nullptr, s_out = nullptr;
     uint8_t *d_vocab = nullptr;
+    std::atomic<int64_t> last_use_ms{0};  // staging janitor: release after an idle period
+
+    // free the pinned host and HBM staging (caller holds mu)
+    void release_staging() {
+        for (Slot &sl : slot) {
+            if (sl.h) (void)hipHostFree(sl.h);
+            if (sl.d) (void)hipFree(sl.d);
+            sl.h = nullptr;
+            sl.d = nullptr;
+            sl.h_cap = sl.d_cap = 0;
+        }
+    }
+};
+
+// The library never leaves the caller on another device: every entry point
+// that selects a device restores the caller's current device on return (the
+// caller's runtime -- e.g. PyTorch's current stream and events -- reads it).
+struct DevGuard {
+    int prev = -1;
+    DevGuard() {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    }
+    ~DevGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
 };
 
 std::once_flag g_once;
 std::vector<DevCtx *> g_devs;
 
 void init_devices() {
+    DevGuard guard;
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
     for (int i = 0; i < n; i++) {
@@ -118,6 +156,47 @@ void init_devices() {
 std::vector<DevCtx *> &devices() {
     std::call_once(g_once, init_devices);
     return g_devs;
+}
+
+int64_t steady_ms() {
+    return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+// Pinned staging (up to NSLOT x 2 GiB host + HBM per device) is released after
+// JFS_STAGING_IDLE_MS (default 15 s; 0 = keep forever) without a batch, so an
+// idle FUSE daemon does not hold it.  jfs_release_staging() frees it at once.
+int64_t staging_idle_ms() {
+    static int64_t v = [] {
+        const char *e = getenv("JFS_STAGING_IDLE_MS");
+        return e ? (int64_t)atoll(e) : (int64_t)15000;
+    }();
+    return v;
+}
+
+void release_dev_staging(DevCtx *d) {
+    (void)hipSetDevice(d->id);  // janitor thread / explicit release: no caller device to keep
+    d->release_staging();
+}
+
+void start_janitor() {
+    static std::once_flag once;
+    if (staging_idle_ms() <= 0) return;
+    std::call_once(once, [] {
+        std::thread([] {
+            for (;;) {
+                std::this_thread::sleep_for(std::chrono::milliseconds(std::min<int64_t>(1000, staging_idle_ms())));
+                for (DevCtx *d : g_devs) {
+                    if (steady_ms() - d->last_use_ms.load() < staging_idle_ms()) continue;
+                    std::unique_lock<std::mutex> lk(d->mu, std::try_to_lock);
+                    if (!lk.owns_lock()) continue;
+                    bool any = false;
+                    for (Slot &sl : d->slot) any |= sl.h != nullptr || sl.d != nullptr;
+                    if (any) release_dev_staging(d);
+                }
+            }
+        }).detach();
+    });
 }
 
 enum Dir { COMPRESS = 0, DECOMPRESS = 1 };
@@ -162,11 +241,15 @@ int64_t staged_cap(int algo, int dir, const jfs_iov &v) {
     int64_t cap = v.dst_cap;
     // LZ4 compress: the kernel never writes at/after cap; stage at most the bound
     if (algo == JFS_ALGO_LZ4 && dir == COMPRESS) cap = std::min<int64_t>(cap, v.src_len + v.src_len / 255 + 16);
-    // Zstd decompress, cap(dst) < hint: DataDog decodes into a new hint-sized buffer
-    if (algo == JFS_ALGO_ZSTD && dir == DECOMPRESS) cap = std::max<int64_t>(cap, zstd_size_hint(v.src, v.src_len));
+    // Zstd decompress: cap(dst) < size hint is answered before staging
+    // (pre_answer), so the output never exceeds cap(dst)
     if (algo == JFS_ALGO_ZSTD && dir == COMPRESS) cap = std::min<int64_t>(cap, jfs_compress_bound(JFS_ALGO_ZSTD, v.src_len));
-    return std::max<int64_t>(cap, 0);
+    // the kernels take int32 capacities (jfs_dev_block)
+    return std::min<int64_t>(std::max<int64_t>(cap, 0), INT32_MAX);
 }
+
+// HBM/pinned bytes one block occupies in a chunk
+int64_t staged_bytes(int algo, int dir, const jfs_iov &v) { return align16(v.src_len) + align16(staged_cap(algo, dir, v)); }
 
 // Host staging chunk (input + output bytes per pipeline stage); default 2 GiB,
 // JFS_HOST_CHUNK_MB overrides.  The decode kernel needs many blocks in flight
@@ -235,7 +318,14 @@ int launch_kernel(int algo, int dir, const jfs_dev_block *d_desc, int nblk, int3
 int64_t run_batch(DevCtx *dev, int algo, int dir, int nblk, const jfs_iov *iov, int64_t *out) {
     if (nblk <= 0) return JFS_OK;
     std::lock_guard<std::mutex> lk(dev->mu);
+    DevGuard guard;
     (void)hipSetDevice(dev->id);
+    dev->last_use_ms = steady_ms();
+    start_janitor();
+    struct Touch {  // the idle clock starts when the batch ends
+        DevCtx *d;
+        ~Touch() { d->last_use_ms = steady_ms(); }
+    } touch{dev};
     std::vector<int64_t> cap(nblk), in_off(nblk), out_off(nblk);
     struct Chunk {
         int s, e, slot;
@@ -249,7 +339,7 @@ int64_t run_batch(DevCtx *dev, int algo, int dir, int nblk, const jfs_iov *iov, 
             Chunk c{s, s, (int)(ch.size() % NSLOT), 0, 0};
             while (c.e < nblk) {
                 const int64_t ci = staged_cap(algo, dir, iov[c.e]);
-                const int64_t ib = align16(iov[c.e].src_len), ob = align16(ci);
+                const int64_t ib = align16(iov[c.e].src_len), ob = align16(ci);  // = staged_bytes()
                 if (c.e > s && c.tin + c.tout + ib + ob > limit) break;
                 cap[c.e] = ci;
                 in_off[c.e] = c.tin;
@@ -275,7 +365,7 @@ int64_t run_batch(DevCtx *dev, int algo, int dir, int nblk, const jfs_iov *iov, 
     };
     auto launch = [&](const Chunk &c) -> int64_t {
         Slot &sl = dev->slot[c.slot];
-        if (!sl.ensure(chunk_bytes(c))) return JFS_ERR_HIP;
+        if (!sl.ensure(chunk_bytes(c))) return JFS_ERR_NO_MEMORY;
         uint8_t *h_in, *h_out, *d_in, *d_out;
         jfs_dev_block *h_desc, *d_desc;
         int32_t *h_ret, *d_ret;
@@ -323,12 +413,7 @@ int64_t run_batch(DevCtx *dev, int algo, int dir, int nblk, const jfs_iov *iov, 
         layout(c, sl.h, &h_in, &h_out, &h_desc, &h_ret);
         std::vector<CopyJob> jobs;
         for (int i = c.s; i < c.e; i++) {
-            int64_t r = finish_result(algo, dir, h_ret[i - c.s]);
-            if (algo == JFS_ALGO_ZSTD && dir == DECOMPRESS && r > 0 &&
-                iov[i].dst_cap < zstd_size_hint(iov[i].src, iov[i].src_len)) {
-                // decoded into DataDog's own buffer: compress.go:99-101 "buffer too short"
-                r = JFS_ERR_SHORT_BUFFER;
-            }
+            const int64_t r = finish_result(algo, dir, h_ret[i - c.s]);
             if (r > 0) jobs.push_back({iov[i].dst, h_out + out_off[i], r});
             out[i] = r;
         }
@@ -352,6 +437,24 @@ int64_t run_batch(DevCtx *dev, int algo, int dir, int nblk, const jfs_iov *iov, 
         (void)hipStreamSynchronize(dev->s_out);
     }
     return rc;
+}
+
+// run_batch with per-block error isolation (a GPU codec
+// reports per-block errors): when a batch fails as a whole (staging
+// allocation, a copy or launch error), every block is re-run on its own, so a
+// failure is charged only to the blocks that fail alone.
+void run_isolated(DevCtx *dev, int algo, int dir, int nblk, const jfs_iov *iov, int64_t *out) {
+    if (nblk <= 0) return;
+    const int64_t rc = run_batch(dev, algo, dir, nblk, iov, out);
+    if (rc == JFS_OK) return;
+    if (nblk == 1) {
+        out[0] = rc;
+        return;
+    }
+    for (int i = 0; i < nblk; i++) {
+        const int64_t r1 = run_batch(dev, algo, dir, 1, iov + i, out + i);
+        if (r1 != JFS_OK) out[i] = r1;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -406,12 +509,16 @@ class Coalescer {
                 int algo = q_.front()->algo, dir = q_.front()->dir;
                 int64_t bytes = 0;
                 batch.clear();
+                // same codec and direction; at most kMaxBytes of staging (the
+                // quantity run_batch stages); a request over the limit rides alone
                 for (auto it = q_.begin(); it != q_.end() && (int)batch.size() < kMaxBlocks;) {
                     Pending *p = *it;
-                    if (p->algo == algo && p->dir == dir && (batch.empty() || bytes + p->iov.src_len <= kMaxBytes)) {
+                    const int64_t b = staged_bytes(p->algo, p->dir, p->iov);
+                    if (p->algo == algo && p->dir == dir && (batch.empty() || bytes + b <= kMaxBytes)) {
                         batch.push_back(p);
-                        bytes += p->iov.src_len + p->iov.dst_cap;
+                        bytes += b;
                         it = q_.erase(it);
+                        if (bytes > kMaxBytes) break;
                     } else {
                         ++it;
                     }
@@ -420,11 +527,11 @@ class Coalescer {
             iov.resize(batch.size());
             out.assign(batch.size(), 0);
             for (size_t i = 0; i < batch.size(); i++) iov[i] = batch[i]->iov;
-            int64_t rc = run_batch(dev, batch[0]->algo, batch[0]->dir, (int)batch.size(), iov.data(), out.data());
+            run_isolated(dev, batch[0]->algo, batch[0]->dir, (int)batch.size(), iov.data(), out.data());
             {
                 std::lock_guard<std::mutex> lk(mu_);
                 for (size_t i = 0; i < batch.size(); i++) {
-                    batch[i]->res = rc == JFS_OK ? out[i] : rc;
+                    batch[i]->res = out[i];
                     batch[i]->done = true;
                 }
             }
@@ -446,6 +553,14 @@ bool pre_answer(int algo, int dir, const jfs_iov &v, int64_t *res) {
     if (algo == JFS_ALGO_LZ4 && dir == COMPRESS && v.src_len > LZ4_MAX_INPUT) { *res = JFS_ERR_COMPRESS_FAIL; return true; }
     if (algo == JFS_ALGO_ZSTD && dir == COMPRESS && v.dst_cap < jfs_compress_bound(JFS_ALGO_ZSTD, v.src_len)) {
         *res = JFS_ERR_SHORT_BUFFER;  // compress.go:86-89 (DataDog checks cap(dst) against CompressBound)
+        return true;
+    }
+    if (algo == JFS_ALGO_ZSTD && dir == DECOMPRESS && v.dst_cap < zstd_size_hint(v.src, v.src_len)) {
+        // DataDog/zstd v1.5.6 Decompress: cap(dst) < decompressSizeHint -> it
+        // decodes into a buffer of its own, so compress.go:99-101 always
+        // answers "buffer too short" (or the frame's own error): an error
+        // either way, and nothing is staged for a size the caller cannot hold
+        *res = JFS_ERR_SHORT_BUFFER;
         return true;
     }
     return false;
@@ -472,11 +587,10 @@ int64_t batch_common(int algo, int dir, int nblk, const jfs_iov *iov, int64_t *o
         part[k % G].push_back(iov[todo[k]]);
         idx[k % G].push_back(todo[k]);
     }
-    std::vector<int64_t> rc(G, JFS_OK);
     std::vector<std::vector<int64_t>> res(G);
     auto work = [&](size_t g) {
         res[g].assign(part[g].size(), 0);
-        rc[g] = run_batch(ds[g], algo, dir, (int)part[g].size(), part[g].data(), res[g].data());
+        run_isolated(ds[g], algo, dir, (int)part[g].size(), part[g].data(), res[g].data());
     };
     if (G == 1) work(0);
     else {
@@ -484,10 +598,8 @@ int64_t batch_common(int algo, int dir, int nblk, const jfs_iov *iov, int64_t *o
         for (size_t g = 0; g < G; g++) th.emplace_back(work, g);
         for (auto &t : th) t.join();
     }
-    for (size_t g = 0; g < G; g++) {
-        if (rc[g] != JFS_OK) return rc[g];
+    for (size_t g = 0; g < G; g++)
         for (size_t k = 0; k < idx[g].size(); k++) out_n[idx[g][k]] = res[g][k];
-    }
     return JFS_OK;
 }
 
@@ -575,7 +687,23 @@ int64_t jfs_zstd_decompress_device(const jfs_dev_block *d_blocks, int nblk, int3
     return jfs_launch_zstd_decode(d_blocks, nblk, d_ret, nullptr, (hipStream_t)stream) == 0 ? JFS_OK : JFS_ERR_HIP;
 }
 
+int64_t jfs_crc32c_device(const jfs_dev_block *d_blocks, int nblk, int32_t seg_bytes, uint32_t *d_crc,
+                          int32_t *d_ret, void *stream) {
+    if (devices().empty()) return JFS_ERR_NO_DEVICE;
+    if (nblk < 0 || seg_bytes < 0 || (seg_bytes > 0 && seg_bytes % 4096 != 0)) return JFS_ERR_INVALID;
+    return jfs_launch_crc32c(d_blocks, nblk, seg_bytes, d_crc, d_ret, (hipStream_t)stream) == 0 ? JFS_OK
+                                                                                              : JFS_ERR_HIP;
+}
+
 int jfs_device_count(void) { return (int)devices().size(); }
+
+void jfs_release_staging(void) {
+    for (DevCtx *d : devices()) {
+        DevGuard guard;
+        std::lock_guard<std::mutex> lk(d->mu);
+        release_dev_staging(d);
+    }
+}
 
 const char *jfs_version(void) { return JFS_VERSION; }
 

@@ -65,6 +65,16 @@ def zstd_compress(desc: torch.Tensor, ret: torch.Tensor, stream=None):
            "jfs_zstd_compress_device")
 
 
+def crc32c(desc: torch.Tensor, crc: torch.Tensor | None = None, ret: torch.Tensor | None = None,
+           seg_bytes: int = 0, stream=None):
+    """CRC-32C per descriptor (jfs_crc32c_device): whole-block values into
+    `crc` (uint32 as int32 tensor), per-segment big-endian sums into each dst."""
+    n = desc.numel() // DESC_DTYPE.itemsize
+    _check(L.load().jfs_crc32c_device(desc.data_ptr(), n, seg_bytes, crc.data_ptr() if crc is not None else None,
+                                      ret.data_ptr() if ret is not None else None, _stream_ptr(stream)),
+           "jfs_crc32c_device")
+
+
 def gen_blocks(out: torch.Tensor, nblk: int, block_bytes: int, cls: str, seed_base: int, stream=None):
     """Fill out[0 : nblk*block_bytes] with synthetic blocks."""
     assert out.numel() >= nblk * block_bytes
@@ -111,6 +121,10 @@ class Lz4Batch:
     def decompress(self, stream=None):
         lz4_decompress(self.dec_desc, self.dec_ret, stream)
 
+    def compress(self, stream=None):
+        """Re-encode raw -> comp (same bytes and sizes as the first encode)."""
+        lz4_compress(self.enc_desc, self.ret, stream)
+
     @property
     def comp_bytes(self) -> int:
         return int(self.csize.sum())
@@ -118,6 +132,7 @@ class Lz4Batch:
     def verify(self) -> bool:
         torch.cuda.synchronize()
         ok = bool((self.dec_ret == self.U).all().item())
+        ok = ok and bool((self.ret.cpu().numpy().astype(np.int64) == self.csize).all())
         return ok and bool(torch.equal(self.out, self.raw))
 
 

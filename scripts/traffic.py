@@ -3,8 +3,14 @@
 correction of MI355X_MICROARCH.md (HBM/rocprofv3 section).
 usage: traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> <kernel-substr> <blocks> <block_bytes> [out.json]"""
 import csv
+import hashlib
 import json
+import os
+import subprocess
 import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 
 
 def per_dispatch(path, kname, counter):
@@ -30,6 +36,14 @@ out = {
                   "so true traffic lies between hbm_bytes_raw and hbm_bytes_per_launch",
     "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes ({fpath}, {wpath})",
 }
+# stamp: bench.py uses the figure only while the kernel sources are unchanged
+from bench import kernel_src_sha256  # noqa: E402
+out["kernel_src_sha256"] = kernel_src_sha256()
+try:
+    out["git_head"] = subprocess.run(["git", "-C", ROOT, "rev-parse", "HEAD"], capture_output=True,
+                                     text=True).stdout.strip() or None
+except Exception:
+    out["git_head"] = None
 s = json.dumps(out, indent=1)
 print(s)
 if len(sys.argv) > 6:

@@ -14,6 +14,10 @@ class Oracle:
         lib.oracle_lz4_compress_default.restype = i32
         lib.oracle_lz4_decompress_safe.argtypes = [vp, vp, i32, i32]
         lib.oracle_lz4_decompress_safe.restype = i32
+        lib.oracle_crc32c_update.argtypes = [ctypes.c_uint32, vp, ctypes.c_size_t]
+        lib.oracle_crc32c_update.restype = ctypes.c_uint32
+        lib.oracle_crc32c_segments.argtypes = [vp, i64, i64, vp]
+        lib.oracle_crc32c_segments.restype = i64
         self.has_zstd = hasattr(lib, "oracle_zstd_decompress")
         if self.has_zstd:
             lib.oracle_zstd_decompress.argtypes = [vp, i64, vp, i64]
@@ -43,6 +47,17 @@ class Oracle:
         dst = ctypes.create_string_buffer(max(cap, 1))
         n = self.lib.oracle_zstd_decompress(src, len(src), dst, cap)
         return n, dst.raw[: max(n, 0)]
+
+    def crc32c(self, data: bytes, crc: int = 0) -> int:
+        """crc32.Update(crc, crc32c, data) (pkg/object/checksum.go:30-45)"""
+        return self.lib.oracle_crc32c_update(crc, data, len(data))
+
+    def crc32c_segments(self, data: bytes, seg: int = 32 << 10) -> bytes:
+        """disk_cache_file.go checksum(): big-endian CRC-32C per seg bytes"""
+        words = (len(data) - 1) // seg + 1 if len(data) else 1
+        out = ctypes.create_string_buffer(4 * words)
+        n = self.lib.oracle_crc32c_segments(data, len(data), seg, out)
+        return out.raw[:n]
 
     def zstd_strict_reserved(self, on: bool):
         self.lib.oracle_zstd_set_strict_reserved(1 if on else 0)
