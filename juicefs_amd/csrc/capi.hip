@@ -123,7 +123,10 @@ struct DevGuard {
 };
 
 std::once_flag g_once;
-std::vector<DevCtx *> g_devs;
+// never destroyed: the coalescer workers and the staging janitor are detached
+// threads that may still look at it while static destructors run at exit
+std::vector<DevCtx *> &g_devs = *new std::vector<DevCtx *>();
+std::atomic<bool> g_exiting{false};
 
 void init_devices() {
     DevGuard guard;
@@ -179,17 +182,28 @@ void release_dev_staging(DevCtx *d) {
     d->release_staging();
 }
 
+// At exit the janitor must not call into a HIP runtime that is being torn
+// down: the handler raises g_exiting and then takes every device lock once,
+// which waits out a release already in progress.
+void on_exit_handler() {
+    g_exiting = true;
+    for (DevCtx *d : g_devs) {
+        std::lock_guard<std::mutex> lk(d->mu);
+    }
+}
+
 void start_janitor() {
     static std::once_flag once;
     if (staging_idle_ms() <= 0) return;
     std::call_once(once, [] {
+        atexit(on_exit_handler);
         std::thread([] {
-            for (;;) {
+            while (!g_exiting) {
                 std::this_thread::sleep_for(std::chrono::milliseconds(std::min<int64_t>(1000, staging_idle_ms())));
                 for (DevCtx *d : g_devs) {
                     if (steady_ms() - d->last_use_ms.load() < staging_idle_ms()) continue;
                     std::unique_lock<std::mutex> lk(d->mu, std::try_to_lock);
-                    if (!lk.owns_lock()) continue;
+                    if (!lk.owns_lock() || g_exiting) continue;
                     bool any = false;
                     for (Slot &sl : d->slot) any |= sl.h != nullptr || sl.d != nullptr;
                     if (any) release_dev_staging(d);

@@ -921,15 +921,18 @@ __device__ __forceinline__ void dp_step(const uint8_t *pc, int32_t lim, uint32_t
     if constexpr (I >= 0) {
         const uint32_t tb = pc[I], e1 = pc[I + 1];
         const uint32_t ll = tb >> 4;
-        const bool llx = ll == 15u;
+        // 0/1 integers combined with bitwise ops: short-circuit && / || here
+        // compiled to exec-mask branches (and SGPR spills) in every step
+        const uint32_t llx = (uint32_t)(ll == 15u);
         // q: offset of the first match-length extension byte (after the offset)
         const uint32_t q = (uint32_t)I + 3u + (llx ? 16u + e1 : ll);
-        const bool oob = (int32_t)q >= lim;  // not staged: exact walk
+        const uint32_t oob = (uint32_t)((int32_t)q >= lim);  // not staged: exact walk
         const uint32_t e2 = pc[oob ? 0u : q];
-        const bool mlx = (tb & 15u) == 15u;
-        const uint32_t nx = q + (mlx ? 1u : 0u);
+        const uint32_t mlx = (uint32_t)((tb & 15u) == 15u);
+        const uint32_t nx = q + mlx;
         // long literal runs land past the piece (else: exact walk)
-        const bool slow = (llx && (e1 == 255u || nx < 32u)) || oob || (mlx && e2 == 255u);
+        const uint32_t slow = (llx & ((uint32_t)(e1 == 255u) | (uint32_t)(nx < 32u))) | oob |
+                              (mlx & (uint32_t)(e2 == 255u));
         uint32_t xi = nx;
         if constexpr (I + 3 < 32) {
             constexpr int bq = (I + 3) >> 2;
