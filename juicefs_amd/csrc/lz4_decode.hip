@@ -53,10 +53,16 @@ constexpr int RMASK = R - 1;
 #define JFS_LZ4_DP 1  // exit-table parser for windows away from the input end
 #endif
 #ifndef JFS_LZ4_SUBST
-#define JFS_LZ4_SUBST 2  // source-substitution hops per batch (2 measured best: 323 vs 317 GiB/s for 3)
+#define JFS_LZ4_SUBST 1  // source-substitution hops per batch (with the whole-wave near fallback: 1 = 2 > 3)
 #endif
 #ifndef JFS_LZ4_NEARPM
-#define JFS_LZ4_NEARPM 1  // exact near-match readiness (prefix max of pending ends)
+#define JFS_LZ4_NEARPM 2  // near readiness: 2 = source wholly before the batch (measured equal to 1 = exact prefix-max rule, and cheaper)
+#endif
+#ifndef JFS_LZ4_NEARSER
+#define JFS_LZ4_NEARSER 1  // near matches: one lane-parallel round, the rest by the whole wave in order
+#endif
+#ifndef JFS_LZ4_LITSER
+#define JFS_LZ4_LITSER 0  // 1: literal runs take one 16-byte lane step, longer runs by the whole wave (measured: no gain)
 #endif
 constexpr int OV = JFS_LZ4_OV;           // speculative-walk pre-roll (bytes before the piece)
 constexpr int TMAX = CW / 3 + 2;       // max tokens in a window (interior token >= 3 bytes)
@@ -567,6 +573,26 @@ __device__ __forceinline__ void copy16(Smem &s, uint32_t sa, uint32_t da, int32_
 }
 
 
+// Whole-wave copy of len bytes to output op from output op - D (all inside the
+// ring), in chunks of at most D bytes so that self-overlapping matches repeat
+// their period; plain byte stores (the bytes are not written by anyone else).
+__device__ __forceinline__ void wave_near(Smem &s, const Ctx &c, int32_t op, int32_t D, int32_t len) {
+    const int l = lane_id();
+    const int32_t step = D < 64 ? D : 64;
+    for (int32_t k = 0; k < len; k += step) {
+        const int32_t i = k + l;
+        if (l < step && i < len) s.ring[slot(c, op + i)] = s.ring[slot(c, op + i - D)];
+    }
+}
+// Whole-wave copy of literal bytes [from, len) of a run staged at cw + litr.
+__device__ __forceinline__ void wave_lit(Smem &s, const Ctx &c, int32_t op, uint32_t litr, int32_t from, int32_t len) {
+    const int l = lane_id();
+    for (int32_t k = from; k < len; k += 64) {
+        const int32_t i = k + l;
+        if (i < len) s.ring[slot(c, op + i)] = c.cw[litr + (uint32_t)i];
+    }
+}
+
 // One lane-parallel batch: lanes with act hold consecutive tokens producing
 // output [O0, O1), O1 - O0 <= BSPAN, every ll/ml <= LMAX.
 __device__ __forceinline__ void batch(Smem &s, Ctx &c, bool act, int32_t o, uint32_t ll, uint32_t ml, uint32_t off,
@@ -600,6 +626,17 @@ __device__ __forceinline__ void batch(Smem &s, Ctx &c, bool act, int32_t o, uint
 #ifdef JFS_SKIP_LIT
     if (0)
 #endif
+#if JFS_LZ4_LITSER
+    // one 16-byte step per lane; the rare longer runs finish by the whole wave
+    if (__ballot(act && ll > 0u)) {
+        PCOUNT(16, 1);
+        if (act && ll > 0u) copy16<false>(s, c.cwoff + litr, slot(c, o), ll < 16u ? (int32_t)ll : 16);
+    }
+    for (uint64_t lm = __ballot(act && ll > 16u); lm; lm &= lm - 1) {
+        const int j = (int)__builtin_ctzll(lm);
+        wave_lit(s, c, (int32_t)readlane((uint32_t)o, j), readlane(litr, j), 16, (int32_t)readlane(ll, j));
+    }
+#else
     for (uint32_t k = 0; __ballot(act && k < ll); k += 16) {
         PCOUNT(16, 1);
         if (act && k < ll) {
@@ -607,6 +644,7 @@ __device__ __forceinline__ void batch(Smem &s, Ctx &c, bool act, int32_t o, uint
             copy16<false>(s, c.cwoff + litr + k, slot(c, o + (int32_t)k), m);
         }
     }
+#endif
     PSTAMP(4);
     // far matches (offset-0 matches write zeros: the span is already zero)
 #ifdef JFS_SKIP_FAR
@@ -666,7 +704,7 @@ __device__ __forceinline__ void batch(Smem &s, Ctx &c, bool act, int32_t o, uint
     // near matches in rounds
     int32_t pos = ms, rem = (int32_t)ml, D = ms - src;
     const int32_t send = src + (int32_t)ml < ms ? src + (int32_t)ml : ms;
-#if JFS_LZ4_NEARPM
+#if JFS_LZ4_NEARPM == 1
     int jl = 0;  // last lane with key < send (jv: such a lane exists)
 #pragma unroll
     for (int stp = 32; stp; stp >>= 1) {
@@ -675,13 +713,48 @@ __device__ __forceinline__ void batch(Smem &s, Ctx &c, bool act, int32_t o, uint
     }
     const bool jv = (uint32_t)__shfl((int)key, jl, 64) < (uint32_t)send;
 #endif
+#if JFS_LZ4_NEARSER
+    // one round: every ready lane copies its first (<= 16 byte) step; what is
+    // left (lanes whose source waits on a match of this batch, matches longer
+    // than one step) is copied by the whole wave in lane order, which is output
+    // order, so every source is complete when its lane's turn comes
 #ifdef JFS_SKIP_NEAR
+    if (0)
+#endif
+    {
+        PCOUNT(18, 1);
+#if JFS_LZ4_NEARPM == 2
+        const bool go = pend && send <= O0;  // source wholly before the batch
+#elif JFS_LZ4_NEARPM
+        const uint32_t pm = dpp_scan_max(pend ? (uint32_t)(ms + (int32_t)ml) : 0u);
+        const uint32_t pmj = (uint32_t)__shfl((int)pm, jl, 64);
+        const bool go = pend && (!jv || pmj <= (uint32_t)src);
+#else
+        const int32_t front = (int32_t)dwave_min(pend ? (uint32_t)ms : 0x7FFFFFFFu);
+        const bool go = pend && send <= front;
+#endif
+        if (__ballot(go)) {
+            PCOUNT(15, 1);
+            if (go) {
+                const int32_t m = rem < 16 ? (rem < D ? rem : D) : (D < 16 ? D : 16);
+                copy16<true>(s, slot(c, pos - D), slot(c, pos), m);
+                pos += m;
+                rem -= m;
+                if (rem <= 0) pend = false;
+            }
+        }
+        for (uint64_t pmk = __ballot(pend); pmk; pmk &= pmk - 1) {
+            const int j = (int)__builtin_ctzll(pmk);
+            wave_near(s, c, (int32_t)readlane((uint32_t)pos, j), (int32_t)readlane((uint32_t)D, j),
+                      (int32_t)readlane((uint32_t)rem, j));
+        }
+    }
     if (0)
 #endif
     for (int guard = 0; __ballot(pend); ++guard) {
         if (guard > 64) { c.bug = 5; break; }
         PCOUNT(18, 1);
-#if JFS_LZ4_NEARPM
+#if JFS_LZ4_NEARPM == 1
         // ready: no still-pending destination [ms_j, ms_j + ml_j) meets the source
         // [src, send).  Destinations are disjoint and in lane order, so that is the
         // prefix max of pending ends at the last lane jl with ms_jl < send.
