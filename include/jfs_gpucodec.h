@@ -129,6 +129,28 @@ int64_t jfs_zstd_compress_device(const jfs_dev_block *d_blocks, int nblk, int32_
 int64_t jfs_crc32c_device(const jfs_dev_block *d_blocks, int nblk, int32_t seg_bytes, uint32_t *d_crc,
                           int32_t *d_ret, void *stream);
 
+/* AES-256-GCM of device-resident blocks: the AEAD of
+ * pkg/object/encrypt.go dataEncryptor for AES256GCM_RSA (aes.NewCipher(key) +
+ * cipher.NewGCM, :178-189): 32-byte key, 12-byte nonce, 16-byte tag, no
+ * additional data.  Seal (Encrypt :226-257): dst = ciphertext || tag,
+ * ret = src_len + 16 (dst_cap must hold it).  Open (Decrypt :259-284):
+ * src = ciphertext || tag, dst = plaintext, ret = src_len - 16, or -1 when the
+ * tag does not verify ("cipher: message authentication failed"; dst is then
+ * not to be used).  ret = -2 for a bad descriptor.  The random key/nonce, the
+ * RSA wrap of the key and the object header (:230-252) are the caller's.
+ * Asynchronous on `stream`; key and nonce are device pointers. */
+typedef struct jfs_aead_block {
+    const uint8_t *src;
+    uint8_t *dst;
+    int32_t src_len;
+    int32_t dst_cap;
+    const uint8_t *key;   /* 32 bytes */
+    const uint8_t *nonce; /* 12 bytes */
+} jfs_aead_block;
+
+int64_t jfs_aes256gcm_seal_device(const jfs_aead_block *d_blocks, int nblk, int32_t *d_ret, void *stream);
+int64_t jfs_aes256gcm_open_device(const jfs_aead_block *d_blocks, int nblk, int32_t *d_ret, void *stream);
+
 /* ---- Runtime / utilities ------------------------------------------------- */
 
 /* Number of usable gfx950 devices (0 when none; never an error). */

@@ -30,7 +30,8 @@ EXPORTS = [
     "jfs_codec_from_name", "jfs_codec_name", "jfs_compress_bound", "jfs_compress", "jfs_decompress",
     "jfs_compress_batch", "jfs_decompress_batch", "jfs_lz4_decompress_device", "jfs_lz4_compress_device",
     "jfs_zstd_decompress_device", "jfs_zstd_compress_device", "jfs_device_count", "jfs_version", "jfs_gen_blocks_device",
-    "jfs_gen_block_host", "jfs_release_staging", "jfs_crc32c_device",
+    "jfs_gen_block_host", "jfs_release_staging", "jfs_crc32c_device", "jfs_aes256gcm_seal_device",
+    "jfs_aes256gcm_open_device",
 ]
 
 
@@ -74,6 +75,9 @@ def load() -> ctypes.CDLL:
         f.restype = i64
     lib.jfs_crc32c_device.argtypes = [vp, ctypes.c_int, ctypes.c_int32, vp, vp, vp]
     lib.jfs_crc32c_device.restype = i64
+    for f in (lib.jfs_aes256gcm_seal_device, lib.jfs_aes256gcm_open_device):
+        f.argtypes = [vp, ctypes.c_int, vp, vp]
+        f.restype = i64
     lib.jfs_release_staging.argtypes = []
     lib.jfs_release_staging.restype = None
     lib.jfs_device_count.argtypes = []

@@ -255,8 +255,12 @@ int64_t staged_cap(int algo, int dir, const jfs_iov &v) {
     int64_t cap = v.dst_cap;
     // LZ4 compress: the kernel never writes at/after cap; stage at most the bound
     if (algo == JFS_ALGO_LZ4 && dir == COMPRESS) cap = std::min<int64_t>(cap, v.src_len + v.src_len / 255 + 16);
-    // Zstd decompress: cap(dst) < size hint is answered before staging
-    // (pre_answer), so the output never exceeds cap(dst)
+    // Zstd decompress with cap(dst) < DataDog's size hint: DataDog decodes into
+    // a buffer of its own, so compress.go:99-101 answers "buffer too short"
+    // unless the frames decode to nothing ((0, nil)) or are corrupt (their own
+    // error).  Decoding into zero bytes of staging tells those three apart
+    // without staging a size the caller cannot hold.
+    if (algo == JFS_ALGO_ZSTD && dir == DECOMPRESS && cap < zstd_size_hint(v.src, v.src_len)) cap = 0;
     if (algo == JFS_ALGO_ZSTD && dir == COMPRESS) cap = std::min<int64_t>(cap, jfs_compress_bound(JFS_ALGO_ZSTD, v.src_len));
     // the kernels take int32 capacities (jfs_dev_block)
     return std::min<int64_t>(std::max<int64_t>(cap, 0), INT32_MAX);
@@ -569,14 +573,6 @@ bool pre_answer(int algo, int dir, const jfs_iov &v, int64_t *res) {
         *res = JFS_ERR_SHORT_BUFFER;  // compress.go:86-89 (DataDog checks cap(dst) against CompressBound)
         return true;
     }
-    if (algo == JFS_ALGO_ZSTD && dir == DECOMPRESS && v.dst_cap < zstd_size_hint(v.src, v.src_len)) {
-        // DataDog/zstd v1.5.6 Decompress: cap(dst) < decompressSizeHint -> it
-        // decodes into a buffer of its own, so compress.go:99-101 always
-        // answers "buffer too short" (or the frame's own error): an error
-        // either way, and nothing is staged for a size the caller cannot hold
-        *res = JFS_ERR_SHORT_BUFFER;
-        return true;
-    }
     return false;
 }
 
@@ -707,6 +703,18 @@ int64_t jfs_crc32c_device(const jfs_dev_block *d_blocks, int nblk, int32_t seg_b
     if (nblk < 0 || seg_bytes < 0 || (seg_bytes > 0 && seg_bytes % 4096 != 0)) return JFS_ERR_INVALID;
     return jfs_launch_crc32c(d_blocks, nblk, seg_bytes, d_crc, d_ret, (hipStream_t)stream) == 0 ? JFS_OK
                                                                                               : JFS_ERR_HIP;
+}
+
+int64_t jfs_aes256gcm_seal_device(const jfs_aead_block *d_blocks, int nblk, int32_t *d_ret, void *stream) {
+    if (devices().empty()) return JFS_ERR_NO_DEVICE;
+    if (nblk < 0) return JFS_ERR_INVALID;
+    return jfs_launch_aes256gcm(d_blocks, nblk, 0, d_ret, (hipStream_t)stream) == 0 ? JFS_OK : JFS_ERR_HIP;
+}
+
+int64_t jfs_aes256gcm_open_device(const jfs_aead_block *d_blocks, int nblk, int32_t *d_ret, void *stream) {
+    if (devices().empty()) return JFS_ERR_NO_DEVICE;
+    if (nblk < 0) return JFS_ERR_INVALID;
+    return jfs_launch_aes256gcm(d_blocks, nblk, 1, d_ret, (hipStream_t)stream) == 0 ? JFS_OK : JFS_ERR_HIP;
 }
 
 int jfs_device_count(void) { return (int)devices().size(); }

@@ -30,6 +30,7 @@ int jfs_launch_zstd_decode(const jfs_dev_block *d_blocks, int nblk, int32_t *d_r
                            hipStream_t stream);
 int jfs_launch_crc32c(const jfs_dev_block *d_blocks, int nblk, int32_t seg_bytes, uint32_t *d_crc, int32_t *d_ret,
                       hipStream_t stream);
+int jfs_launch_aes256gcm(const jfs_aead_block *d_blocks, int nblk, int mode, int32_t *d_ret, hipStream_t stream);
 int jfs_launch_gen(uint8_t *d_dst, int nblk, int64_t block_bytes, char cls, uint64_t seed_base,
                    const uint8_t *d_vocab, hipStream_t stream);
 }

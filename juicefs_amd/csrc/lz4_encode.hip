@@ -10,8 +10,18 @@
 // wave-uniform control flow; the 64 lanes do the byte-parallel parts: match
 // extension (64 bytes per compare + ballot), backward catch-up, literal
 // copies and table clears.  Throughput comes from running thousands of blocks
-// at once (8 wavefronts per CU).  Output is staged in an LDS ring and written
-// to HBM with wide stores; nothing is written at or beyond dst_cap.
+// at once.  What keeps the serial parse off HBM latency:
+//   * the bytes ahead of the parse position live in a 2 KiB LDS window that
+//     slides in 1 KiB steps; the next step is prefetched into registers one
+//     step early, so hashing and the parse-side compare read LDS only;
+//   * every hash-table entry (byU32 table) carries check bits -- a hash of the
+//     4 bytes at its position -- next to the position.  A candidate whose
+//     check bits differ from those of the current 4 bytes cannot match, so the
+//     HBM read of the candidate's bytes is made only when a match is likely.
+//     The decision is still the exact 4-byte compare, so the parse (and every
+//     output byte) is unchanged.
+// Output is staged in an LDS ring and written to HBM with wide stores; nothing
+// is written at or beyond dst_cap.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -22,13 +32,17 @@ namespace jfs {
 namespace lz4e {
 
 constexpr int64_t kMaxInput = 0x7E000000;
-constexpr int OB = 4096;  // output staging ring
+constexpr int OB = 2048;  // output staging ring (the put_* paths assume OB >= 2 * OFLUSH + slack)
 constexpr int OBMASK = OB - 1;
-constexpr int OFLUSH = 2048;
+constexpr int OFLUSH = 1024;
+constexpr int SW = 2048;  // source window (LDS), slides in SW/2 steps
+constexpr int SWMASK = SW - 1;
+constexpr int SWSTEP = SW / 2;  // = 64 lanes x 16 bytes
 
 struct Smem {
     alignas(16) uint32_t table[4096];  // byU32 view; byU16 view is the same 16 KiB
     alignas(16) uint8_t ob[OB];
+    alignas(16) uint8_t sw[SW];
 };
 
 struct Enc {
@@ -38,6 +52,13 @@ struct Enc {
     int64_t op;  // output bytes produced
     int64_t F;   // flushed up to
     uint32_t dmis;
+    // source window: covers "aligned offsets" q in [wq, wq + SW), q = p + smis
+    // for source position p; pf = this lane's 16 bytes of [wq + SW, wq + SW + SWSTEP)
+    const gc_u4 *sa;  // src rounded down to 16 bytes
+    int64_t smis, wq, nq;
+    uint4 pf;
+    int pb;        // position bits of a byU32 table entry (check bits above)
+    uint32_t pmask;
 };
 
 __device__ __forceinline__ uint32_t ld32u(const gc_u8 *p) {
@@ -50,29 +71,90 @@ __device__ __forceinline__ uint32_t ld32u(const gc_u8 *p) {
     return __builtin_amdgcn_alignbyte(w1, w0, sh);
 }
 
-__device__ __forceinline__ uint64_t ld64u(const gc_u8 *p) {
-    uintptr_t a = (uintptr_t)p;
-    const gc_u32 *w = (const gc_u32 *)(a & ~(uintptr_t)3);
-    uint32_t sh = (uint32_t)(a & 3);
-    uint32_t w0 = w[0], w1 = w[1];
-    if (sh == 0) return (uint64_t)w0 | ((uint64_t)w1 << 32);
-    uint32_t w2 = w[2];
-    uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh);
-    uint32_t hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
+// ---- source window ---------------------------------------------------------
+__device__ __forceinline__ uint4 sw_chunk(const Enc &e, int64_t q) {  // 16 bytes at aligned offset q
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (q < e.nq) v = e.sa[q >> 4];
+    return v;
+}
+__device__ __forceinline__ void sw_put(Smem &s, int64_t q, const uint4 &v) {
+    *(uint4 *)(s.sw + (uint32_t)(q & SWMASK)) = v;
+}
+// (re)fill the window to start at aligned offset wq (multiple of SWSTEP)
+__device__ __forceinline__ void sw_fill(Smem &s, Enc &e, int64_t wq) {
+    const int l = lane_id();
+    const uint4 a = sw_chunk(e, wq + 16 * l), b = sw_chunk(e, wq + SWSTEP + 16 * l);
+    e.pf = sw_chunk(e, wq + SW + 16 * l);
+    sw_put(s, wq + 16 * l, a);
+    sw_put(s, wq + SWSTEP + 16 * l, b);
+    e.wq = wq;
+    __builtin_amdgcn_wave_barrier();
+}
+// make source bytes [p, p + len) readable from the window (len <= 16)
+__device__ __forceinline__ void sw_need(Smem &s, Enc &e, int64_t p, int len) {
+    const int64_t q = p + e.smis;
+    if (q + len <= e.wq + SW) return;
+    if (q + len <= e.wq + SW + SWSTEP && q >= e.wq + SWSTEP) {
+        // slide by one step: the prefetched chunk replaces the oldest half
+        const int l = lane_id();
+        sw_put(s, e.wq + SW + 16 * l, e.pf);
+        e.wq += SWSTEP;
+        e.pf = sw_chunk(e, e.wq + SW + 16 * l);
+        __builtin_amdgcn_wave_barrier();
+        return;
+    }
+    sw_fill(s, e, (q & ~(int64_t)(SWSTEP - 1)) - SWSTEP > 0 ? (q & ~(int64_t)(SWSTEP - 1)) - SWSTEP : 0);
+}
+__device__ __forceinline__ bool sw_has(const Enc &e, int64_t p, int len) {
+    const int64_t q = p + e.smis;
+    return q >= e.wq && q + len <= e.wq + SW;
+}
+__device__ __forceinline__ uint32_t sw_rd32(const Smem &s, const Enc &e, int64_t p) {
+    const uint32_t q = (uint32_t)(p + e.smis);
+    const uint32_t a = q & ~3u, sh = q & 3u;
+    const uint32_t w0 = *(const uint32_t *)(s.sw + (a & SWMASK)), w1 = *(const uint32_t *)(s.sw + ((a + 4) & SWMASK));
+    return __builtin_amdgcn_alignbyte(w1, w0, sh);
+}
+__device__ __forceinline__ uint64_t sw_rd64(const Smem &s, const Enc &e, int64_t p) {
+    const uint32_t q = (uint32_t)(p + e.smis);
+    const uint32_t a = q & ~3u, sh = q & 3u;
+    const uint32_t w0 = *(const uint32_t *)(s.sw + (a & SWMASK)), w1 = *(const uint32_t *)(s.sw + ((a + 4) & SWMASK)),
+                   w2 = *(const uint32_t *)(s.sw + ((a + 8) & SWMASK));
+    return (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32);
+}
+// 8 bytes at p through the window (slides it forward as needed)
+__device__ __forceinline__ uint64_t src64(Smem &s, Enc &e, int64_t p) {
+    sw_need(s, e, p, 8);
+    if (sw_has(e, p, 8)) return sw_rd64(s, e, p);
+    const uint32_t lo = ld32u(e.src + p), hi = ld32u(e.src + p + 4);  // (window just reset below p)
     return (uint64_t)lo | ((uint64_t)hi << 32);
 }
+// 4 bytes at an arbitrary earlier position (window if present, else HBM)
+__device__ __forceinline__ uint32_t src32(const Smem &s, const Enc &e, int64_t p) {
+    if (sw_has(e, p, 4)) return sw_rd32(s, e, p);
+    return ld32u(e.src + p);
+}
 
-__device__ __forceinline__ uint32_t hpos(const gc_u8 *p, bool u16) {
-    if (u16) return (ld32u(p) * 2654435761u) >> 19;
-    return (uint32_t)(((ld64u(p) << 24) * 889523592379ull) >> 52);
+__device__ __forceinline__ uint32_t hash_of(uint64_t v, bool u16) {
+    if (u16) return ((uint32_t)v * 2654435761u) >> 19;
+    return (uint32_t)(((v << 24) * 889523592379ull) >> 52);
+}
+// check bits of the 4 bytes v (independent of the table hash)
+__device__ __forceinline__ uint32_t check_of(const Enc &e, uint32_t v) {
+    return ((v * 0x9E3779B1u) >> e.pb) << e.pb;  // top (32 - pb) bits
 }
 
 __device__ __forceinline__ uint32_t tget(const Smem &s, uint32_t h, bool u16) {
     return u16 ? (uint32_t)((const uint16_t *)s.table)[h] : s.table[h];
 }
-__device__ __forceinline__ void tput(Smem &s, uint32_t h, uint32_t v, bool u16) {
-    if (u16) ((uint16_t *)s.table)[h] = (uint16_t)v;
-    else s.table[h] = v;
+// insert position pos whose first 4 bytes are v
+__device__ __forceinline__ void tput(Smem &s, const Enc &e, uint32_t h, uint32_t pos, uint32_t v, bool u16) {
+    if (u16) ((uint16_t *)s.table)[h] = (uint16_t)pos;
+    else s.table[h] = pos | check_of(e, v);
+}
+// can the entry (found for 4 bytes v) be a match?  (byU16: always ask HBM)
+__device__ __forceinline__ bool may_match(const Enc &e, uint32_t ent, uint32_t v, bool u16) {
+    return u16 || (ent & ~e.pmask) == check_of(e, v);
 }
 
 // staging slot of output position x (mirrors HBM 16-byte alignment)
@@ -124,8 +206,10 @@ __device__ __forceinline__ void put_lits(Smem &s, Enc &e, int64_t from, int64_t 
     const int l = lane_id();
     for (int64_t k = 0; k < len; k += 64) {
         maybe_flush(s, e, keep_from);
-        if (e.op + 64 - e.F > OB) {
-            // token pending too far back: flush past it; the token is patched in HBM
+        if (e.op + 64 + 16 - e.F > OB) {
+            // token pending too far back: flush past it (the token is patched in
+            // HBM); the 16 bytes of slack hold the offset bytes that follow the
+            // run before the next flush, so the ring never wraps onto unflushed bytes
             int64_t to = ((e.op + e.dmis) & ~(int64_t)15) - e.dmis;
             oflush2(s, e, to);
         }
@@ -143,6 +227,7 @@ __device__ __forceinline__ void put_token(Smem &s, Enc &e, int64_t tp, uint32_t 
     }
 }
 
+// Residency: 20 KiB of LDS per block -> 8 blocks (waves) per CU.
 __global__ __launch_bounds__(64) void lz4_encode_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
                                                        int32_t *__restrict__ ret) {
     __shared__ Smem s;
@@ -158,6 +243,11 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(const jfs_dev_block *__r
     e.op = 0;
     e.F = 0;
     e.dmis = (uint32_t)((uintptr_t)d.dst & 15u);
+    e.sa = (const gc_u4 *)((uintptr_t)d.src & ~(uintptr_t)15);
+    e.smis = (int64_t)((uintptr_t)d.src & 15u);
+    e.nq = e.n + e.smis;
+    e.wq = 0;
+    e.pf = make_uint4(0, 0, 0, 0);
     const gc_u8 *src = e.src;
     const int64_t n = e.n;
     int32_t result;
@@ -171,14 +261,23 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(const jfs_dev_block *__r
         }
     } else {
         const bool u16 = n < 65536 + 12 - 1;
-        for (int k = l; k < 4096; k += 64) s.table[k] = 0;
+        // byU32 entries: position in the low pb bits, check bits above
+        e.pb = 32 - __builtin_clz((uint32_t)n);
+        if (e.pb < 16) e.pb = 16;
+        e.pmask = e.pb >= 32 ? 0xFFFFFFFFu : ((1u << e.pb) - 1u);
+        sw_fill(s, e, 0);
+        // empty table: every entry is position 0 (LZ4's zeroed table), with its check bits
+        const uint32_t init = u16 ? 0u : (n >= 4 ? check_of(e, sw_rd32(s, e, 0)) : 0u);
+        for (int k = l; k < 4096; k += 64) s.table[k] = init;
         __builtin_amdgcn_wave_barrier();
         const int64_t mflimitP1 = n - 12 + 1, matchlimit = n - 5;
         int64_t ip = 0, anchor = 0;
         if (n >= 13) {
-            tput(s, hpos(src, u16), 0, u16);
+            uint64_t v0 = src64(s, e, 0);
+            tput(s, e, hash_of(v0, u16), 0, (uint32_t)v0, u16);
             ip = 1;
-            uint32_t fh = hpos(src + ip, u16);
+            uint64_t fv = src64(s, e, ip);  // 8 bytes at the next search position
+            uint32_t fh = hash_of(fv, u16);
             for (;;) {
                 int64_t match;
                 // ---- search (skip schedule: step = searchMatchNb++ >> 6)
@@ -187,18 +286,21 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(const jfs_dev_block *__r
                     int32_t step = 1, snb = 1 << 6;
                     bool last = false;
                     for (;;) {
-                        uint32_t h = fh;
-                        int64_t cur = fip;
-                        uint32_t mi = tget(s, h, u16);
+                        const uint32_t h = fh;
+                        const int64_t cur = fip;
+                        const uint32_t cv = (uint32_t)fv;
+                        const uint32_t ent = tget(s, h, u16);
                         ip = fip;
                         fip += step;
                         step = snb++ >> 6;
                         if (fip > mflimitP1) { last = true; break; }
-                        match = mi;
-                        fh = hpos(src + fip, u16);
-                        tput(s, h, (uint32_t)cur, u16);
-                        if (!u16 && (int64_t)mi + 65535 < cur) continue;
-                        if (ld32u(src + match) == ld32u(src + ip)) break;
+                        match = u16 ? ent : (ent & e.pmask);
+                        fv = src64(s, e, fip);
+                        fh = hash_of(fv, u16);
+                        tput(s, e, h, (uint32_t)cur, cv, u16);
+                        if (!u16 && match + 65535 < cur) continue;
+                        if (!may_match(e, ent, cv, u16)) continue;
+                        if (src32(s, e, match) == cv) break;
                     }
                     if (last) break;
                 }
@@ -255,11 +357,20 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(const jfs_dev_block *__r
                     maybe_flush(s, e, INT64_MAX);
                     anchor = ip;
                     if (ip >= mflimitP1) break;
-                    tput(s, hpos(src + ip - 2, u16), (uint32_t)(ip - 2), u16);
-                    uint32_t h = hpos(src + ip, u16);
-                    uint32_t mi = tget(s, h, u16);
-                    tput(s, h, (uint32_t)ip, u16);
-                    if ((u16 || (int64_t)mi + 65535 >= ip) && ld32u(src + mi) == ld32u(src + ip)) {
+                    {
+                        const uint64_t v2 = src64(s, e, ip - 2);
+                        tput(s, e, hash_of(v2, u16), (uint32_t)(ip - 2), (uint32_t)v2, u16);
+                    }
+                    const uint64_t vi = src64(s, e, ip);
+                    const uint32_t h = hash_of(vi, u16);
+                    const uint32_t ent = tget(s, h, u16);
+                    const uint32_t mi = u16 ? ent : (ent & e.pmask);
+                    tput(s, e, h, (uint32_t)ip, (uint32_t)vi, u16);
+                    bool rm = (u16 || (int64_t)mi + 65535 >= ip) && may_match(e, ent, (uint32_t)vi, u16);
+                    if (rm) {
+                        rm = src32(s, e, mi) == (uint32_t)vi;
+                    }
+                    if (rm) {
                         match = mi;
                         tp = e.op;
                         e.op++;
@@ -270,7 +381,8 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(const jfs_dev_block *__r
                 }
                 if (anchor >= mflimitP1) break;
                 ++ip;
-                fh = hpos(src + ip, u16);
+                fv = src64(s, e, ip);
+                fh = hash_of(fv, u16);
             }
         }
         // ---- last literals

@@ -75,6 +75,31 @@ def crc32c(desc: torch.Tensor, crc: torch.Tensor | None = None, ret: torch.Tenso
            "jfs_crc32c_device")
 
 
+AEAD_DTYPE = np.dtype([("src", "<u8"), ("dst", "<u8"), ("src_len", "<i4"), ("dst_cap", "<i4"),
+                       ("key", "<u8"), ("nonce", "<u8")])
+
+
+def make_aead_desc(src: torch.Tensor, src_offs, src_lens, dst: torch.Tensor, dst_offs, dst_caps,
+                   kn: torch.Tensor, key_offs, nonce_offs) -> torch.Tensor:
+    """jfs_aead_block descriptors (40 bytes each); keys and nonces live in `kn`."""
+    a = np.zeros(len(src_offs), dtype=AEAD_DTYPE)
+    a["src"] = src.data_ptr() + np.asarray(src_offs, dtype=np.uint64)
+    a["dst"] = dst.data_ptr() + np.asarray(dst_offs, dtype=np.uint64)
+    a["src_len"] = np.asarray(src_lens, dtype=np.int32)
+    a["dst_cap"] = np.asarray(dst_caps, dtype=np.int32)
+    a["key"] = kn.data_ptr() + np.asarray(key_offs, dtype=np.uint64)
+    a["nonce"] = kn.data_ptr() + np.asarray(nonce_offs, dtype=np.uint64)
+    return torch.from_numpy(a.view(np.uint8).copy()).to(src.device)
+
+
+def aes256gcm(desc: torch.Tensor, ret: torch.Tensor, seal: bool, stream=None):
+    """AES-256-GCM seal (True) or open (False) per jfs_aead_block descriptor."""
+    n = desc.numel() // AEAD_DTYPE.itemsize
+    lib = L.load()
+    fn = lib.jfs_aes256gcm_seal_device if seal else lib.jfs_aes256gcm_open_device
+    _check(fn(desc.data_ptr(), n, ret.data_ptr(), _stream_ptr(stream)), "jfs_aes256gcm")
+
+
 def gen_blocks(out: torch.Tensor, nblk: int, block_bytes: int, cls: str, seed_base: int, stream=None):
     """Fill out[0 : nblk*block_bytes] with synthetic blocks."""
     assert out.numel() >= nblk * block_bytes

@@ -18,6 +18,9 @@ class Oracle:
         lib.oracle_crc32c_update.restype = ctypes.c_uint32
         lib.oracle_crc32c_segments.argtypes = [vp, i64, i64, vp]
         lib.oracle_crc32c_segments.restype = i64
+        for f in (lib.oracle_aes256gcm_seal, lib.oracle_aes256gcm_open):
+            f.argtypes = [vp, vp, vp, i64, vp]
+            f.restype = i64
         self.has_zstd = hasattr(lib, "oracle_zstd_decompress")
         if self.has_zstd:
             lib.oracle_zstd_decompress.argtypes = [vp, i64, vp, i64]
@@ -58,6 +61,18 @@ class Oracle:
         out = ctypes.create_string_buffer(4 * words)
         n = self.lib.oracle_crc32c_segments(data, len(data), seg, out)
         return out.raw[:n]
+
+    def aes256gcm_seal(self, key: bytes, nonce: bytes, pt: bytes) -> bytes:
+        """aead.Seal(nil, nonce, pt, nil) (pkg/object/encrypt.go:255)"""
+        out = ctypes.create_string_buffer(len(pt) + 16)
+        n = self.lib.oracle_aes256gcm_seal(key, nonce, pt, len(pt), out)
+        return out.raw[:n]
+
+    def aes256gcm_open(self, key: bytes, nonce: bytes, ct: bytes):
+        """aead.Open; None when the tag does not verify"""
+        out = ctypes.create_string_buffer(max(len(ct) - 16, 1))
+        n = self.lib.oracle_aes256gcm_open(key, nonce, ct, len(ct), out)
+        return None if n < 0 else out.raw[:n]
 
     def zstd_strict_reserved(self, on: bool):
         self.lib.oracle_zstd_set_strict_reserved(1 if on else 0)

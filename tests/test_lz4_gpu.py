@@ -314,3 +314,23 @@ def test_lz4_far_source_at_block_start(gpu, oracle):
         for i, w in enumerate(want):
             assert r[i] == len(w), (mis, i, r[i], len(w))
             assert oh[offs_d[i]:offs_d[i] + len(w)].tobytes() == w, (mis, i)
+
+
+def test_lz4_encode_long_literal_runs(gpu, oracle):
+    """Literal runs around the encoder's output-ring sizes (the token stays
+    pending while the run streams out) inside text blocks, byte-exact."""
+    c = C.LZ4()
+    srcs = []
+    for i, run in enumerate((960, 1000, 1024, 1040, 1100, 1984, 2000, 2048, 2100, 4000, 4096, 9000)):
+        base = bytearray(gen_block("T", 80 + i, 300000))
+        k = 1000 + 17 * i
+        base[k:k + run] = gen_block("R", 90 + i, run)
+        k2 = 150000 + 31 * i
+        base[k2:k2 + run] = gen_block("R", 190 + i, run)
+        srcs.append(bytes(base))
+    srcs.append(gen_block("R", 7, 2048) + gen_block("T", 8, 5000))
+    pairs = [(bytearray(c.CompressBound(len(s))), s) for s in srcs]
+    res = c.CompressBatch(pairs)
+    for s, (d, _), (n, err) in zip(srcs, pairs, res):
+        m, ref = oracle.lz4_compress(s)
+        assert err is None and n == m and bytes(d[:n]) == ref
