@@ -61,6 +61,25 @@ struct Slot {
     int64_t h_cap = 0;
     uint8_t *d = nullptr;
     int64_t d_cap = 0;
+    // Zstd decode scratch of this slot (planned on the host per chunk)
+    uint8_t *z_lit = nullptr, *z_items = nullptr;
+    uint16_t *z_tabs = nullptr;
+    uint64_t z_lit_cap = 0, z_items_cap = 0, z_tabs_cap = 0;
+
+    bool ensure_zstd(const uint64_t *t) {  // t: items, literal bytes, table cells
+        auto grow = [](auto **p, uint64_t *cap, uint64_t want, size_t elem) {
+            if (*cap >= want) return true;
+            if (*p) (void)hipFree(*p);
+            *p = nullptr;
+            *cap = 0;
+            const uint64_t n = want + want / 4;
+            if (hipMalloc((void **)p, (size_t)(n * elem)) != hipSuccess) return false;
+            *cap = n;
+            return true;
+        };
+        return grow(&z_items, &z_items_cap, t[0], 16) && grow(&z_lit, &z_lit_cap, t[1], 1) &&
+               grow(&z_tabs, &z_tabs_cap, t[2], 2);
+    }
 
     bool ensure(int64_t bytes) {
         const int64_t want = (bytes + (64ll << 20) - 1) & ~((64ll << 20) - 1);  // grow in 64 MiB steps
@@ -102,9 +121,13 @@ struct DevCtx {
         for (Slot &sl : slot) {
             if (sl.h) (void)hipHostFree(sl.h);
             if (sl.d) (void)hipFree(sl.d);
-            sl.h = nullptr;
-            sl.d = nullptr;
+            if (sl.z_lit) (void)hipFree(sl.z_lit);
+            if (sl.z_items) (void)hipFree(sl.z_items);
+            if (sl.z_tabs) (void)hipFree(sl.z_tabs);
+            sl.h = sl.d = sl.z_lit = sl.z_items = nullptr;
+            sl.z_tabs = nullptr;
             sl.h_cap = sl.d_cap = 0;
+            sl.z_lit_cap = sl.z_items_cap = sl.z_tabs_cap = 0;
         }
     }
 };
@@ -205,7 +228,7 @@ void start_janitor() {
                     std::unique_lock<std::mutex> lk(d->mu, std::try_to_lock);
                     if (!lk.owns_lock() || g_exiting) continue;
                     bool any = false;
-                    for (Slot &sl : d->slot) any |= sl.h != nullptr || sl.d != nullptr;
+                    for (Slot &sl : d->slot) any |= sl.h != nullptr || sl.d != nullptr || sl.z_items != nullptr;
                     if (any) release_dev_staging(d);
                 }
             }
@@ -370,25 +393,31 @@ int64_t run_batch(DevCtx *dev, int algo, int dir, int nblk, const jfs_iov *iov, 
             s = c.e;
         }
     }
-    auto layout = [&](const Chunk &c, uint8_t *base, uint8_t **in, uint8_t **outp, jfs_dev_block **desc, int32_t **ret) {
+    // Zstd decode: the per-input scratch plan (ZInfo) rides in the chunk
+    const bool zplan = algo == JFS_ALGO_ZSTD && dir == DECOMPRESS;
+    const int64_t zib = zplan ? (int64_t)jfs_zstd_info_bytes() : 0;
+    auto layout = [&](const Chunk &c, uint8_t *base, uint8_t **in, uint8_t **outp, jfs_dev_block **desc, int32_t **ret,
+                      uint8_t **zinfo) {
         const int64_t desc_bytes = align16((int64_t)(c.e - c.s) * (int64_t)sizeof(jfs_dev_block));
+        const int64_t ret_bytes = align16((int64_t)(c.e - c.s) * 4);
         *in = base;
         *outp = base + c.tin;
         *desc = (jfs_dev_block *)(base + c.tin + c.tout);
         *ret = (int32_t *)(base + c.tin + c.tout + desc_bytes);
+        *zinfo = base + c.tin + c.tout + desc_bytes + ret_bytes;
     };
     auto chunk_bytes = [&](const Chunk &c) {
         return c.tin + c.tout + align16((int64_t)(c.e - c.s) * (int64_t)sizeof(jfs_dev_block)) +
-               align16((int64_t)(c.e - c.s) * 4);
+               align16((int64_t)(c.e - c.s) * 4) + align16((int64_t)(c.e - c.s) * zib);
     };
     auto launch = [&](const Chunk &c) -> int64_t {
         Slot &sl = dev->slot[c.slot];
         if (!sl.ensure(chunk_bytes(c))) return JFS_ERR_NO_MEMORY;
-        uint8_t *h_in, *h_out, *d_in, *d_out;
+        uint8_t *h_in, *h_out, *d_in, *d_out, *h_zi, *d_zi;
         jfs_dev_block *h_desc, *d_desc;
         int32_t *h_ret, *d_ret;
-        layout(c, sl.h, &h_in, &h_out, &h_desc, &h_ret);
-        layout(c, sl.d, &d_in, &d_out, &d_desc, &d_ret);
+        layout(c, sl.h, &h_in, &h_out, &h_desc, &h_ret, &h_zi);
+        layout(c, sl.d, &d_in, &d_out, &d_desc, &d_ret, &d_zi);
         std::vector<CopyJob> jobs;
         for (int i = c.s; i < c.e; i++) {
             const int k = i - c.s;
@@ -404,13 +433,29 @@ int64_t run_batch(DevCtx *dev, int algo, int dir, int nblk, const jfs_iov *iov, 
             fprintf(stderr, "[jfs host] chunk %d-%d stage-in %.1f MiB %.2f ms\n", c.s, c.e, c.tin / 1048576.0, now_ms() - t0);
         const int n = c.e - c.s;
         if (algo != JFS_ALGO_LZ4 && algo != JFS_ALGO_ZSTD) return JFS_ERR_UNSUPPORTED;
+        if (zplan) {  // plan the Zstd scratch from the staged inputs: no device round trip
+            std::vector<const uint8_t *> srcs(n);
+            std::vector<int32_t> lens(n), caps(n);
+            for (int k = 0; k < n; k++) {
+                srcs[k] = h_in + in_off[c.s + k];
+                lens[k] = h_desc[k].src_len;
+                caps[k] = h_desc[k].dst_cap;
+            }
+            uint64_t tot[3];
+            jfs_zstd_plan_host(srcs.data(), lens.data(), caps.data(), n, h_zi, tot);
+            if (!sl.ensure_zstd(tot)) return JFS_ERR_NO_MEMORY;
+        }
         if (hipMemcpyAsync(d_in, h_in, (size_t)c.tin, hipMemcpyHostToDevice, dev->s_in) != hipSuccess) return JFS_ERR_HIP;
         if (hipMemcpyAsync(d_desc, h_desc, (size_t)n * sizeof(jfs_dev_block), hipMemcpyHostToDevice, dev->s_in) !=
             hipSuccess)
             return JFS_ERR_HIP;
+        if (zplan && hipMemcpyAsync(d_zi, h_zi, (size_t)(n * zib), hipMemcpyHostToDevice, dev->s_in) != hipSuccess)
+            return JFS_ERR_HIP;
         if (hipEventRecord(sl.ev_in, dev->s_in) != hipSuccess) return JFS_ERR_HIP;
         if (hipStreamWaitEvent(sl.st, sl.ev_in, 0) != hipSuccess) return JFS_ERR_HIP;
-        if (launch_kernel(algo, dir, d_desc, n, d_ret, sl.st) != 0) return JFS_ERR_HIP;
+        const int lk = zplan ? jfs_launch_zstd_decode_planned(d_desc, n, d_ret, d_zi, sl.z_lit, sl.z_tabs, sl.z_items, sl.st)
+                             : launch_kernel(algo, dir, d_desc, n, d_ret, sl.st);
+        if (lk != 0) return JFS_ERR_HIP;
         if (hipEventRecord(sl.ev_k, sl.st) != hipSuccess) return JFS_ERR_HIP;
         if (hipStreamWaitEvent(dev->s_out, sl.ev_k, 0) != hipSuccess) return JFS_ERR_HIP;
         if (hipMemcpyAsync(h_ret, d_ret, (size_t)n * 4, hipMemcpyDeviceToHost, dev->s_out) != hipSuccess)
@@ -425,10 +470,10 @@ int64_t run_batch(DevCtx *dev, int algo, int dir, int nblk, const jfs_iov *iov, 
         const double t0 = host_trace() ? now_ms() : 0.0;
         if (hipEventSynchronize(sl.ev) != hipSuccess) return JFS_ERR_HIP;
         const double t1 = host_trace() ? now_ms() : 0.0;
-        uint8_t *h_in, *h_out;
+        uint8_t *h_in, *h_out, *h_zi;
         jfs_dev_block *h_desc;
         int32_t *h_ret;
-        layout(c, sl.h, &h_in, &h_out, &h_desc, &h_ret);
+        layout(c, sl.h, &h_in, &h_out, &h_desc, &h_ret, &h_zi);
         std::vector<CopyJob> jobs;
         for (int i = c.s; i < c.e; i++) {
             const int64_t r = finish_result(algo, dir, h_ret[i - c.s]);

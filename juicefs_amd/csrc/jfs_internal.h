@@ -28,6 +28,11 @@ int jfs_launch_lz4_encode(const jfs_dev_block *d_blocks, int nblk, int32_t *d_re
 int jfs_launch_zstd_encode(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, hipStream_t stream);
 int jfs_launch_zstd_decode(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, uint8_t *d_scratch,
                            hipStream_t stream);
+int jfs_launch_zstd_decode_planned(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *d_info,
+                                   uint8_t *d_lit, uint16_t *d_tabs, void *d_items, hipStream_t stream);
+size_t jfs_zstd_info_bytes(void);
+void jfs_zstd_plan_host(const uint8_t *const *srcs, const int32_t *lens, const int32_t *caps, int nblk, void *info_out,
+                        uint64_t *totals);
 int jfs_launch_crc32c(const jfs_dev_block *d_blocks, int nblk, int32_t seg_bytes, uint32_t *d_crc, int32_t *d_ret,
                       hipStream_t stream);
 int jfs_launch_aes256gcm(const jfs_aead_block *d_blocks, int nblk, int mode, int32_t *d_ret, hipStream_t stream);

@@ -25,6 +25,7 @@
 
 #include <stdlib.h>
 
+#include <algorithm>
 #include <mutex>
 #include <vector>
 
@@ -46,7 +47,7 @@ __device__ unsigned long long g_zprof[8];
 #define ZP_ADD(i, v) do { } while (0)
 #endif
 
-enum { E_CORRUPT = -1, E_DSTSMALL = -2, E_SRCSIZE = -3, E_BUG = -100 };
+enum { E_CORRUPT = -1, E_DSTSMALL = -2, E_SRCSIZE = -3, E_SCRATCH = -4, E_BUG = -100 };
 enum { IT_SEQ = 0, IT_FSTART = 1, IT_FEND = 2, IT_BSTART = 3, IT_BEND = 4, IT_ERR = 5, IT_BREP = 6 };
 // Offsets of sequence items may be symbolic: bit 31 set, bits 29-30 = j,
 // bits 0-28 = d  ->  offset = max(1, rep_j - d) with rep_j the repeat-offset
@@ -67,7 +68,7 @@ struct ZInfo {
     uint32_t n_cblk;        // zscan: compressed blocks (TAB_CELLS table cells each)
     uint32_t lit_err_blk;   // zlit: ordinal of the block whose literals failed
     int32_t lit_err_code;
-    uint32_t pad;
+    uint32_t ovf;           // zplan: the scratch cannot hold this input (ret = E_SCRATCH)
 };
 constexpr int TAB_CELLS = 1280;  // u16 FSE cells per compressed block: LL 512, OF 256, ML 512
 
@@ -88,10 +89,10 @@ __constant__ int16_t ML_DEF[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 
 __constant__ int16_t OF_DEF[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1,
                                    1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
 
-__device__ __forceinline__ uint32_t rd8(const gc_u8 *s, int32_t p) { return s[p]; }
-__device__ __forceinline__ uint32_t rd16(const gc_u8 *s, int32_t p) { return s[p] | (s[p + 1] << 8); }
-__device__ __forceinline__ uint32_t rd24(const gc_u8 *s, int32_t p) { return rd16(s, p) | (s[p + 2] << 16); }
-__device__ __forceinline__ uint32_t rd32(const gc_u8 *s, int32_t p) { return rd16(s, p) | (rd16(s, p + 2) << 16); }
+__host__ __device__ __forceinline__ uint32_t rd8(const gc_u8 *s, int32_t p) { return s[p]; }
+__host__ __device__ __forceinline__ uint32_t rd16(const gc_u8 *s, int32_t p) { return s[p] | (s[p + 1] << 8); }
+__host__ __device__ __forceinline__ uint32_t rd24(const gc_u8 *s, int32_t p) { return rd16(s, p) | (s[p + 2] << 16); }
+__host__ __device__ __forceinline__ uint32_t rd32(const gc_u8 *s, int32_t p) { return rd16(s, p) | (rd16(s, p + 2) << 16); }
 
 // ---------------------------------------------------------------------------
 // frame / block walk (ZSTD_decompressMultiFrame + ZSTD_decompressFrame order)
@@ -112,13 +113,13 @@ struct Walk {
     int32_t btype, bsize, bpos;
 };
 
-__device__ __forceinline__ void walk_init(Walk &w, const gc_u8 *s, int32_t n, int32_t cap) {
+__host__ __device__ __forceinline__ void walk_init(Walk &w, const gc_u8 *s, int32_t n, int32_t cap) {
     w.s = s; w.n = n; w.p = 0; w.cap = cap; w.lb = 0; w.phase = 0; w.frames_done = 0; w.after_last = 0;
     w.check = 0; w.has_fcs = 0; w.fcs = 0; w.ordinal = 0; w.btype = 0; w.bsize = 0; w.bpos = 0;
 }
 
 // Next event.  *err for EV_ERROR; for EV_FEND *flags/*chk describe the frame end.
-__device__ __forceinline__ int walk_next(Walk &w, int32_t *err, uint32_t *flags, uint32_t *chk) {
+__host__ __device__ __forceinline__ int walk_next(Walk &w, int32_t *err, uint32_t *flags, uint32_t *chk) {
     const gc_u8 *s = w.s;
     if (w.phase == 2) return EV_DONE;
     if (w.phase == 1 && w.after_last) {
@@ -206,7 +207,7 @@ __device__ __forceinline__ int walk_next(Walk &w, int32_t *err, uint32_t *flags,
 struct LitHdr {
     int32_t type, regen, csize, hsz, streams, sec;
 };
-__device__ __forceinline__ int32_t lit_header(const gc_u8 *s, int32_t bpos, int32_t bsize, LitHdr &h) {
+__host__ __device__ __forceinline__ int32_t lit_header(const gc_u8 *s, int32_t bpos, int32_t bsize, LitHdr &h) {
     if (bsize < 3) return E_CORRUPT;  // MIN_CBLOCK_SIZE
     uint32_t b0 = rd8(s, bpos);
     h.type = b0 & 3;
@@ -246,7 +247,7 @@ __device__ __forceinline__ int32_t lit_header(const gc_u8 *s, int32_t bpos, int3
 }
 
 // nbSeq field (ZSTD_decodeSeqHeaders prefix).  Returns 0 or error; *nseq, *used.
-__device__ __forceinline__ int32_t nbseq_header(const gc_u8 *s, int32_t ip, int32_t end, int32_t *nseq, int32_t *used) {
+__host__ __device__ __forceinline__ int32_t nbseq_header(const gc_u8 *s, int32_t ip, int32_t end, int32_t *nseq, int32_t *used) {
     if (ip >= end) return E_SRCSIZE;
     int32_t v = (int32_t)rd8(s, ip);
     int32_t u = 1;
@@ -629,12 +630,11 @@ __device__ __forceinline__ void build_seq_fse(uint2 *t, const int16_t *norm, int
 // ---------------------------------------------------------------------------
 // kernel 1: header scan -> scratch sizes
 // ---------------------------------------------------------------------------
-__global__ void zscan_kernel(const jfs_dev_block *__restrict__ blocks, int nblk, ZInfo *__restrict__ info) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nblk) return;
-    jfs_dev_block b = blocks[i];
+// Scratch one input needs (exact): items, literal bytes, compressed blocks.
+// Host and device: run_batch plans from the host copy of its inputs.
+__host__ __device__ inline void zscan_one(const gc_u8 *src, int32_t n, int32_t cap, ZInfo &out) {
     Walk w;
-    walk_init(w, (const gc_u8 *)b.src, b.src_len, b.dst_cap);
+    walk_init(w, src, n, cap);
     uint64_t items = 0, lits = 0;
     uint32_t cblk = 0;
     for (;;) {
@@ -663,9 +663,68 @@ __global__ void zscan_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
         cblk++;
         w.lb += (int64_t)h.regen + 3 * (int64_t)nseq;
     }
-    info[i].n_items = (uint32_t)(items + 1);
-    info[i].lit_bytes = (uint32_t)(lits + 16);
-    info[i].n_cblk = cblk;
+    out.n_items = (uint32_t)(items + 1);
+    out.lit_bytes = (uint32_t)(lits + 16);
+    out.n_cblk = cblk;
+}
+
+__global__ void zscan_kernel(const jfs_dev_block *__restrict__ blocks, int nblk, ZInfo *__restrict__ info) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nblk) return;
+    jfs_dev_block b = blocks[i];
+    zscan_one((const gc_u8 *)b.src, b.src_len, b.dst_cap, info[i]);
+}
+
+// Offsets of every input's scratch (exclusive prefix sums over the inputs,
+// one workgroup), the capacity check, and the totals the launch needed
+// (need[0..2] = items, literal bytes, table cells) -- so the host never waits
+// for zscan: an input that does not fit the current scratch reports
+// E_SCRATCH and the library grows the scratch for the next call.
+constexpr int PLAN_T = 1024;
+__global__ __launch_bounds__(PLAN_T) void zplan_kernel(ZInfo *__restrict__ info, int nblk, uint64_t cap_items,
+                                                       uint64_t cap_lits, uint64_t cap_tabs,
+                                                       uint64_t *__restrict__ need) {
+    __shared__ uint64_t sh[3][PLAN_T];
+    const int t = threadIdx.x;
+    const int per = (nblk + PLAN_T - 1) / PLAN_T;
+    const int b0 = t * per, b1 = b0 + per < nblk ? b0 + per : nblk;
+    uint64_t a = 0, c = 0, d = 0;
+    for (int i = b0; i < b1; i++) {
+        a += info[i].n_items;
+        c += (info[i].lit_bytes + 15u) & ~15u;
+        d += (uint64_t)info[i].n_cblk * TAB_CELLS;
+    }
+    sh[0][t] = a;
+    sh[1][t] = c;
+    sh[2][t] = d;
+    __syncthreads();
+    for (int o = 1; o < PLAN_T; o <<= 1) {  // inclusive scan (Hillis-Steele)
+        uint64_t x0 = 0, x1 = 0, x2 = 0;
+        if (t >= o) { x0 = sh[0][t - o]; x1 = sh[1][t - o]; x2 = sh[2][t - o]; }
+        __syncthreads();
+        sh[0][t] += x0;
+        sh[1][t] += x1;
+        sh[2][t] += x2;
+        __syncthreads();
+    }
+    uint64_t oi = sh[0][t] - a, ol = sh[1][t] - c, ot = sh[2][t] - d;
+    for (int i = b0; i < b1; i++) {
+        ZInfo &z = info[i];
+        z.item_off = oi;
+        z.lit_off = ol;
+        z.tab_off = ot;
+        z.lit_err_blk = 0xFFFFFFFFu;
+        z.lit_err_code = 0;
+        oi += z.n_items;
+        ol += (z.lit_bytes + 15u) & ~15u;
+        ot += (uint64_t)z.n_cblk * TAB_CELLS;
+        z.ovf = (oi + 64 > cap_items || ol + 4096 + 64 > cap_lits || ot + 64 > cap_tabs) ? 1u : 0u;
+    }
+    if (t == PLAN_T - 1) {
+        need[0] = sh[0][t];
+        need[1] = sh[1][t];
+        need[2] = sh[2][t];
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -942,6 +1001,7 @@ __global__ __launch_bounds__(64) void zlit_kernel(const jfs_dev_block *__restric
     const int bi = blockIdx.x;
     if (bi >= nblk) return;
     const jfs_dev_block b = blocks[bi];
+    if (info[bi].ovf) return;
     lit_wave(sm, b, info[bi], (g_u8 *)litbuf);
 }
 
@@ -1178,6 +1238,7 @@ __global__ __launch_bounds__(64) void zseq_kernel(const jfs_dev_block *__restric
         if (bi >= nblk) break;
         const jfs_dev_block b = blocks[bi];
         ZInfo &zi = info[bi];
+        if (zi.ovf) continue;
         const gc_u8 *s = (const gc_u8 *)b.src;
         g_u16 *tabs = (g_u16 *)tabs_all + zi.tab_off;
         g_u4 *items = (g_u4 *)items_all + zi.item_off;
@@ -1651,6 +1712,7 @@ __global__ __launch_bounds__(64) void zexec_kernel(const jfs_dev_block *__restri
     __builtin_amdgcn_wave_barrier();
     x.dmis = (uint32_t)((uintptr_t)b.dst & 15u);
     int32_t result = E_BUG;
+    if (zi.ovf) { if (l == 0) ret[bi] = E_SCRATCH; return; }
     if (zi.n_items == 0xFFFFFFFFu) { if (l == 0) ret[bi] = -103; return; }
     const gc_u4 *it = (const gc_u4 *)items + zi.item_off;
     const uint32_t nit = zi.n_items;
@@ -1749,9 +1811,10 @@ __global__ __launch_bounds__(64) void zexec_kernel(const jfs_dev_block *__restri
 // host launcher: scan -> size scratch -> entropy -> execute
 // ---------------------------------------------------------------------------
 namespace {
+// Scratch of one stream of launches: the entropy decoders' outputs (items,
+// literal bytes, FSE table cells) and the per-input plan.
 struct ZScratch {
-    int dev = -1;
-    jfs::zstdd::ZInfo *d_info = nullptr, *h_info = nullptr;
+    jfs::zstdd::ZInfo *d_info = nullptr;
     size_t info_cap = 0;
     uint8_t *d_lit = nullptr;
     size_t lit_cap = 0;
@@ -1759,6 +1822,12 @@ struct ZScratch {
     size_t items_cap = 0;
     uint16_t *d_tabs = nullptr;
     size_t tabs_cap = 0;
+    // device API only: the totals the previous launch needed (read once its
+    // copy has landed; no host wait), and the event that orders launches that
+    // share this scratch on different streams
+    uint64_t *d_need = nullptr, *h_need = nullptr;
+    hipEvent_t ev_need = nullptr, ev_done = nullptr;
+    bool pending = false;
     std::mutex mu;
 };
 ZScratch g_scr[16];
@@ -1777,8 +1846,24 @@ bool grow_dev(T **p, size_t *cap, size_t need) {
 // reference pins 1.5.6); see oracle/zstd_oracle.c.
 constexpr int g_strict_reserved = 1;
 
+int launch_entropy_exec(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, jfs::zstdd::ZInfo *d_info,
+                        uint8_t *d_lit, uint16_t *d_tabs, uint4 *d_items, hipStream_t stream) {
+    using namespace jfs::zstdd;
+    hipLaunchKernelGGL(zlit_kernel, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, d_info, d_lit);
+    if (hipGetLastError() != hipSuccess) return -1;
+    hipLaunchKernelGGL(zseq_kernel, dim3((nblk + ZSEQ_INPUTS - 1) / ZSEQ_INPUTS), dim3(64), 0, stream, d_blocks, nblk,
+                       d_info, d_tabs, d_items, g_strict_reserved);
+    if (hipGetLastError() != hipSuccess) return -1;
+    hipLaunchKernelGGL(zexec_kernel, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, d_info, d_lit, d_items, d_ret);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 }  // namespace
 
+// Device API: zscan -> zplan -> entropy -> execute, all enqueued on `stream`
+// with no host wait.  An input that does not fit the device's scratch gets
+// ret = -4 (E_SCRATCH); the totals the launch needed come back through a
+// pinned copy and the next call grows the scratch before it launches (the
+// only host wait: freeing scratch an earlier launch may still use).
 extern "C" int jfs_launch_zstd_decode(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, uint8_t *,
                                       hipStream_t stream) {
     using namespace jfs::zstdd;
@@ -1787,47 +1872,87 @@ extern "C" int jfs_launch_zstd_decode(const jfs_dev_block *d_blocks, int nblk, i
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return -1;
     ZScratch &z = g_scr[dev];
     std::lock_guard<std::mutex> lk(z.mu);
-    if (z.info_cap < (size_t)nblk) {
-        if (z.d_info) (void)hipFree(z.d_info);
-        if (z.h_info) (void)hipHostFree(z.h_info);
-        z.d_info = nullptr; z.h_info = nullptr; z.info_cap = 0;
-        if (hipMalloc((void **)&z.d_info, sizeof(ZInfo) * nblk) != hipSuccess) return -1;
-        if (hipHostMalloc((void **)&z.h_info, sizeof(ZInfo) * nblk, hipHostMallocDefault) != hipSuccess) return -1;
-        z.info_cap = nblk;
+    if (!z.d_need) {
+        if (hipMalloc((void **)&z.d_need, 3 * sizeof(uint64_t)) != hipSuccess) return -1;
+        if (hipHostMalloc((void **)&z.h_need, 3 * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess) return -1;
+        if (hipEventCreateWithFlags(&z.ev_need, hipEventDisableTiming) != hipSuccess) return -1;
+        if (hipEventCreateWithFlags(&z.ev_done, hipEventDisableTiming) != hipSuccess) return -1;
+        z.h_need[0] = z.h_need[1] = z.h_need[2] = 0;
     }
+    // what the previous launch needed, if its copy has landed
+    uint64_t want_items = 0, want_lits = 0, want_tabs = 0;
+    if (z.pending && hipEventQuery(z.ev_need) == hipSuccess) {
+        want_items = z.h_need[0];
+        want_lits = z.h_need[1];
+        want_tabs = z.h_need[2];
+        z.pending = false;
+    }
+    // a first sizing guess: 4 KiB of items and 1 KiB of literals per input
+    want_items = std::max<uint64_t>(want_items + 64, (uint64_t)nblk * 256);
+    want_lits = std::max<uint64_t>(want_lits + 4096 + 64, (uint64_t)nblk * 1024);
+    want_tabs = std::max<uint64_t>(want_tabs + 64, (uint64_t)nblk * 4 * TAB_CELLS);
+    const bool grow = want_items > z.items_cap || want_lits > z.lit_cap || want_tabs > z.tabs_cap ||
+                      (size_t)nblk > z.info_cap;
+    if (grow) {
+        // earlier launches (any stream) may still read the old scratch
+        if (hipEventSynchronize(z.ev_done) != hipSuccess) return -1;
+        if (!grow_dev(&z.d_items, &z.items_cap, want_items)) return -1;
+        if (!grow_dev(&z.d_lit, &z.lit_cap, want_lits)) return -1;
+        if (!grow_dev(&z.d_tabs, &z.tabs_cap, want_tabs)) return -1;
+        if (!grow_dev(&z.d_info, &z.info_cap, (size_t)nblk)) return -1;
+    }
+    // launches that share the scratch run in call order across streams
+    if (hipStreamWaitEvent(stream, z.ev_done, 0) != hipSuccess) return -1;
     hipLaunchKernelGGL(zscan_kernel, dim3((nblk + 63) / 64), dim3(64), 0, stream, d_blocks, nblk, z.d_info);
     if (hipGetLastError() != hipSuccess) return -1;
-    if (hipMemcpyAsync(z.h_info, z.d_info, sizeof(ZInfo) * nblk, hipMemcpyDeviceToHost, stream) != hipSuccess)
-        return -1;
-    if (hipStreamSynchronize(stream) != hipSuccess) return -1;
-    uint64_t items = 0, lits = 0, tabs = 0;
-    for (int i = 0; i < nblk; i++) {
-        z.h_info[i].item_off = items;
-        z.h_info[i].lit_off = lits;
-        z.h_info[i].tab_off = tabs;
-        items += z.h_info[i].n_items;
-        lits += (z.h_info[i].lit_bytes + 15) & ~15u;
-        tabs += (uint64_t)z.h_info[i].n_cblk * TAB_CELLS;
-        z.h_info[i].lit_err_blk = 0xFFFFFFFFu;
-        z.h_info[i].lit_err_code = 0;
+    hipLaunchKernelGGL(zplan_kernel, dim3(1), dim3(PLAN_T), 0, stream, z.d_info, nblk, (uint64_t)z.items_cap,
+                       (uint64_t)z.lit_cap, (uint64_t)z.tabs_cap, z.d_need);
+    if (hipGetLastError() != hipSuccess) return -1;
+    if (!z.pending) {  // report the totals back (the pinned record is free again)
+        if (hipMemcpyAsync(z.h_need, z.d_need, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, stream) != hipSuccess)
+            return -1;
+        if (hipEventRecord(z.ev_need, stream) != hipSuccess) return -1;
+        z.pending = true;
     }
-    if (!grow_dev(&z.d_items, &z.items_cap, items + 64)) return -1;
-    if (!grow_dev(&z.d_lit, &z.lit_cap, lits + 4096 + 64)) return -1;
-    if (!grow_dev(&z.d_tabs, &z.tabs_cap, tabs + 64)) return -1;
-    if (hipMemcpyAsync(z.d_info, z.h_info, sizeof(ZInfo) * nblk, hipMemcpyHostToDevice, stream) != hipSuccess)
-        return -1;
-    hipLaunchKernelGGL(zlit_kernel, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, z.d_info, z.d_lit);
-    if (hipGetLastError() != hipSuccess) return -1;
-    hipLaunchKernelGGL(zseq_kernel, dim3((nblk + ZSEQ_INPUTS - 1) / ZSEQ_INPUTS), dim3(64), 0, stream, d_blocks, nblk,
-                       z.d_info, z.d_tabs, z.d_items,
-                       g_strict_reserved);
-    if (hipGetLastError() != hipSuccess) return -1;
-    hipLaunchKernelGGL(zexec_kernel, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, z.d_info, z.d_lit, z.d_items,
-                       d_ret);
-    if (hipGetLastError() != hipSuccess) return -1;
-    // keep the pinned mirror alive until the H2D copy has run
-    if (hipStreamSynchronize(stream) != hipSuccess) return -1;
-    return 0;
+    if (launch_entropy_exec(d_blocks, nblk, d_ret, z.d_info, z.d_lit, z.d_tabs, z.d_items, stream) != 0) return -1;
+    return hipEventRecord(z.ev_done, stream) == hipSuccess ? 0 : -1;
+}
+
+// Batch path (capi.hip run_batch): the caller planned the scratch on the host
+// from its host copy of the inputs (jfs_zstd_plan_host) and owns the scratch
+// (one per staging slot), so nothing is shared and nothing waits.
+extern "C" int jfs_launch_zstd_decode_planned(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *d_info,
+                                              uint8_t *d_lit, uint16_t *d_tabs, void *d_items, hipStream_t stream) {
+    if (nblk <= 0) return 0;
+    return launch_entropy_exec(d_blocks, nblk, d_ret, (jfs::zstdd::ZInfo *)d_info, d_lit, d_tabs, (uint4 *)d_items,
+                               stream);
+}
+
+// Host plan of a batch: info[i] (ZInfo, 48 bytes each) from the host copy of
+// input i; returns the scratch totals (items, literal bytes, table cells).
+extern "C" size_t jfs_zstd_info_bytes(void) { return sizeof(jfs::zstdd::ZInfo); }
+extern "C" void jfs_zstd_plan_host(const uint8_t *const *srcs, const int32_t *lens, const int32_t *caps, int nblk,
+                                   void *info_out, uint64_t *totals) {
+    using namespace jfs::zstdd;
+    ZInfo *info = (ZInfo *)info_out;
+    uint64_t oi = 0, ol = 0, ot = 0;
+    for (int i = 0; i < nblk; i++) {
+        ZInfo &z = info[i];
+        z = ZInfo{};
+        zscan_one((const gc_u8 *)srcs[i], lens[i], caps[i], z);
+        z.item_off = oi;
+        z.lit_off = ol;
+        z.tab_off = ot;
+        z.lit_err_blk = 0xFFFFFFFFu;
+        z.lit_err_code = 0;
+        z.ovf = 0;
+        oi += z.n_items;
+        ol += (z.lit_bytes + 15u) & ~15u;
+        ot += (uint64_t)z.n_cblk * TAB_CELLS;
+    }
+    totals[0] = oi + 64;
+    totals[1] = ol + 4096 + 64;
+    totals[2] = ot + 64;
 }
 
 #ifdef JFS_PROF

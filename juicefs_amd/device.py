@@ -59,6 +59,21 @@ def zstd_decompress(desc: torch.Tensor, ret: torch.Tensor, stream=None):
            "jfs_zstd_decompress_device")
 
 
+ZSTD_ERR_SCRATCH = -4  # the device's scratch was too small for this input: submit it again
+
+
+def zstd_decompress_sync(desc: torch.Tensor, ret: torch.Tensor, stream=None, tries: int = 3):
+    """zstd_decompress, waited for; inputs answered ZSTD_ERR_SCRATCH (the
+    library sizes its scratch from the previous call's needs, asynchronously)
+    are submitted again."""
+    for _ in range(tries):
+        zstd_decompress(desc, ret, stream)
+        torch.cuda.synchronize()
+        if not bool((ret == ZSTD_ERR_SCRATCH).any().item()):
+            return
+    raise RuntimeError("jfs_zstd_decompress_device: scratch did not grow")
+
+
 def zstd_compress(desc: torch.Tensor, ret: torch.Tensor, stream=None):
     n = desc.numel() // DESC_DTYPE.itemsize
     _check(L.load().jfs_zstd_compress_device(desc.data_ptr(), n, ret.data_ptr(), _stream_ptr(stream)),
@@ -189,8 +204,7 @@ def zstd_compress_rate(nblk: int, block_bytes: int, cls: str = "T", seed_base: i
     out = torch.empty(nblk * block_bytes, dtype=torch.uint8, device=dev)
     ddesc = make_desc(comp, offs * slot, csize, out, offs * block_bytes, [block_bytes] * nblk)
     dret = torch.empty(nblk, dtype=torch.int32, device=dev)
-    zstd_decompress(ddesc, dret)
-    torch.cuda.synchronize()
+    zstd_decompress_sync(ddesc, dret)
     if not (bool((dret == block_bytes).all().item()) and torch.equal(out, raw)):
         raise RuntimeError("Zstd round trip mismatch")
     return nblk * block_bytes / (ms / 1e3) / 2**30, nblk * block_bytes / float(csize.sum()), ms
@@ -277,6 +291,7 @@ class ZstdBatch:
         self.dec_desc = make_desc(self.comp, offs * self.slot, self.csize, self.out, offs * block_bytes,
                                   [block_bytes] * nblk)
         self.dec_ret = torch.empty(nblk, dtype=torch.int32, device=self.device)
+        zstd_decompress_sync(self.dec_desc, self.dec_ret)  # sizes the device scratch for this batch
 
     def decompress(self, stream=None):
         zstd_decompress(self.dec_desc, self.dec_ret, stream)
