@@ -15,7 +15,10 @@
 //      in LDS, acceleration skip on misses like LZ4's, forward extension 64
 //      bytes per step across the wave, backward catch-up); literals go
 //      straight to the output, sequences to a per-input scratch list;
-//   2. literals section: Raw_Literals_Block;
+//   2. literals section: Huffman-compressed (Compressed_Literals_Block, 4
+//      streams, code lengths <= 11, the tree description FSE-compressed or as
+//      direct 4-bit weights), RLE for one repeated byte, else raw -- whichever
+//      is smallest, like HUF_compress in libzstd;
 //   3. sequences section: Predefined_Mode for all three codes (no table
 //      descriptions), FSE-encoded backwards exactly as RFC 8878 section 4.1.2
 //      reads it (offsets are sent as offset + 3: no repeat codes);
@@ -33,7 +36,10 @@ namespace zstde {
 
 constexpr int32_t BLK = 128 << 10;          // Block_Maximum_Size
 constexpr int64_t SEQ_CAP = BLK / 4 + 64;   // sequences per block (every match is >= 4 bytes)
-constexpr int64_t SCR_PER = SEQ_CAP * 8;    // scratch bytes per input
+constexpr int64_t LSTREAM = 36 << 10;       // one Huffman stream (<= 32 KiB of literals) in scratch
+constexpr int64_t SCR_PER = SEQ_CAP * 8 + 4 * LSTREAM;  // scratch bytes per input
+constexpr int HUF_MAXB = 11;                // code length limit (HUF_TABLELOG_DEFAULT)
+constexpr int HUF_MINL = 64;                // fewer literals stay raw
 constexpr int32_t HBITS = 12;               // hash table: 4096 positions
 
 // RFC 8878 3.1.1.3.2.1 code tables and 3.1.1.3.2.2 predefined distributions
@@ -56,17 +62,40 @@ __constant__ int16_t OF_DEF[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1,
 
 // FSE compression table (FSE_buildCTable semantics) of one code type
 struct CTab {
-    uint16_t st[64];   // state table: tableSize + spread position, by cumulative symbol rank
+    uint16_t st[512];  // state table: tableSize + spread position, by cumulative symbol rank
     int32_t dnb[53];   // deltaNbBits
     int32_t dfs[53];   // deltaFindState
+};
+
+// Huffman literal coding state of the current block (lane 0 builds, lanes 0-3 encode)
+struct HufSmem {
+    uint32_t cnt[256];
+    uint32_t w[512];    // tree node weights (leaves 0..n-1, sorted by count)
+    uint16_t par[512];
+    uint8_t dep[512];
+    uint16_t sym[256];  // leaf -> symbol
+    uint16_t code[256];
+    uint8_t len[256];
+    uint8_t wt[256];    // Huffman weights of symbols 0..maxsym
+    int16_t norm[16];   // FSE normalized counts of the weights
+    uint8_t hdr[192];   // tree description (header byte first)
+    int32_t hsize, maxbits, maxsym, nsym;
+    int32_t ssz[4];     // stream sizes
 };
 
 struct Smem {
     uint32_t table[1 << HBITS];
     CTab ct[3];  // 0 LL (log 6), 1 ML (log 6), 2 OF (log 5)
+    CTab wct;    // Huffman weights (log 6)
+    CTab act[3]; // FSE_Compressed tables of the current block (LL, ML, OF)
     uint8_t lut_ll[64], lut_ml[128];
-    uint8_t tsym[64];
+    uint8_t tsym[512];
     int32_t cumul[64];
+    uint32_t scnt[3][64];  // code histograms of the current block's sequences
+    int16_t snorm[3][64];
+    uint8_t shdr[3][96];   // their normalized-count headers
+    int32_t shsz[3], smode[3], slog[3];
+    HufSmem h;
 };
 
 __device__ __forceinline__ uint32_t highbit(uint32_t v) { return 31u - (uint32_t)__builtin_clz(v); }
@@ -132,6 +161,27 @@ __device__ __forceinline__ uint32_t ld32u(const gc_u8 *p) {
 }
 
 __device__ __forceinline__ uint32_t hash4(uint32_t v) { return (v * 2654435761u) >> (32 - HBITS); }
+// ZSTD_hash6Ptr: the low 6 bytes of an 8-byte little-endian read
+__device__ __forceinline__ uint32_t hash6(uint64_t v) { return (uint32_t)(((v << 16) * 227718039650203ull) >> (64 - HBITS)); }
+__device__ __forceinline__ uint64_t ld64u(const gc_u8 *p) {
+    const uintptr_t a = (uintptr_t)p;
+    const gc_u32 *w = (const gc_u32 *)(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3);
+    const uint32_t w0 = w[0], w1 = w[1];
+    if (sh == 0) return (uint64_t)w0 | ((uint64_t)w1 << 32);
+    const uint32_t w2 = w[2];
+    return (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32);
+}
+#ifndef JFS_ZE_WLOG
+#define JFS_ZE_WLOG 19
+#endif
+#ifndef JFS_ZE_HASH
+#define JFS_ZE_HASH 4  // bytes hashed for match candidates (libzstd level 1: 6)
+#endif
+#ifndef JFS_ZE_REP
+#define JFS_ZE_REP 1   // try the repeat offset one byte ahead first (zstd_fast)
+#endif
+constexpr int64_t WMAX = 1 << JFS_ZE_WLOG;  // match window (windowLog 19, like level 1)
 
 // ---------------------------------------------------------------------------
 // backward bitstream writer (BIT_CStream semantics), uniform; bytes go to HBM
@@ -186,14 +236,17 @@ __device__ __forceinline__ void seq_fields(const uint64_t *seq, int64_t i, uint3
     off = (uint32_t)(r >> 35);
 }
 
-// Encode sequences [0, ns) (scratch records: ll | ml << 17 | off << 35 as
+// Encode sequences [0, ns) (scratch records: ll | ml << 17 | Offset_Value << 35 as
 // u64) as the predefined-mode FSE bitstream at w.wp (ZSTD_encodeSequences
 // order: last sequence first, states OF/ML/LL, extra bits LL/ML/OF).
 __device__ void encode_sequences(const Smem &s, BitW &w, const uint64_t *seq, int64_t ns) {
-    const CTab &TL = s.ct[0], &TM = s.ct[1], &TO = s.ct[2];
+    // per table: the block's FSE_Compressed table (mode 2) or the predefined one
+    const CTab &TL = s.smode[0] == 2 ? s.act[0] : s.ct[0];
+    const CTab &TM = s.smode[1] == 2 ? s.act[1] : s.ct[1];
+    const CTab &TO = s.smode[2] == 2 ? s.act[2] : s.ct[2];
     uint32_t ll, ml, off;
     seq_fields(seq, ns - 1, ll, ml, off);
-    uint32_t lc = ll_code(s, ll), mc = ml_code(s, ml - 3), ofv = off + 3, oc = highbit(ofv);
+    uint32_t lc = ll_code(s, ll), mc = ml_code(s, ml - 3), ofv = off, oc = highbit(ofv);
     uint32_t sML = fse_init(TM, mc), sOF = fse_init(TO, oc), sLL = fse_init(TL, lc);
     bw_add(w, ll - LL_BASE[lc], LL_BITS[lc]);
     bw_add(w, ml - ML_BASE[mc], ML_BITS[mc]);
@@ -204,7 +257,7 @@ __device__ void encode_sequences(const Smem &s, BitW &w, const uint64_t *seq, in
         seq_fields(seq, i, ll, ml, off);
         lc = ll_code(s, ll);
         mc = ml_code(s, ml - 3);
-        ofv = off + 3;
+        ofv = off;
         oc = highbit(ofv);
         fse_enc(w, TO, sOF, oc);
         fse_enc(w, TM, sML, mc);
@@ -216,9 +269,9 @@ __device__ void encode_sequences(const Smem &s, BitW &w, const uint64_t *seq, in
         bw_add(w, ofv - (1u << oc), (int)oc);
         bw_flush(w);
     }
-    fse_fin(w, sML, 6);
-    fse_fin(w, sOF, 5);
-    fse_fin(w, sLL, 6);
+    fse_fin(w, sML, s.slog[1]);
+    fse_fin(w, sOF, s.slog[2]);
+    fse_fin(w, sLL, s.slog[0]);
     bw_add(w, 1, 1);  // end mark
     bw_flush(w);
     if (w.bp > 0) {   // last partial byte
@@ -228,6 +281,374 @@ __device__ void encode_sequences(const Smem &s, BitW &w, const uint64_t *seq, in
         w.bp = 0;
         w.bc = 0;
     }
+}
+
+
+// ---------------------------------------------------------------------------
+// Huffman-compressed literals (RFC 8878 4.2.1; the choices of libzstd's
+// HUF_compress: code lengths limited to 11, 4 streams, tree description
+// FSE-compressed with two interleaved states or as direct 4-bit weights)
+// ---------------------------------------------------------------------------
+// FSE normalized-count header (RFC 8878 4.1.1; FSE_writeNCount layout).
+__device__ int write_ncount(uint8_t *out, const int16_t *norm, int maxsv, int tlog) {
+    int o = 0;
+    const int tsize = 1 << tlog;
+    int remaining = tsize + 1, threshold = tsize, nbits = tlog + 1;
+    uint32_t bs = (uint32_t)(tlog - 5);
+    int bc = 4;
+    int sym = 0, prev0 = 0;
+    const int alpha = maxsv + 1;
+    while (sym < alpha && remaining > 1) {
+        if (prev0) {
+            int start = sym;
+            while (sym < alpha && !norm[sym]) sym++;
+            if (sym == alpha) break;
+            while (sym >= start + 24) {
+                start += 24;
+                bs += 0xFFFFu << bc;
+                out[o] = (uint8_t)bs;
+                out[o + 1] = (uint8_t)(bs >> 8);
+                o += 2;
+                bs >>= 16;
+            }
+            while (sym >= start + 3) {
+                start += 3;
+                bs += 3u << bc;
+                bc += 2;
+            }
+            bs += (uint32_t)(sym - start) << bc;
+            bc += 2;
+            if (bc > 16) {
+                out[o] = (uint8_t)bs;
+                out[o + 1] = (uint8_t)(bs >> 8);
+                o += 2;
+                bs >>= 16;
+                bc -= 16;
+            }
+        }
+        int count = norm[sym++];
+        const int max = (2 * threshold - 1) - remaining;
+        remaining -= count < 0 ? -count : count;
+        count++;
+        if (count >= threshold) count += max;
+        bs += (uint32_t)count << bc;
+        bc += nbits;
+        bc -= count < max ? 1 : 0;
+        prev0 = count == 1;
+        while (remaining < threshold) {
+            nbits--;
+            threshold >>= 1;
+        }
+        if (bc > 16) {
+            out[o] = (uint8_t)bs;
+            out[o + 1] = (uint8_t)(bs >> 8);
+            o += 2;
+            bs >>= 16;
+            bc -= 16;
+        }
+    }
+    out[o] = (uint8_t)bs;
+    out[o + 1] = (uint8_t)(bs >> 8);
+    o += (bc + 7) / 8;
+    return o;
+}
+
+// lane-local backward bitstream into LDS (the tree description)
+struct LBits {
+    uint8_t *out;
+    int o, lim;
+    uint64_t bc;
+    int bp;
+};
+__device__ __forceinline__ void lb_add(LBits &b, uint32_t v, int nb) {
+    b.bc |= ((uint64_t)v & ((1ull << nb) - 1ull)) << b.bp;
+    b.bp += nb;
+}
+__device__ __forceinline__ void lb_flush(LBits &b) {
+    while (b.bp >= 8) {
+        if (b.o < b.lim) b.out[b.o] = (uint8_t)b.bc;
+        b.o++;
+        b.bc >>= 8;
+        b.bp -= 8;
+    }
+}
+__device__ __forceinline__ void lb_enc(LBits &b, const CTab &t, uint32_t &st, uint32_t sym) {
+    const uint32_t nbo = (uint32_t)(((int32_t)st + t.dnb[sym]) >> 16);
+    lb_add(b, st, (int)nbo);
+    st = t.st[(st >> nbo) + (uint32_t)t.dfs[sym]];
+}
+
+// Code lengths (<= HUF_MAXB, complete code) of the counted literals; lane 0.
+// Returns max length, 0 when Huffman does not apply (fewer than 2 symbols or
+// no exact length limit found).
+__device__ int huf_build(HufSmem &h) {
+    int n = 0;
+    for (int c = 0; c < 256; c++) {
+        h.len[c] = 0;
+        if (h.cnt[c]) h.sym[n++] = (uint16_t)c;
+    }
+    h.nsym = n;
+    if (n < 2) return 0;
+    for (int i = 1; i < n; i++) {  // insertion sort by count (stable in symbol order)
+        const uint16_t x = h.sym[i];
+        const uint32_t cx = h.cnt[x];
+        int j = i - 1;
+        while (j >= 0 && h.cnt[h.sym[j]] > cx) {
+            h.sym[j + 1] = h.sym[j];
+            j--;
+        }
+        h.sym[j + 1] = x;
+    }
+    for (int i = 0; i < n; i++) h.w[i] = h.cnt[h.sym[i]];
+    int li = 0, qi = n;
+    for (int k = n; k < 2 * n - 1; k++) {  // two-queue merge
+        int x, y;
+        if (li < n && (qi >= k || h.w[li] <= h.w[qi])) x = li++;
+        else x = qi++;
+        if (li < n && (qi >= k || h.w[li] <= h.w[qi])) y = li++;
+        else y = qi++;
+        h.w[k] = h.w[x] + h.w[y];
+        h.par[x] = h.par[y] = (uint16_t)k;
+    }
+    const int root = 2 * n - 2;
+    h.dep[root] = 0;
+    for (int k = root - 1; k >= 0; k--) h.dep[k] = (uint8_t)(h.dep[h.par[k]] + 1);
+    // limit to HUF_MAXB: clamp; while the code is over-subscribed lengthen the
+    // rarest code still below the limit; then, while under-subscribed, shorten
+    // the most frequent codes whose step still fits (Kraft sum in units of
+    // 2^-HUF_MAXB; every step is a power of two and codes at the limit step
+    // by 1, so the sum lands exactly on 2^HUF_MAXB: a complete prefix code)
+    const int64_t full = 1ll << HUF_MAXB;
+    int64_t kraft = 0;
+    for (int i = 0; i < n; i++) {
+        const int d = h.dep[i] > HUF_MAXB ? HUF_MAXB : h.dep[i];
+        h.dep[i] = (uint8_t)d;
+        kraft += 1ll << (HUF_MAXB - d);
+    }
+    for (int guard = 0; kraft > full && guard < 4096; guard++) {
+        int i = 0;  // leaves are sorted by count: index 0 is the rarest
+        while (i < n && h.dep[i] >= HUF_MAXB) i++;
+        if (i == n) return 0;
+        kraft -= 1ll << (HUF_MAXB - h.dep[i] - 1);
+        h.dep[i]++;
+    }
+    for (int guard = 0; kraft < full && guard < 64; guard++) {
+        for (int i = n - 1; i >= 0 && kraft < full; i--) {  // most frequent first
+            const int64_t add = h.dep[i] > 1 ? 1ll << (HUF_MAXB - h.dep[i]) : full;
+            if (kraft + add <= full) {
+                h.dep[i]--;
+                kraft += add;
+            }
+        }
+    }
+    if (kraft != full) return 0;
+    int maxb = 0;
+    for (int i = 0; i < n; i++) {
+        h.len[h.sym[i]] = h.dep[i];
+        maxb = h.dep[i] > maxb ? h.dep[i] : maxb;
+    }
+    // canonical codes: longest first, symbol order within a length
+    uint32_t c = 0;
+    for (int nb = maxb; nb >= 1; nb--) {
+        for (int v = 0; v < 256; v++)
+            if (h.len[v] == nb) h.code[v] = (uint16_t)c++;
+        c >>= 1;
+    }
+    int maxsym = 0;
+    for (int v = 0; v < 256; v++) {
+        h.wt[v] = h.len[v] ? (uint8_t)(maxb + 1 - h.len[v]) : 0;
+        if (h.len[v]) maxsym = v;
+    }
+    h.maxsym = maxsym;
+    return maxb;
+}
+
+// Tree description into h.hdr: FSE-compressed weights (2 states, table log
+// 6) when that is smaller, else direct 4-bit weights (<= 128 transmitted).
+// Returns its size, or -1 when neither applies.  Lane 0 (uses s.tsym/cumul).
+__device__ int huf_describe(Smem &s) {
+    HufSmem &h = s.h;
+    const int nw = h.maxsym;  // weights of symbols 0..maxsym-1 (the last one is implied)
+    int fse = -1;
+    if (nw >= 2) {
+        int wc[16] = {0};
+        int maxsv = 0;
+        for (int i = 0; i < nw; i++) {
+            wc[h.wt[i]]++;
+            maxsv = h.wt[i] > maxsv ? h.wt[i] : maxsv;
+        }
+        const int tlog = 6, tsize = 1 << tlog;
+        int sum = 0, big = 0;
+        for (int v = 0; v <= maxsv; v++) {
+            h.norm[v] = (int16_t)(wc[v] ? (wc[v] * tsize / nw > 0 ? wc[v] * tsize / nw : 1) : 0);
+            sum += h.norm[v];
+            if (wc[v] > wc[big]) big = v;
+        }
+        h.norm[big] = (int16_t)(h.norm[big] + (tsize - sum));
+        if (h.norm[big] >= 1) {
+            int o = 1 + write_ncount(h.hdr + 1, h.norm, maxsv, tlog);
+            build_ctab(s, s.wct, h.norm, maxsv, tlog);
+            LBits b;
+            b.out = h.hdr;
+            b.o = o;
+            b.lim = 128;
+            b.bc = 0;
+            b.bp = 0;
+            // FSE_compress_usingCTable order: two states, last symbols first
+            int ip = nw;
+            uint32_t s1, s2;
+            if (nw & 1) {
+                s1 = fse_init(s.wct, h.wt[--ip]);
+                s2 = fse_init(s.wct, h.wt[--ip]);
+                lb_enc(b, s.wct, s1, h.wt[--ip]);
+                lb_flush(b);
+            } else {
+                s2 = fse_init(s.wct, h.wt[--ip]);
+                s1 = fse_init(s.wct, h.wt[--ip]);
+            }
+            if ((nw - 2) & 2) {
+                lb_enc(b, s.wct, s2, h.wt[--ip]);
+                lb_enc(b, s.wct, s1, h.wt[--ip]);
+                lb_flush(b);
+            }
+            while (ip > 0) {
+                lb_enc(b, s.wct, s2, h.wt[--ip]);
+                lb_enc(b, s.wct, s1, h.wt[--ip]);
+                lb_enc(b, s.wct, s2, h.wt[--ip]);
+                lb_enc(b, s.wct, s1, h.wt[--ip]);
+                lb_flush(b);
+            }
+            lb_add(b, s2, tlog);
+            lb_flush(b);
+            lb_add(b, s1, tlog);
+            lb_flush(b);
+            lb_add(b, 1, 1);  // end mark
+            lb_flush(b);
+            if (b.bp > 0) {
+                if (b.o < b.lim) b.out[b.o] = (uint8_t)b.bc;
+                b.o++;
+            }
+            if (b.o - 1 < 128) {
+                h.hdr[0] = (uint8_t)(b.o - 1);
+                fse = b.o;
+            }
+        }
+    }
+    const int direct = nw <= 128 ? 1 + (nw + 1) / 2 : -1;
+    if (fse > 0 && (direct < 0 || fse <= direct)) return fse;
+    if (direct < 0) return -1;
+    h.hdr[0] = (uint8_t)(127 + nw);
+    for (int i = 0; i < nw; i += 2) h.hdr[1 + i / 2] = (uint8_t)((h.wt[i] << 4) | (i + 1 < nw ? h.wt[i + 1] : 0));
+    return direct;
+}
+
+// Encode literals lit[0, L) as four Huffman streams into the scratch (lanes
+// 0-3, one stream each, last symbol first); returns the streams' total size.
+__device__ int64_t huf_streams(Smem &s, const gc_u8 *lit, int64_t L, g_u8 *scr) {
+    HufSmem &h = s.h;
+    const int l = lane_id();
+    const int64_t seg = (L + 3) / 4;
+    if (l < 4) {
+        const int64_t a = l * seg, e = (l + 1) * seg < L ? (l + 1) * seg : L;
+        g_u8 *out = scr + l * LSTREAM;
+        int64_t o = 0;
+        uint64_t bc = 0;
+        int bp = 0;
+        for (int64_t i = e - 1; i >= a; --i) {
+            const uint32_t v = lit[i];
+            bc |= (uint64_t)h.code[v] << bp;
+            bp += h.len[v];
+            if (bp >= 32) {
+                out[o] = (uint8_t)bc;
+                out[o + 1] = (uint8_t)(bc >> 8);
+                out[o + 2] = (uint8_t)(bc >> 16);
+                out[o + 3] = (uint8_t)(bc >> 24);
+                o += 4;
+                bc >>= 32;
+                bp -= 32;
+            }
+        }
+        bc |= 1ull << bp;  // end mark
+        bp += 1;
+        while (bp > 0) {
+            out[o++] = (uint8_t)bc;
+            bc >>= 8;
+            bp -= 8;
+        }
+        h.ssz[l] = (int32_t)o;
+    }
+    __syncthreads();
+    return (int64_t)h.ssz[0] + h.ssz[1] + h.ssz[2] + h.ssz[3];
+}
+
+// Sequence tables of one block (RFC 8878 3.1.1.3.2.1): FSE_Compressed when the
+// estimated bits (symbols + table header) beat the predefined distribution.
+// All lanes histogram the codes; lane 0 normalizes, writes the headers and
+// builds the tables.  Sets s.smode / s.slog / s.shdr / s.shsz.
+__device__ void choose_seq_tables(Smem &s, const uint64_t *seq, int64_t ns) {
+    const int l = lane_id();
+    for (int k = l; k < 3 * 64; k += 64) (&s.scnt[0][0])[k] = 0;
+    __syncthreads();
+    for (int64_t i = l; i < ns; i += 64) {
+        uint32_t ll, ml, off;
+        seq_fields(seq, i, ll, ml, off);
+        atomicAdd(&s.scnt[0][ll_code(s, ll)], 1u);
+        atomicAdd(&s.scnt[1][ml_code(s, ml - 3)], 1u);
+        atomicAdd(&s.scnt[2][highbit(off)], 1u);
+    }
+    __syncthreads();
+    if (l == 0) {
+        const int16_t *pre[3] = {LL_DEF, ML_DEF, OF_DEF};
+        const int prelog[3] = {6, 6, 5}, premax[3] = {35, 52, 28}, maxlog[3] = {9, 9, 8}, nsym[3] = {36, 53, 32};
+        for (int t = 0; t < 3; t++) {
+            s.smode[t] = 0;
+            s.slog[t] = prelog[t];
+            s.shsz[t] = 0;
+            const uint32_t *cnt = s.scnt[t];
+            int maxsv = 0, distinct = 0;
+            for (int v = 0; v < nsym[t]; v++)
+                if (cnt[v]) { maxsv = v; distinct++; }
+            if (ns < 64 || distinct < 2) continue;
+            // predefined cost (bits); a code it cannot express forces mode 2
+            float pc = 0.f;
+            bool pre_ok = maxsv <= premax[t];
+            for (int v = 0; v <= maxsv && pre_ok; v++) {
+                if (!cnt[v]) continue;
+                const int pn = pre[t][v] == -1 ? 1 : pre[t][v];
+                if (pn <= 0) { pre_ok = false; break; }
+                pc += (float)cnt[v] * ((float)prelog[t] - __log2f((float)pn));
+            }
+            int tlog = (int)highbit((uint32_t)(ns - 1)) - 2;
+            tlog = tlog < 5 ? 5 : tlog > maxlog[t] ? maxlog[t] : tlog;
+            while ((1 << tlog) < 2 * distinct && tlog < maxlog[t]) tlog++;
+            const int tsize = 1 << tlog;
+            int16_t *norm = s.snorm[t];
+            int sum = 0, big = 0;
+            for (int v = 0; v <= maxsv; v++) {
+                int nv = 0;
+                if (cnt[v]) {
+                    nv = (int)(((uint64_t)cnt[v] * (uint64_t)tsize) / (uint64_t)ns);
+                    nv = nv < 1 ? 1 : nv;
+                }
+                norm[v] = (int16_t)nv;
+                sum += nv;
+                if (cnt[v] > cnt[big]) big = v;
+            }
+            norm[big] = (int16_t)(norm[big] + (tsize - sum));
+            if (norm[big] < 1) continue;  // (cannot happen with 2 * distinct <= tsize)
+            float cc = 0.f;
+            for (int v = 0; v <= maxsv; v++)
+                if (cnt[v]) cc += (float)cnt[v] * ((float)tlog - __log2f((float)norm[v]));
+            const int hs = write_ncount(s.shdr[t], norm, maxsv, tlog);
+            cc += 8.f * (float)hs;
+            if (pre_ok && pc <= cc) continue;
+            build_ctab(s, s.act[t], norm, maxsv, tlog);
+            s.smode[t] = 2;
+            s.slog[t] = tlog;
+            s.shsz[t] = hs;
+        }
+    }
+    __syncthreads();
 }
 
 // wave-parallel byte copy src[a, a+len) -> dst[o, o+len)
@@ -251,7 +672,8 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(const jfs_dev_block *__
     const gc_u8 *src = (const gc_u8 *)d.src;
     g_u8 *dst = (g_u8 *)d.dst;
     const int64_t n = d.src_len, cap = d.dst_cap;
-    uint64_t *seq = scratch + (int64_t)b * SEQ_CAP;
+    uint64_t *seq = (uint64_t *)((uint8_t *)scratch + (int64_t)b * SCR_PER);
+    g_u8 *lscr = (g_u8 *)((uint8_t *)scratch + (int64_t)b * SCR_PER + SEQ_CAP * 8);
     const int64_t bound = n + (n >> 8) + (n < BLK ? (BLK - n) >> 11 : 0);
     if (n < 0 || cap < bound) {  // compress.go:86-89: cap(dst) < CompressBound -> "buffer too short"
         if (l == 0) ret[b] = -2;
@@ -268,6 +690,11 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(const jfs_dev_block *__
         int c = 0;
         while (c + 1 < 53 && ML_BASE[c + 1] - 3 <= (uint32_t)v) c++;
         s.lut_ml[v] = (uint8_t)c;
+    }
+    for (int t = l; t < 3; t += 64) {
+        s.smode[t] = 0;
+        s.slog[t] = t == 2 ? 5 : 6;
+        s.shsz[t] = 0;
     }
     build_ctab(s, s.ct[0], LL_DEF, 35, 6);
     __builtin_amdgcn_wave_barrier();
@@ -302,7 +729,8 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(const jfs_dev_block *__
         op = hn;
     }
 
-    // ---- blocks
+    // ---- blocks (the repeat offsets carry across the frame's blocks, RFC 8878 3.1.1.5)
+    uint32_t rep0 = 1;  // Repeated_Offset1 (only it is reused: Offset_Value 1 with LL > 0)
     int64_t bs = 0;
     do {
         const int64_t be = bs + BLK < n ? bs + BLK : n;
@@ -315,16 +743,27 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(const jfs_dev_block *__
         {
             int64_t ip = bs, anchor = bs;
             uint32_t miss = 0;
-            while (ok && ip + 4 <= be) {
-                const uint32_t v = ld32u(src + ip);
-                const uint32_t h = hash4(v);
-                const int64_t cand = (int64_t)s.table[h];
-                s.table[h] = (uint32_t)ip;
-                bool hit = cand < ip && ip - cand <= 65535;
-                if (hit) hit = ld32u(src + cand) == v;
-                if (!hit) {
-                    ip += 1 + (miss++ >> 6);
-                    continue;
+            while (ok && ip + 8 <= be) {
+                // zstd_fast: a repeat-offset match one byte ahead first, else the
+                // 6-byte hash candidate (level 1: minMatch 6) within the window
+                int64_t cand;
+                uint32_t ofv = 0;  // Offset_Value: 1 = repeat offset 1, else offset + 3
+                const int64_t rp = ip + 1;
+                if (JFS_ZE_REP && rep0 <= rp && ld32u(src + rp) == ld32u(src + rp - rep0)) {
+                    cand = rp - rep0;
+                    ip = rp;
+                    ofv = 1;
+                } else {
+                    const uint64_t v = ld64u(src + ip);
+                    const uint32_t h = JFS_ZE_HASH == 6 ? hash6(v) : hash4((uint32_t)v);
+                    cand = (int64_t)s.table[h];
+                    s.table[h] = (uint32_t)ip;
+                    bool hit = cand < ip && ip - cand <= WMAX;
+                    if (hit) hit = ld32u(src + cand) == (uint32_t)v;
+                    if (!hit) {
+                        ip += 1 + (miss++ >> 6);
+                        continue;
+                    }
                 }
                 miss = 0;
                 // forward extension from +4, 64 bytes per step, up to the block end
@@ -337,9 +776,9 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(const jfs_dev_block *__
                     ml += run;
                     if (run < 64) break;
                 }
-                // backward catch-up into the pending literals
+                // backward catch-up into the pending literals (new offsets only)
                 int64_t m0 = cand;
-                {
+                if (ofv == 0) {
                     int64_t lim = ip - anchor;
                     if (m0 < lim) lim = m0;
                     int64_t back = 0;
@@ -360,11 +799,19 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(const jfs_dev_block *__
                 copy_bytes(dst, lit0 + L, src, anchor, ll);
                 L += ll;
                 if (ns >= SEQ_CAP) { ok = false; break; }
-                if (l == 0) seq[ns] = (uint64_t)ll | ((uint64_t)ml << 17) | ((uint64_t)(ip - m0) << 35);
+                if (ofv == 0) {  // a new offset enters the repeat history
+                    const uint32_t off = (uint32_t)(ip - m0);
+                    ofv = off + 3;
+                    rep0 = off;
+                }
+                if (l == 0) seq[ns] = (uint64_t)ll | ((uint64_t)ml << 17) | ((uint64_t)ofv << 35);
                 ns++;
                 ip += ml;
                 anchor = ip;
-                if (ip - 2 >= bs && ip + 2 <= n) s.table[hash4(ld32u(src + ip - 2))] = (uint32_t)(ip - 2);
+                if (ip - 2 >= bs && ip + 6 <= n) {
+                    const uint64_t v2 = ld64u(src + ip - 2);
+                    s.table[JFS_ZE_HASH == 6 ? hash6(v2) : hash4((uint32_t)v2)] = (uint32_t)(ip - 2);
+                }
             }
             if (ok) {  // last literals of the block
                 copy_bytes(dst, lit0 + L, src, anchor, be - anchor);
@@ -375,13 +822,69 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(const jfs_dev_block *__
         // 2./3. headers and the sequences bitstream
         int64_t end = lit0 + L;
         if (ok) {
+            // literal section kind: 2 Huffman, 1 RLE, 0 raw -- the smallest
+            const int hsz = L < 32 ? 1 : L < 4096 ? 2 : 3;  // raw / RLE header bytes
+            int kind = 0;
+            int64_t hcs = 0;  // Huffman: Compressed_Size (tree + jump table + streams)
+            int hlh = 0;      // Huffman: literal header bytes
+            if (L >= HUF_MINL) {
+                wait_vm();  // the literals this wave stored are read back
+                for (int k = l; k < 256; k += 64) s.h.cnt[k] = 0;
+                __syncthreads();
+                for (int64_t k = l; k < L; k += 64) atomicAdd(&s.h.cnt[dst[lit0 + k]], 1u);
+                __syncthreads();
+                if (l == 0) {
+                    s.h.maxbits = huf_build(s.h);
+                    s.h.hsize = s.h.maxbits > 0 ? huf_describe(s) : -1;
+                }
+                __syncthreads();
+                if (s.h.nsym == 1) {
+                    kind = 1;
+                } else if (s.h.maxbits > 0 && s.h.hsize > 0) {
+                    const int64_t ss = huf_streams(s, (const gc_u8 *)dst + lit0, L, lscr);
+                    hcs = s.h.hsize + 6 + ss;
+                    const int64_t big = L > hcs ? L : hcs;
+                    hlh = big < 1024 ? 3 : big < 16384 ? 4 : 5;
+                    if (big < (1 << 18) && hlh + hcs < hsz + L) kind = 2;
+                }
+                wait_vm();
+                __syncthreads();
+            }
+            if (kind == 2) {
+                const uint64_t sf = hlh == 3 ? 1 : hlh == 4 ? 2 : 3;
+                const int sb = hlh == 3 ? 10 : hlh == 4 ? 14 : 18;
+                const uint64_t lh = 2u | (sf << 2) | ((uint64_t)L << 4) | ((uint64_t)hcs << (4 + sb));
+                int64_t o = op + 3;
+                if (l < hlh) dst[o + l] = (uint8_t)(lh >> (8 * l));
+                o += hlh;
+                for (int k = l; k < s.h.hsize; k += 64) dst[o + k] = s.h.hdr[k];
+                o += s.h.hsize;
+                if (l < 3) {  // jump table: sizes of streams 1-3
+                    dst[o + 2 * l] = (uint8_t)s.h.ssz[l];
+                    dst[o + 2 * l + 1] = (uint8_t)(s.h.ssz[l] >> 8);
+                }
+                o += 6;
+                for (int k = 0; k < 4; k++) {
+                    copy_bytes(dst, o, (const gc_u8 *)lscr + k * LSTREAM, 0, s.h.ssz[k]);
+                    o += s.h.ssz[k];
+                }
+                end = o;
+            } else if (kind == 1) {
+                const uint32_t lh = hsz == 1   ? ((uint32_t)L << 3) | 1u
+                                    : hsz == 2 ? (1u << 2) | ((uint32_t)L << 4) | 1u
+                                               : (3u << 2) | ((uint32_t)L << 4) | 1u;
+                const uint8_t v = dst[lit0];
+                __builtin_amdgcn_wave_barrier();
+                if (l < hsz) dst[op + 3 + l] = (uint8_t)(lh >> (8 * l));
+                if (l == 0) dst[op + 3 + hsz] = v;
+                end = op + 3 + hsz + 1;
+            }
             // Raw_Literals_Block with the smallest Size_Format (1, 2 or 3 header
             // bytes, like libzstd); the literals move down to follow it
-            const int hsz = L < 32 ? 1 : L < 4096 ? 2 : 3;
             const uint32_t lh = hsz == 1   ? (uint32_t)L << 3
                                 : hsz == 2 ? (1u << 2) | ((uint32_t)L << 4)
                                            : (3u << 2) | ((uint32_t)L << 4);
-            if (hsz < 3) {
+            if (kind == 0 && hsz < 3) {
                 const int64_t to = op + 3 + hsz;
                 for (int64_t k = 0; k < L; k += 64) {  // dst < src: ascending chunks are safe
                     uint8_t v = 0;
@@ -391,7 +894,8 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(const jfs_dev_block *__
                 }
                 end = to + L;
             }
-            if (l < hsz) dst[op + 3 + l] = (uint8_t)(lh >> (8 * l));
+            if (kind == 0 && l < hsz) dst[op + 3 + l] = (uint8_t)(lh >> (8 * l));
+            __threadfence_block();
             if (ns < 128) {
                 if (l == 0) dst[end] = (uint8_t)ns;
                 end += 1;
@@ -407,8 +911,15 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(const jfs_dev_block *__
                 end += 3;
             }
             if (ns > 0) {
-                if (l == 0) dst[end] = 0;  // Symbol_Compression_Modes: predefined x3
+                choose_seq_tables(s, seq, ns);
+                // Symbol_Compression_Modes: LL bits 7-6, OF 5-4, ML 3-2; then the
+                // table descriptions in the order LL, OF, ML
+                if (l == 0) dst[end] = (uint8_t)((s.smode[0] << 6) | (s.smode[2] << 4) | (s.smode[1] << 2));
                 end += 1;
+                for (int t : {0, 2, 1}) {
+                    for (int k = l; k < s.shsz[t]; k += 64) dst[end + k] = s.shdr[t][k];
+                    end += s.shsz[t];
+                }
                 __threadfence_block();
                 BitW w;
                 w.dst = dst;
@@ -461,7 +972,7 @@ extern "C" int jfs_launch_zstd_encode(const jfs_dev_block *d_blocks, int nblk, i
         if (z.d) (void)hipFree(z.d);  // hipFree synchronises with work still using it
         z.d = nullptr;
         z.cap = 0;
-        if (hipMalloc((void **)&z.d, (size_t)SCR_PER * (size_t)nblk) != hipSuccess) return -1;
+        if (hipMalloc((void **)&z.d, (size_t)SCR_PER * (size_t)nblk) != hipSuccess) return -1;  // bytes
         z.cap = (size_t)nblk;
     }
     hipLaunchKernelGGL(zstd_encode_kernel, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, d_ret, z.d);

@@ -138,3 +138,14 @@ def test_zstandard_compress_contract(gpu):
     back = z.DecompressBatch([(o, bytes(d[:n])) for o, (d, _), (n, e) in zip(outs, pairs, res)])
     for s, o, (n, e) in zip(srcs, outs, back):
         assert e is None and n == len(s) and bytes(o) == s
+
+
+def test_zstd_encode_ratio_floor(gpu):
+    """Huffman literals + FSE sequences: the GPU frames of 4 MiB text blocks
+    reach a level-1-class ratio (floor guards regressions; libzstd level 1
+    reaches ~3.2 on this generator)."""
+    srcs = [gen_block("T", 900 + i, 4 << 20) for i in range(2)]
+    r, frames = encode_device(srcs, gpu)
+    ratio = sum(len(s) for s in srcs) / sum(r)
+    print("zstd GPU ratio", ratio)
+    assert ratio >= 2.7, ratio
