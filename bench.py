@@ -416,6 +416,45 @@ def configs2_roundtrip(a, S, world, rank, dev):
                     "size and decoded bytes verified"}
 
 
+def checksum_and_aead(batch, S, world, dev):
+    """SURVEY.md 8(f)4 and 8(f)3 on the headline's own buffers: CRC-32C of the
+    4096 decoded 4 MiB blocks (object checksum + the disk cache's per-32 KiB
+    sums, pkg/object/checksum.go:30-45, pkg/chunk/disk_cache_file.go:139-152)
+    and AES-256-GCM seal of the 4096 compressed blocks (what an encrypted
+    volume PUTs after compression, pkg/object/encrypt.go:226-257)."""
+    import torch
+    from juicefs_amd import device as D
+    n, U = batch.nblk, batch.U
+    offs = np.arange(n, dtype=np.int64)
+    words = (U - 1) // (32 << 10) + 1
+    sums = torch.empty(n * 4 * words, dtype=torch.uint8, device=dev)
+    desc = D.make_desc(batch.out, offs * U, [U] * n, sums, offs * 4 * words, [4 * words] * n)
+    crc = torch.empty(n, dtype=torch.int32, device=dev)
+    ret = torch.empty(n, dtype=torch.int32, device=dev)
+    el, kms = timed_launches(lambda st: D.crc32c(desc, crc, ret, seg_bytes=32 << 10, stream=st), 3, 1, S, world, dev)
+    out = {"crc32c": {"value": S.whole_job_gib_s(world, n, U, 3, el), "unit": "GiB/s", "kernel_ms": kms,
+                      "roofline": {"bound": "hbm", "achieved": n * U / (kms / 1e3) / 1e9, "peak": HBM_PEAK_GBS,
+                                   "unit": "GB/s", "frac": n * U / (kms / 1e3) / 1e9 / HBM_PEAK_GBS},
+                      "workload": f"{n} x 4 MiB decoded blocks: whole-block CRC-32C + big-endian sums per 32 KiB"}}
+    rng = np.random.default_rng(5)
+    kn = torch.from_numpy(rng.integers(0, 256, 64 * n, dtype=np.uint8)).to(dev)
+    slot = batch.slot + 16
+    sealed = torch.empty(n * slot, dtype=torch.uint8, device=dev)
+    adesc = D.make_aead_desc(batch.comp, offs * batch.slot, batch.csize, sealed, offs * slot, batch.csize + 16, kn,
+                             offs * 64, offs * 64 + 32)
+    aret = torch.empty(n, dtype=torch.int32, device=dev)
+    el, kms = timed_launches(lambda st: D.aes256gcm(adesc, aret, True, stream=st), 3, 1, S, world, dev)
+    if not bool((aret.cpu().numpy().astype(np.int64) == batch.csize + 16).all()):
+        raise RuntimeError("AES-GCM seal failed")
+    C = int(batch.csize.sum())
+    out["aes256gcm_seal"] = {"value": world * C * 3 / el / 2**30, "unit": "GiB/s", "kernel_ms": kms,
+                             "roofline": {"bound": "hbm", "achieved": 2 * C / (kms / 1e3) / 1e9, "peak": HBM_PEAK_GBS,
+                                          "unit": "GB/s", "frac": 2 * C / (kms / 1e3) / 1e9 / HBM_PEAK_GBS},
+                             "workload": f"{n} compressed blocks ({C / n / 2**20:.2f} MiB each), one key/nonce per "
+                                         "block; GiB/s of plaintext"}
+    return out
+
+
 def measured_traffic(path, nblk, U):
     """HBM bytes per launch from profiles/traffic.json, only if it was
     measured on these kernel sources at this workload."""
@@ -517,6 +556,10 @@ def main():
             out["configs_2"] = configs2_roundtrip(a, S, world, rank, dev)
         except Exception as e:
             out["configs_2"] = {"error": repr(e)}
+        try:
+            out["checksum_aead"] = checksum_and_aead(batch, S, world, dev)
+        except Exception as e:
+            out["checksum_aead"] = {"error": repr(e)}
     if rank == 0 and world == 1:
         # bounded sample for the CPU legs: 32 distinct blocks of the headline batch
         ns = min(32, nblk)

@@ -151,6 +151,23 @@ typedef struct jfs_aead_block {
 int64_t jfs_aes256gcm_seal_device(const jfs_aead_block *d_blocks, int nblk, int32_t *d_ret, void *stream);
 int64_t jfs_aes256gcm_open_device(const jfs_aead_block *d_blocks, int nblk, int32_t *d_ret, void *stream);
 
+/* Fused object paths (compression runs before encryption on PUT and after
+ * decryption on GET, cmd/format.go:289-302, docs internals.md:920), chained on
+ * `stream` with no host round trip: the second kernel reads each block's
+ * length from the first kernel's results on the device.
+ *   compress -> seal: d_comp[i] LZ4-compresses into an intermediate buffer
+ *     (d_ret_comp[i] = LZ4 result); d_aead[i].src must be that buffer (its
+ *     src_len is ignored) and is sealed into d_aead[i].dst; d_ret[i] = sealed
+ *     bytes, or JFS_CHAIN_FAILED (INT32_MIN) when the compression failed.
+ *   open -> decompress: d_aead[i] opens into an intermediate buffer
+ *     (d_ret_open[i] = plaintext length or -1); d_dec[i].src must be that
+ *     buffer (its src_len is ignored); d_ret[i] = the LZ4_decompress_safe
+ *     result, or INT32_MIN when the tag did not verify. */
+int64_t jfs_lz4_compress_seal_device(const jfs_dev_block *d_comp, const jfs_aead_block *d_aead, int nblk,
+                                     int32_t *d_ret_comp, int32_t *d_ret, void *stream);
+int64_t jfs_open_lz4_decompress_device(const jfs_aead_block *d_aead, const jfs_dev_block *d_dec, int nblk,
+                                       int32_t *d_ret_open, int32_t *d_ret, void *stream);
+
 /* ---- Runtime / utilities ------------------------------------------------- */
 
 /* Number of usable gfx950 devices (0 when none; never an error). */

@@ -31,7 +31,7 @@ EXPORTS = [
     "jfs_compress_batch", "jfs_decompress_batch", "jfs_lz4_decompress_device", "jfs_lz4_compress_device",
     "jfs_zstd_decompress_device", "jfs_zstd_compress_device", "jfs_device_count", "jfs_version", "jfs_gen_blocks_device",
     "jfs_gen_block_host", "jfs_release_staging", "jfs_crc32c_device", "jfs_aes256gcm_seal_device",
-    "jfs_aes256gcm_open_device",
+    "jfs_aes256gcm_open_device", "jfs_lz4_compress_seal_device", "jfs_open_lz4_decompress_device",
 ]
 
 
@@ -77,6 +77,9 @@ def load() -> ctypes.CDLL:
     lib.jfs_crc32c_device.restype = i64
     for f in (lib.jfs_aes256gcm_seal_device, lib.jfs_aes256gcm_open_device):
         f.argtypes = [vp, ctypes.c_int, vp, vp]
+        f.restype = i64
+    for f in (lib.jfs_lz4_compress_seal_device, lib.jfs_open_lz4_decompress_device):
+        f.argtypes = [vp, vp, ctypes.c_int, vp, vp, vp]
         f.restype = i64
     lib.jfs_release_staging.argtypes = []
     lib.jfs_release_staging.restype = None

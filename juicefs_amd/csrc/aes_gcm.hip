@@ -196,8 +196,10 @@ __device__ __forceinline__ void store_part(g_u8 *p, const uint4 &v, int len, boo
 
 // mode 0 = seal (src = plaintext, n = src_len; dst = ciphertext || tag),
 // mode 1 = open (src = ciphertext || tag, n = src_len - 16; dst = plaintext)
+// lens (optional): per-block input lengths produced on the device by the
+// previous kernel of a fused chain (LZ4 compress: <= 0 = it failed).
 __global__ __launch_bounds__(LANES) void gcm_kernel(const jfs_aead_block *__restrict__ blocks, int nblk, int mode,
-                                                     int32_t *__restrict__ ret) {
+                                                     int32_t *__restrict__ ret, const int32_t *__restrict__ lens) {
     __shared__ Smem s;
     const int b = blockIdx.x;
     const int t = threadIdx.x, l = t & 63, wv = t >> 6;
@@ -207,7 +209,15 @@ __global__ __launch_bounds__(LANES) void gcm_kernel(const jfs_aead_block *__rest
         for (int i = t; i < (int)(sizeof(Tables) / 4); i += LANES) d[i] = g[i];
     }
     if (b >= nblk) return;
-    const jfs_aead_block blk = ((JFS_GLOBAL const jfs_aead_block *)blocks)[b];
+    jfs_aead_block blk = ((JFS_GLOBAL const jfs_aead_block *)blocks)[b];
+    if (lens) {
+        const int32_t ln = lens[b];
+        if (ln <= 0) {  // the chained step failed
+            if (t == 0) ret[b] = JFS_CHAIN_FAILED;
+            return;
+        }
+        blk.src_len = ln;
+    }
     const gc_u8 *src = (const gc_u8 *)blk.src;
     g_u8 *dst = (g_u8 *)blk.dst;
     const int64_t n = mode == 0 ? (int64_t)blk.src_len : (int64_t)blk.src_len - 16;
@@ -335,8 +345,9 @@ __global__ __launch_bounds__(LANES) void gcm_kernel(const jfs_aead_block *__rest
 }  // namespace jfs
 
 extern "C" int jfs_launch_aes256gcm(const jfs_aead_block *d_blocks, int nblk, int mode, int32_t *d_ret,
-                                    hipStream_t stream) {
+                                    const int32_t *d_lens, hipStream_t stream) {
     if (nblk <= 0) return 0;
-    hipLaunchKernelGGL(jfs::gcm::gcm_kernel, dim3(nblk), dim3(jfs::gcm::LANES), 0, stream, d_blocks, nblk, mode, d_ret);
+    hipLaunchKernelGGL(jfs::gcm::gcm_kernel, dim3(nblk), dim3(jfs::gcm::LANES), 0, stream, d_blocks, nblk, mode, d_ret,
+                       d_lens);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

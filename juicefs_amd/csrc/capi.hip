@@ -753,13 +753,31 @@ int64_t jfs_crc32c_device(const jfs_dev_block *d_blocks, int nblk, int32_t seg_b
 int64_t jfs_aes256gcm_seal_device(const jfs_aead_block *d_blocks, int nblk, int32_t *d_ret, void *stream) {
     if (devices().empty()) return JFS_ERR_NO_DEVICE;
     if (nblk < 0) return JFS_ERR_INVALID;
-    return jfs_launch_aes256gcm(d_blocks, nblk, 0, d_ret, (hipStream_t)stream) == 0 ? JFS_OK : JFS_ERR_HIP;
+    return jfs_launch_aes256gcm(d_blocks, nblk, 0, d_ret, nullptr, (hipStream_t)stream) == 0 ? JFS_OK : JFS_ERR_HIP;
 }
 
 int64_t jfs_aes256gcm_open_device(const jfs_aead_block *d_blocks, int nblk, int32_t *d_ret, void *stream) {
     if (devices().empty()) return JFS_ERR_NO_DEVICE;
     if (nblk < 0) return JFS_ERR_INVALID;
-    return jfs_launch_aes256gcm(d_blocks, nblk, 1, d_ret, (hipStream_t)stream) == 0 ? JFS_OK : JFS_ERR_HIP;
+    return jfs_launch_aes256gcm(d_blocks, nblk, 1, d_ret, nullptr, (hipStream_t)stream) == 0 ? JFS_OK : JFS_ERR_HIP;
+}
+
+int64_t jfs_lz4_compress_seal_device(const jfs_dev_block *d_comp, const jfs_aead_block *d_aead, int nblk,
+                                     int32_t *d_ret_comp, int32_t *d_ret, void *stream) {
+    if (devices().empty()) return JFS_ERR_NO_DEVICE;
+    if (nblk < 0) return JFS_ERR_INVALID;
+    hipStream_t st = (hipStream_t)stream;
+    if (jfs_launch_lz4_encode(d_comp, nblk, d_ret_comp, st) != 0) return JFS_ERR_HIP;
+    return jfs_launch_aes256gcm(d_aead, nblk, 0, d_ret, d_ret_comp, st) == 0 ? JFS_OK : JFS_ERR_HIP;
+}
+
+int64_t jfs_open_lz4_decompress_device(const jfs_aead_block *d_aead, const jfs_dev_block *d_dec, int nblk,
+                                       int32_t *d_ret_open, int32_t *d_ret, void *stream) {
+    if (devices().empty()) return JFS_ERR_NO_DEVICE;
+    if (nblk < 0) return JFS_ERR_INVALID;
+    hipStream_t st = (hipStream_t)stream;
+    if (jfs_launch_aes256gcm(d_aead, nblk, 1, d_ret_open, nullptr, st) != 0) return JFS_ERR_HIP;
+    return jfs_launch_lz4_decode_lens(d_dec, nblk, d_ret, d_ret_open, st) == 0 ? JFS_OK : JFS_ERR_HIP;
 }
 
 int jfs_device_count(void) { return (int)devices().size(); }

@@ -35,7 +35,12 @@ void jfs_zstd_plan_host(const uint8_t *const *srcs, const int32_t *lens, const i
                         uint64_t *totals);
 int jfs_launch_crc32c(const jfs_dev_block *d_blocks, int nblk, int32_t seg_bytes, uint32_t *d_crc, int32_t *d_ret,
                       hipStream_t stream);
-int jfs_launch_aes256gcm(const jfs_aead_block *d_blocks, int nblk, int mode, int32_t *d_ret, hipStream_t stream);
+int jfs_launch_aes256gcm(const jfs_aead_block *d_blocks, int nblk, int mode, int32_t *d_ret, const int32_t *d_lens,
+                         hipStream_t stream);
+int jfs_launch_lz4_decode_lens(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, const int32_t *d_lens,
+                               hipStream_t stream);
+// ret value of a fused chain's second step when its first step failed
+#define JFS_CHAIN_FAILED (-2147483647 - 1)
 int jfs_launch_gen(uint8_t *d_dst, int nblk, int64_t block_bytes, char cls, uint64_t seed_base,
                    const uint8_t *d_vocab, hipStream_t stream);
 }

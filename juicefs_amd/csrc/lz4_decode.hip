@@ -1307,8 +1307,11 @@ __device__ __forceinline__ void copier_wave(Smem &s, Ctx &c, int32_t *retp PROF_
 #define JFS_LZ4_NSGPR 80
 #endif
 #define JFS_LZ4_ATTR __attribute__((amdgpu_num_sgpr(JFS_LZ4_NSGPR), amdgpu_waves_per_eu(8)))
+// lens (optional): per-block input lengths produced on the device by the
+// previous kernel of a fused chain (AES-GCM open); < 0 = that step failed.
 __global__ __launch_bounds__(128) JFS_LZ4_ATTR void lz4_decode_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
-                                                        int32_t *__restrict__ ret) {
+                                                        int32_t *__restrict__ ret,
+                                                        const int32_t *__restrict__ lens) {
     __shared__ Smem s;
     const int b = blockIdx.x;
     if (b >= nblk) return;
@@ -1317,7 +1320,11 @@ __global__ __launch_bounds__(128) JFS_LZ4_ATTR void lz4_decode_kernel(const jfs_
     Ctx c;
     c.src = (const gc_u8 *)d.src;
     c.dst = (g_u8 *)d.dst;
-    c.n = d.src_len;
+    c.n = lens ? lens[b] : d.src_len;
+    if (lens && c.n < 0) {  // the chained step failed: report it, decode nothing
+        if (threadIdx.x == 64) ret[b] = JFS_CHAIN_FAILED;
+        return;
+    }
     c.cap = d.dst_cap;
     c.F = 0;
     c.Fw = 0;
@@ -1360,7 +1367,12 @@ extern "C" int jfs_prof_reset() {
 #endif
 
 extern "C" int jfs_launch_lz4_decode(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, hipStream_t stream) {
+    return jfs_launch_lz4_decode_lens(d_blocks, nblk, d_ret, nullptr, stream);
+}
+
+extern "C" int jfs_launch_lz4_decode_lens(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, const int32_t *d_lens,
+                                          hipStream_t stream) {
     if (nblk <= 0) return 0;
-    hipLaunchKernelGGL(jfs::lz4d::lz4_decode_kernel, dim3(nblk), dim3(128), 0, stream, d_blocks, nblk, d_ret);
+    hipLaunchKernelGGL(jfs::lz4d::lz4_decode_kernel, dim3(nblk), dim3(128), 0, stream, d_blocks, nblk, d_ret, d_lens);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -115,6 +115,25 @@ def aes256gcm(desc: torch.Tensor, ret: torch.Tensor, seal: bool, stream=None):
     _check(fn(desc.data_ptr(), n, ret.data_ptr(), _stream_ptr(stream)), "jfs_aes256gcm")
 
 
+JFS_CHAIN_FAILED = -(1 << 31)  # the first step of a fused chain failed for this block
+
+
+def lz4_compress_seal(comp_desc: torch.Tensor, aead_desc: torch.Tensor, ret_comp: torch.Tensor, ret: torch.Tensor,
+                      stream=None):
+    """Fused LZ4 compress -> AES-256-GCM seal (jfs_lz4_compress_seal_device)."""
+    n = comp_desc.numel() // DESC_DTYPE.itemsize
+    _check(L.load().jfs_lz4_compress_seal_device(comp_desc.data_ptr(), aead_desc.data_ptr(), n, ret_comp.data_ptr(),
+                                                 ret.data_ptr(), _stream_ptr(stream)), "jfs_lz4_compress_seal_device")
+
+
+def open_lz4_decompress(aead_desc: torch.Tensor, dec_desc: torch.Tensor, ret_open: torch.Tensor, ret: torch.Tensor,
+                        stream=None):
+    """Fused AES-256-GCM open -> LZ4 decompress (jfs_open_lz4_decompress_device)."""
+    n = dec_desc.numel() // DESC_DTYPE.itemsize
+    _check(L.load().jfs_open_lz4_decompress_device(aead_desc.data_ptr(), dec_desc.data_ptr(), n, ret_open.data_ptr(),
+                                                   ret.data_ptr(), _stream_ptr(stream)), "jfs_open_lz4_decompress_device")
+
+
 def gen_blocks(out: torch.Tensor, nblk: int, block_bytes: int, cls: str, seed_base: int, stream=None):
     """Fill out[0 : nblk*block_bytes] with synthetic blocks."""
     assert out.numel() >= nblk * block_bytes

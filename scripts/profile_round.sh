@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 O=gpurun_out/prof
 mkdir -p $O
 if [ "$what" = lz4 ] || [ "$what" = all ]; then
-  timeout -k 10 300 python bench.py > $O/bench_lz4.json 2> $O/bench_lz4.err
+  timeout -k 10 400 python bench.py > $O/bench_lz4.json 2> $O/bench_lz4.err
   tail -1 $O/bench_lz4.json
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt_lz4 -o kt --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-extras --no-host-path > $O/kt_lz4.log 2>&1
   find $O/kt_lz4 -name '*kernel_stats.csv' -exec cp {} $O/lz4_kernel_stats.csv \;

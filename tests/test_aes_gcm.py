@@ -192,3 +192,61 @@ def test_gcm_gpu_4mib_blocks(gpu, oracle):
         want = oracle.aes256gcm_seal(kh[64 * i:64 * i + 32].tobytes(), kh[64 * i + 32:64 * i + 44].tobytes(),
                                      host[i * U:(i + 1) * U].tobytes())
         assert oh[i * (U + 16):(i + 1) * (U + 16)].tobytes() == want, i
+
+
+@pytest.mark.gpu
+def test_fused_compress_seal_and_open_decompress(gpu, oracle):
+    """SURVEY.md 8(f)3 fused paths: LZ4 compress -> seal and open -> LZ4
+    decompress chained on one stream (lengths passed on the device).  The
+    sealed objects equal oracle.seal(oracle.lz4_compress(block)); opening them
+    gives the blocks back; a tampered object fails its block only."""
+    import torch
+    from juicefs_amd import device as D
+    rng = np.random.default_rng(8)
+    srcs = [gen_block("T", 70 + i, n) for i, n in enumerate((1 << 20, 300000, 4096, (1 << 20) + 7, 65536))]
+    srcs.append(gen_block("R", 3, 200000))
+    n = len(srcs)
+    bound = [len(s) + len(s) // 255 + 16 for s in srcs]
+    so = np.cumsum([0] + [(len(s) + 255) // 256 * 256 for s in srcs[:-1]])
+    co = np.cumsum([0] + [(b + 255) // 256 * 256 for b in bound[:-1]])
+    eo = np.cumsum([0] + [(b + 16 + 255) // 256 * 256 for b in bound[:-1]])
+    raw = torch.zeros(int(so[-1]) + len(srcs[-1]) + 256, dtype=torch.uint8, device=gpu)
+    for s, o in zip(srcs, so):
+        raw[int(o):int(o) + len(s)] = torch.from_numpy(np.frombuffer(s, dtype=np.uint8).copy()).to(gpu)
+    comp = torch.zeros(int(co[-1]) + bound[-1] + 256, dtype=torch.uint8, device=gpu)
+    sealed = torch.zeros(int(eo[-1]) + bound[-1] + 16 + 256, dtype=torch.uint8, device=gpu)
+    kn_h = rng.integers(0, 256, 64 * n, dtype=np.uint8)
+    kn = torch.from_numpy(kn_h).to(gpu)
+    cdesc = D.make_desc(raw, so, [len(s) for s in srcs], comp, co, bound)
+    adesc = D.make_aead_desc(comp, co, [0] * n, sealed, eo, [b + 16 for b in bound], kn,
+                             [64 * i for i in range(n)], [64 * i + 32 for i in range(n)])
+    rc, rs = torch.zeros(n, dtype=torch.int32, device=gpu), torch.zeros(n, dtype=torch.int32, device=gpu)
+    D.lz4_compress_seal(cdesc, adesc, rc, rs)
+    torch.cuda.synchronize()
+    csz, ssz = rc.cpu().tolist(), rs.cpu().tolist()
+    sh = sealed.cpu().numpy()
+    objs = []
+    for i, s in enumerate(srcs):
+        m, ref = oracle.lz4_compress(s)
+        assert csz[i] == m and ssz[i] == m + 16
+        key, nonce = kn_h[64 * i:64 * i + 32].tobytes(), kn_h[64 * i + 32:64 * i + 44].tobytes()
+        obj = sh[int(eo[i]):int(eo[i]) + ssz[i]].tobytes()
+        assert obj == oracle.aes256gcm_seal(key, nonce, ref), i
+        objs.append(obj)
+    # tamper with object 2, then open -> decompress everything
+    sealed[int(eo[2]) + 5] ^= 1
+    plain = torch.zeros_like(comp)
+    out = torch.zeros_like(raw)
+    odesc = D.make_aead_desc(sealed, eo, ssz, plain, co, bound, kn, [64 * i for i in range(n)],
+                             [64 * i + 32 for i in range(n)])
+    ddesc = D.make_desc(plain, co, [0] * n, out, so, [len(s) for s in srcs])
+    ro, rd = torch.zeros(n, dtype=torch.int32, device=gpu), torch.zeros(n, dtype=torch.int32, device=gpu)
+    D.open_lz4_decompress(odesc, ddesc, ro, rd)
+    torch.cuda.synchronize()
+    ro_h, rd_h, oh = ro.cpu().tolist(), rd.cpu().tolist(), out.cpu().numpy()
+    for i, s in enumerate(srcs):
+        if i == 2:
+            assert ro_h[i] == -1 and rd_h[i] == D.JFS_CHAIN_FAILED
+            continue
+        assert ro_h[i] == csz[i] and rd_h[i] == len(s)
+        assert oh[int(so[i]):int(so[i]) + len(s)].tobytes() == s, i
