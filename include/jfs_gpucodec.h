@@ -170,8 +170,43 @@ int64_t jfs_open_lz4_decompress_device(const jfs_aead_block *d_aead, const jfs_d
 
 /* ---- Runtime / utilities ------------------------------------------------- */
 
-/* Number of usable gfx950 devices (0 when none; never an error). */
+/* Number of usable gfx950 devices (0 when none; never an error).  Only the
+ * devices JFS_GPU_DEVICES selects count (a comma list of ordinals such as
+ * "0,2,5", a mask such as "0x25", or "all" = the default). */
 int jfs_device_count(void);
+
+/* Codec selector, read once from JFS_GPU_CODEC:
+ *   "off"   -> JFS_MODE_OFF: the library reports no device; every GPU entry
+ *              point returns JFS_ERR_NO_DEVICE and the Go adapter keeps the
+ *              CPU codecs of compress.go (NewCompressor unchanged);
+ *   "auto"  -> JFS_MODE_AUTO (default, also for unknown values): the adapter
+ *              uses this library when jfs_device_count() > 0, else the CPU
+ *              codecs;
+ *   "force" -> JFS_MODE_FORCE: the adapter must use this library and fail at
+ *              start-up when jfs_device_count() == 0.
+ * The library itself never runs a CPU codec in any mode. */
+#define JFS_MODE_OFF 0
+#define JFS_MODE_AUTO 1
+#define JFS_MODE_FORCE 2
+int jfs_gpu_mode(void);
+
+/* Per-codec counters (the data behind cachedStore's object_request_data_bytes
+ * and block-size metrics, cached_store.go:931-974).  Index algo * 2 + dir,
+ * dir 0 = compress, 1 = decompress; 6 entries.  Host-path calls (one-call and
+ * batch) count blocks, bytes and errors per block; device-resident launches
+ * count only calls and blocks (their results stay in HBM). */
+typedef struct jfs_op_stats {
+    uint64_t calls;     /* API calls */
+    uint64_t blocks;    /* blocks submitted */
+    uint64_t bytes_in;  /* input bytes of host-path blocks that succeeded */
+    uint64_t bytes_out; /* output bytes of host-path blocks that succeeded */
+    uint64_t errors;    /* host-path blocks that returned an error code */
+    uint64_t nanos;     /* wall time spent inside host-path calls */
+} jfs_op_stats;
+#define JFS_STATS_N 6
+/* Copy min(n, JFS_STATS_N) entries to out; returns JFS_STATS_N. */
+int jfs_stats(jfs_op_stats *out, int n);
+void jfs_stats_reset(void);
 /* Free the batch path's pinned host + HBM staging now (it is also released
  * after JFS_STAGING_IDLE_MS, default 15000, of no batch activity). */
 void jfs_release_staging(void);

@@ -32,12 +32,20 @@ EXPORTS = [
     "jfs_zstd_decompress_device", "jfs_zstd_compress_device", "jfs_device_count", "jfs_version", "jfs_gen_blocks_device",
     "jfs_gen_block_host", "jfs_release_staging", "jfs_crc32c_device", "jfs_aes256gcm_seal_device",
     "jfs_aes256gcm_open_device", "jfs_lz4_compress_seal_device", "jfs_open_lz4_decompress_device",
+    "jfs_gpu_mode", "jfs_stats", "jfs_stats_reset",
 ]
+
+MODE_OFF, MODE_AUTO, MODE_FORCE = 0, 1, 2
+STATS_N = 6  # index algo * 2 + dir (0 compress, 1 decompress)
 
 
 class JfsIov(ctypes.Structure):
     _fields_ = [("src", ctypes.c_void_p), ("src_len", ctypes.c_int64),
                 ("dst", ctypes.c_void_p), ("dst_cap", ctypes.c_int64)]
+
+
+class JfsOpStats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in ("calls", "blocks", "bytes_in", "bytes_out", "errors", "nanos")]
 
 
 class JfsDevBlock(ctypes.Structure):
@@ -85,6 +93,12 @@ def load() -> ctypes.CDLL:
     lib.jfs_release_staging.restype = None
     lib.jfs_device_count.argtypes = []
     lib.jfs_device_count.restype = ctypes.c_int
+    lib.jfs_gpu_mode.argtypes = []
+    lib.jfs_gpu_mode.restype = ctypes.c_int
+    lib.jfs_stats.argtypes = [ctypes.POINTER(JfsOpStats), ctypes.c_int]
+    lib.jfs_stats.restype = ctypes.c_int
+    lib.jfs_stats_reset.argtypes = []
+    lib.jfs_stats_reset.restype = None
     lib.jfs_version.argtypes = []
     lib.jfs_version.restype = ctypes.c_char_p
     lib.jfs_gen_blocks_device.argtypes = [vp, ctypes.c_int, i64, ctypes.c_char, ctypes.c_uint64, vp]

@@ -145,6 +145,70 @@ struct DevGuard {
     }
 };
 
+// JFS_GPU_CODEC (include/jfs_gpucodec.h): off | auto (default) | force
+int gpu_mode() {
+    static int m = [] {
+        const char *e = getenv("JFS_GPU_CODEC");
+        if (!e) return JFS_MODE_AUTO;
+        std::string v(e);
+        for (auto &ch : v) ch = (char)tolower((unsigned char)ch);
+        if (v == "off" || v == "0" || v == "false") return JFS_MODE_OFF;
+        if (v == "force") return JFS_MODE_FORCE;
+        return JFS_MODE_AUTO;
+    }();
+    return m;
+}
+
+// JFS_GPU_DEVICES: "all" (default), a comma list of ordinals, or a 0x mask
+uint64_t device_select_mask() {
+    const char *e = getenv("JFS_GPU_DEVICES");
+    if (!e || !*e || !strcmp(e, "all")) return ~0ull;
+    if (e[0] == '0' && (e[1] == 'x' || e[1] == 'X')) return strtoull(e + 2, nullptr, 16);
+    uint64_t m = 0;
+    for (const char *p = e; *p;) {
+        char *end = nullptr;
+        const long v = strtol(p, &end, 10);
+        if (end == p) break;
+        if (v >= 0 && v < 64) m |= 1ull << v;
+        p = *end == ',' ? end + 1 : end;
+    }
+    return m;
+}
+
+// per-(algo, dir) counters behind jfs_stats()
+struct OpStats {
+    std::atomic<uint64_t> calls{0}, blocks{0}, bytes_in{0}, bytes_out{0}, errors{0}, nanos{0};
+};
+OpStats g_stats[JFS_STATS_N];
+
+inline OpStats *op_stats(int algo, int dir) {
+    return (algo >= 0 && algo <= 2 && (dir == 0 || dir == 1)) ? &g_stats[algo * 2 + dir] : nullptr;
+}
+
+int64_t steady_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+// one host-path block's outcome
+inline void stat_block(OpStats *st, int64_t in, int64_t out) {
+    if (!st) return;
+    st->blocks.fetch_add(1, std::memory_order_relaxed);
+    if (out >= 0) {
+        st->bytes_in.fetch_add((uint64_t)(in > 0 ? in : 0), std::memory_order_relaxed);
+        st->bytes_out.fetch_add((uint64_t)out, std::memory_order_relaxed);
+    } else {
+        st->errors.fetch_add(1, std::memory_order_relaxed);
+    }
+}
+
+inline void stat_launch(int algo, int dir, int nblk) {
+    if (OpStats *st = op_stats(algo, dir)) {
+        st->calls.fetch_add(1, std::memory_order_relaxed);
+        if (nblk > 0) st->blocks.fetch_add((uint64_t)nblk, std::memory_order_relaxed);
+    }
+}
+
 std::once_flag g_once;
 // never destroyed: the coalescer workers and the staging janitor are detached
 // threads that may still look at it while static destructors run at exit
@@ -152,10 +216,13 @@ std::vector<DevCtx *> &g_devs = *new std::vector<DevCtx *>();
 std::atomic<bool> g_exiting{false};
 
 void init_devices() {
+    if (gpu_mode() == JFS_MODE_OFF) return;
     DevGuard guard;
+    const uint64_t sel = device_select_mask();
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
     for (int i = 0; i < n; i++) {
+        if (i >= 64 || !((sel >> i) & 1ull)) continue;
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, i) != hipSuccess) continue;
         if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) continue;
@@ -698,47 +765,68 @@ int64_t jfs_compress_bound(int algo, int64_t n) {
     }
 }
 
-int64_t jfs_compress(int algo, uint8_t *dst, int64_t dst_cap, const uint8_t *src, int64_t n) {
+static int64_t one_call(int algo, int dir, uint8_t *dst, int64_t dst_cap, const uint8_t *src, int64_t n) {
     if (algo != JFS_ALGO_NONE && algo != JFS_ALGO_LZ4 && algo != JFS_ALGO_ZSTD) return JFS_ERR_INVALID;
+    const int64_t t0 = steady_ns();
     jfs_iov v{src, n, dst, dst_cap};
     int64_t r;
-    if (pre_answer(algo, COMPRESS, v, &r)) return r;
-    return Coalescer::get().submit(algo, COMPRESS, v);
+    if (!pre_answer(algo, dir, v, &r)) r = Coalescer::get().submit(algo, dir, v);
+    OpStats *st = op_stats(algo, dir);
+    st->calls.fetch_add(1, std::memory_order_relaxed);
+    stat_block(st, n, r);
+    st->nanos.fetch_add((uint64_t)(steady_ns() - t0), std::memory_order_relaxed);
+    return r;
+}
+
+int64_t jfs_compress(int algo, uint8_t *dst, int64_t dst_cap, const uint8_t *src, int64_t n) {
+    return one_call(algo, COMPRESS, dst, dst_cap, src, n);
 }
 
 int64_t jfs_decompress(int algo, uint8_t *dst, int64_t dst_cap, const uint8_t *src, int64_t n) {
-    if (algo != JFS_ALGO_NONE && algo != JFS_ALGO_LZ4 && algo != JFS_ALGO_ZSTD) return JFS_ERR_INVALID;
-    jfs_iov v{src, n, dst, dst_cap};
-    int64_t r;
-    if (pre_answer(algo, DECOMPRESS, v, &r)) return r;
-    return Coalescer::get().submit(algo, DECOMPRESS, v);
+    return one_call(algo, DECOMPRESS, dst, dst_cap, src, n);
+}
+
+static int64_t batch_call(int algo, int dir, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t device_mask) {
+    const int64_t t0 = steady_ns();
+    const int64_t r = batch_common(algo, dir, nblk, iov, out_n, device_mask);
+    if (OpStats *st = op_stats(algo, dir)) {
+        st->calls.fetch_add(1, std::memory_order_relaxed);
+        if (r == JFS_OK)
+            for (int i = 0; i < nblk; i++) stat_block(st, iov[i].src_len, out_n[i]);
+        st->nanos.fetch_add((uint64_t)(steady_ns() - t0), std::memory_order_relaxed);
+    }
+    return r;
 }
 
 int64_t jfs_compress_batch(int algo, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t device_mask) {
-    return batch_common(algo, COMPRESS, nblk, iov, out_n, device_mask);
+    return batch_call(algo, COMPRESS, nblk, iov, out_n, device_mask);
 }
 
 int64_t jfs_decompress_batch(int algo, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t device_mask) {
-    return batch_common(algo, DECOMPRESS, nblk, iov, out_n, device_mask);
+    return batch_call(algo, DECOMPRESS, nblk, iov, out_n, device_mask);
 }
 
 int64_t jfs_lz4_decompress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream) {
     if (devices().empty()) return JFS_ERR_NO_DEVICE;
+    stat_launch(JFS_ALGO_LZ4, DECOMPRESS, nblk);
     return jfs_launch_lz4_decode(d_blocks, nblk, d_ret, (hipStream_t)stream) == 0 ? JFS_OK : JFS_ERR_HIP;
 }
 
 int64_t jfs_lz4_compress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream) {
     if (devices().empty()) return JFS_ERR_NO_DEVICE;
+    stat_launch(JFS_ALGO_LZ4, COMPRESS, nblk);
     return jfs_launch_lz4_encode(d_blocks, nblk, d_ret, (hipStream_t)stream) == 0 ? JFS_OK : JFS_ERR_HIP;
 }
 
 int64_t jfs_zstd_compress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream) {
     if (devices().empty()) return JFS_ERR_NO_DEVICE;
+    stat_launch(JFS_ALGO_ZSTD, COMPRESS, nblk);
     return jfs_launch_zstd_encode(d_blocks, nblk, d_ret, (hipStream_t)stream) == 0 ? JFS_OK : JFS_ERR_HIP;
 }
 
 int64_t jfs_zstd_decompress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream) {
     if (devices().empty()) return JFS_ERR_NO_DEVICE;
+    stat_launch(JFS_ALGO_ZSTD, DECOMPRESS, nblk);
     return jfs_launch_zstd_decode(d_blocks, nblk, d_ret, nullptr, (hipStream_t)stream) == 0 ? JFS_OK : JFS_ERR_HIP;
 }
 
@@ -781,6 +869,32 @@ int64_t jfs_open_lz4_decompress_device(const jfs_aead_block *d_aead, const jfs_d
 }
 
 int jfs_device_count(void) { return (int)devices().size(); }
+
+int jfs_gpu_mode(void) { return gpu_mode(); }
+
+int jfs_stats(jfs_op_stats *out, int n) {
+    for (int i = 0; out && i < n && i < JFS_STATS_N; i++) {
+        const OpStats &g = g_stats[i];
+        out[i].calls = g.calls.load(std::memory_order_relaxed);
+        out[i].blocks = g.blocks.load(std::memory_order_relaxed);
+        out[i].bytes_in = g.bytes_in.load(std::memory_order_relaxed);
+        out[i].bytes_out = g.bytes_out.load(std::memory_order_relaxed);
+        out[i].errors = g.errors.load(std::memory_order_relaxed);
+        out[i].nanos = g.nanos.load(std::memory_order_relaxed);
+    }
+    return JFS_STATS_N;
+}
+
+void jfs_stats_reset(void) {
+    for (OpStats &g : g_stats) {
+        g.calls = 0;
+        g.blocks = 0;
+        g.bytes_in = 0;
+        g.bytes_out = 0;
+        g.errors = 0;
+        g.nanos = 0;
+    }
+}
 
 void jfs_release_staging(void) {
     for (DevCtx *d : devices()) {

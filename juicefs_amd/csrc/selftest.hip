@@ -29,6 +29,7 @@ extern "C" int jfs_selftest_wave(const uint32_t *d_in, uint32_t *d_out) {
     return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
 }
 
+#ifdef JFS_DIAG  // diagnostic builds only (scripts/build_variant.sh diag -DJFS_DIAG), never in the product .so
 // Probe: does this device honour unaligned LDS b128/b64 reads (SH_MEM_CONFIG
 // alignment mode)?  out[l*4 + j] = dword j of ds_read_b128 at byte l (l < 16),
 // out[64 + l*2 + j] = dword j of ds_read_b64 at byte 4*l.
@@ -59,3 +60,4 @@ extern "C" int jfs_selftest_lds_align(uint32_t *d_out) {
     if (hipGetLastError() != hipSuccess) return -1;
     return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
 }
+#endif  // JFS_DIAG

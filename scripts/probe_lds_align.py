@@ -1,3 +1,4 @@
+# Diagnostic: needs the diag variant (scripts/build_variant.sh diag -DJFS_DIAG; JFS_GPU_LIB=juicefs_amd/lib/libjfsgpu_diag.so)
 import ctypes, sys
 sys.path.insert(0, '/root/repo')
 import torch

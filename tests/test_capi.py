@@ -64,3 +64,58 @@ def test_empty_input_errors_before_device(lib):
 
 def test_version(lib):
     assert b"gfx950" in lib.jfs_version()
+
+
+def _stats(lib):
+    arr = (L.JfsOpStats * L.STATS_N)()
+    assert lib.jfs_stats(arr, L.STATS_N) == L.STATS_N
+    return arr
+
+
+def test_stats_count_host_path_blocks(lib):
+    # counters behind cachedStore's data-bytes metrics (cached_store.go:931-974);
+    # the "none" codec is a host memmove, so this runs without a GPU
+    lib.jfs_stats_reset()
+    src = b"x" * 1000
+    dst = ctypes.create_string_buffer(1000)
+    assert lib.jfs_compress(0, dst, 1000, src, 1000) == 1000
+    assert lib.jfs_compress(0, dst, 10, src, 1000) == L.JFS_ERR_SHORT_BUFFER
+    assert lib.jfs_decompress(0, dst, 1000, src, 600) == 600
+    iov = (L.JfsIov * 2)(L.JfsIov(ctypes.cast(src, ctypes.c_void_p), 100, ctypes.addressof(dst), 1000),
+                         L.JfsIov(ctypes.cast(src, ctypes.c_void_p), 200, ctypes.addressof(dst), 1000))
+    out = (ctypes.c_int64 * 2)()
+    assert lib.jfs_compress_batch(0, 2, iov, out, 0) == 0 and list(out) == [100, 200]
+    s = _stats(lib)
+    c, d = s[0], s[1]  # algo none: compress, decompress
+    assert (c.calls, c.blocks, c.bytes_in, c.bytes_out, c.errors) == (3, 4, 1300, 1300, 1)
+    assert (d.calls, d.blocks, d.bytes_in, d.bytes_out, d.errors) == (1, 1, 600, 600, 0)
+    assert all(s[i].calls == 0 for i in range(2, L.STATS_N))
+    lib.jfs_stats_reset()
+    assert _stats(lib)[0].calls == 0
+
+
+def _mode_in_subprocess(env_value, devices=None):
+    import subprocess
+    import sys
+    env = dict(os.environ)
+    env["JFS_GPU_CODEC"] = env_value
+    if devices is not None:
+        env["JFS_GPU_DEVICES"] = devices
+    code = ("import ctypes; from juicefs_amd import _lib as L; lib = L.load(); "
+            "d = ctypes.create_string_buffer(64); "
+            "print(lib.jfs_gpu_mode(), lib.jfs_device_count(), lib.jfs_compress(1, d, 64, b'a' * 20, 20))")
+    r = subprocess.run([sys.executable, "-c", code], env=env, cwd=ROOT, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    return [int(x) for x in r.stdout.split()]
+
+
+def test_codec_selector_env():
+    # JFS_GPU_CODEC=off|auto|force (+ JFS_GPU_DEVICES mask)
+    mode, ndev, rc = _mode_in_subprocess("off")
+    assert (mode, ndev, rc) == (L.MODE_OFF, 0, L.JFS_ERR_NO_DEVICE)
+    assert _mode_in_subprocess("FORCE")[0] == L.MODE_FORCE
+    assert _mode_in_subprocess("auto")[0] == L.MODE_AUTO
+    assert _mode_in_subprocess("bogus")[0] == L.MODE_AUTO
+    # an empty device selection leaves no device (and no CPU fallback)
+    mode, ndev, rc = _mode_in_subprocess("force", devices="0x0")
+    assert (mode, ndev, rc) == (L.MODE_FORCE, 0, L.JFS_ERR_NO_DEVICE)
