@@ -249,6 +249,61 @@ def host_path_rate(comp_blocks, raw_blocks, U, nblk, reps=2):
                     "host buffers, 2-stream chunk pipeline, 1 GPU, GiB/s of uncompressed bytes"}
 
 
+def oneshot_concurrency(comp_blocks, raw_blocks, U, n_dec=200, n_enc=20, rounds=2):
+    """The drop-in shape: pkg/chunk's one-call-per-block Compress/Decompress
+    from many goroutines at once (max-downloads 200, max-uploads 20,
+    cmd/flags.go:133-139), here Python threads calling the C ABI (the GIL is
+    released inside each call; the library's coalescer batches whatever is
+    queued).  Per-call latency percentiles and aggregate throughput; a lone
+    call's latency for comparison.  Every output is checked."""
+    import threading
+    from juicefs_amd import compress as C
+    c = C.LZ4()
+    bound = c.CompressBound(U)
+
+    def pct(v, q):
+        v = sorted(v)
+        return v[min(len(v) - 1, int(q * len(v)))] * 1e3
+
+    def run(n, k, fn):
+        lat, errs = [[] for _ in range(n)], []
+        bar = threading.Barrier(n + 1)
+
+        def worker(t):
+            bar.wait()
+            for r in range(k):
+                t0 = time.perf_counter()
+                ok = fn(t, r)
+                lat[t].append(time.perf_counter() - t0)
+                if not ok:
+                    errs.append((t, r))
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(n)]
+        for x in th:
+            x.start()
+        bar.wait()
+        t0 = time.perf_counter()
+        for x in th:
+            x.join()
+        wall = time.perf_counter() - t0
+        flat = [v for row in lat for v in row]
+        return {"calls": n * k, "p50_ms": pct(flat, 0.5), "p99_ms": pct(flat, 0.99),
+                "value": n * k * U / wall / 2**30, "unit": "GiB/s", "errors": len(errs)}
+
+    nc = len(comp_blocks)
+    ddst = [bytearray(U) for _ in range(n_dec)]
+    dec = lambda t, r: c.Decompress(ddst[t], comp_blocks[(t + r) % nc])[0] == U and \
+        ddst[t] == raw_blocks[(t + r) % nc]
+    edst = [bytearray(bound) for _ in range(n_enc)]
+    enc = lambda t, r: c.Compress(edst[t], raw_blocks[(t + r) % nc])[0] > 0
+    run(4, 1, dec)  # warm the coalescer and staging
+    out = {"decompress_lone": run(1, 5, dec), "compress_lone": run(1, 2, enc),
+           f"decompress_{n_dec}_concurrent": run(n_dec, rounds, dec),
+           f"compress_{n_enc}_concurrent": run(n_enc, 1, enc),
+           "path": "LZ4 one-call API (jfs_compress / jfs_decompress) from concurrent host threads, host buffers, "
+                   "1 GPU; value = uncompressed GiB/s over the wall time of all calls"}
+    return out
+
+
 def configs0_roundtrip(dev, nblk, U, seed_base=90001):
     """BASELINE configs[0]: LZ4 round trip of nblk x 4 MiB synthetic host
     blocks through the pkg/compress-shaped C ABI (jfs_compress_batch then
@@ -599,6 +654,10 @@ def main():
                     out["host_path"] = host_path_rate(comp_blocks, raw_blocks, U, a.host_blocks)
                 except Exception as e:
                     out["host_path"] = {"error": repr(e)}
+                try:
+                    out["oneshot_concurrency"] = oneshot_concurrency(comp_blocks, raw_blocks, U)
+                except Exception as e:
+                    out["oneshot_concurrency"] = {"error": repr(e)}
                 if not a.no_mixed:
                     try:
                         out["mixed_host_path"] = mixed_host_path(raw_blocks, a.mixed_blocks)

@@ -26,4 +26,4 @@ w = max(buf[10], 1)
 print(f"windows/block {buf[10]/nblk:.1f}  per window: walk iters {buf[11]/w:.2f}  fix-up rounds {buf[12]/w:.2f}  "
       f"partial iters {buf[13]/w:.2f}  batches {buf[14]/w:.2f}  near copy iters {buf[15]/w:.2f}")
 b = max(buf[14], 1)
-print(f"per batch: literal iters {buf[16]/b:.2f}  far iters {buf[17]/b:.2f}  near rounds {buf[18]/b:.2f}  near copy iters {buf[15]/b:.2f}")
+print(f"per batch: literal iters {buf[16]/b:.2f}  far iters {buf[17]/b:.2f}  near rounds {buf[18]/b:.2f}  near copy iters {buf[15]/b:.2f}  serial near matches {buf[19]/b:.2f}")
