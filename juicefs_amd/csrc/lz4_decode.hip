@@ -745,6 +745,7 @@ __device__ __forceinline__ void batch(Smem &s, Ctx &c, bool act, int32_t o, uint
         }
         for (uint64_t pmk = __ballot(pend); pmk; pmk &= pmk - 1) {
             const int j = (int)__builtin_ctzll(pmk);
+            PCOUNT(19, 1);
             wave_near(s, c, (int32_t)readlane((uint32_t)pos, j), (int32_t)readlane((uint32_t)D, j),
                       (int32_t)readlane((uint32_t)rem, j));
         }

@@ -41,7 +41,11 @@ __device__ unsigned long long g_zprof[8];
 #define ZP_NOW() __builtin_amdgcn_s_memtime()
 #define ZP_ADD(i, v) do { if (lane_id() == 0) atomicAdd(&g_zprof[i], (unsigned long long)(v)); } while (0)
 #define XP_ADD(i, v) do { x.pacc[i] += (v); } while (0)
+// zseq: 0 phase A (walk + tables), 1 table staging, 2 phase B decode, 3 phase C, 4 sub-groups, 5 groups
+__device__ unsigned long long g_zsprof[8];
+#define ZS_ADD(i, v) do { if (lane_id() == 0) atomicAdd(&g_zsprof[i], (unsigned long long)(v)); } while (0)
 #else
+#define ZS_ADD(i, v) do { } while (0)
 #define XP_ADD(i, v) do { } while (0)
 #define ZP_NOW() 0ull
 #define ZP_ADD(i, v) do { } while (0)
@@ -1026,13 +1030,45 @@ struct GBlk {
 };
 // Inputs per sequence workgroup: a 4 MiB frame has 32 compressed blocks, so
 // two inputs fill the 64 lanes of phase B.
-constexpr int ZSEQ_INPUTS = 2;
+#ifndef JFS_ZSEQ_INPUTS
+#define JFS_ZSEQ_INPUTS 2
+#endif
+constexpr int ZSEQ_INPUTS = JFS_ZSEQ_INPUTS;
+// Phase B decodes with the tables in LDS: the blocks of a group are taken in
+// sub-groups whose tables fit this arena (u16 cells; >= 11 blocks of the
+// largest tables), one lane per block.  Gathers from a per-block table in HBM
+// (2.5 KiB x 64 lanes x every wave: hundreds of MiB live at once) missed every
+// cache and each sequence waited on one, behind the wave's item stores.
+#ifndef JFS_ZSEQ_ARENA
+#define JFS_ZSEQ_ARENA 0  // > 0: tables staged in LDS per sub-group (measured slower: few lanes per wave)
+#endif
+constexpr int ZARENA = JFS_ZSEQ_ARENA;
+#ifndef JFS_ZSEQ_RING
+#define JFS_ZSEQ_RING 1  // tables in HBM: bitstreams staged in LDS rings, items buffered in LDS
+#endif
+// lanes (blocks) per phase-B pass, sequences per period (one HBM round trip:
+// bitstream refill + item flush), ring bytes per lane (16-byte blocks)
+constexpr int ZSUB = JFS_ZSEQ_ARENA > 0 ? 16 : 64;
+constexpr int ZK = JFS_ZSEQ_ARENA > 0 ? 8 : 4;
+constexpr int ZRB = JFS_ZSEQ_ARENA > 0 ? 256 : 128;
+static_assert(ZK * 12 + 24 <= ZRB - 16 && ZRB / 16 - 1 <= 15 + 0, "a period's bits must stay resident");
+static_assert(ZARENA == 0 || ZARENA >= 1280 + 8, "one block's largest tables must fit");
 struct SeqSmem {
     uint8_t stage[256];
     int16_t norm[64];
     uint8_t symat[512], mark[512], ksym[512];
     uint32_t lut_ll[36], lut_ml[53];  // value base | extra bits << 24
     GBlk g[64];
+#if JFS_ZSEQ_ARENA > 0
+    alignas(16) uint16_t arena[ZARENA];
+    uint16_t aofs[64][4];   // arena cell offsets of a sub-group block's LL / OF / ML tables
+    uint32_t rr[3][64];     // phase B results per group block: symbolic repeat offsets
+    uint32_t brep[64];
+#endif
+#if JFS_ZSEQ_ARENA > 0 || JFS_ZSEQ_RING
+    alignas(16) uint8_t bring[ZSUB][ZRB];  // per-lane sequence bitstream ring (16-byte blocks)
+    uint4 ibuf[ZK][ZSUB];                  // items of the current period, flushed together
+#endif
 };
 
 // u16 cell = sym | ns << 6  (nb = al - highbit(ns), next-state base = (ns << nb) - 2^al)
@@ -1140,12 +1176,258 @@ __device__ __forceinline__ uint32_t rep_res(uint32_t v, uint32_t e0, uint32_t e1
     return e > d + 1 ? e - d : 1u;
 }
 
+#if JFS_ZSEQ_ARENA > 0 || JFS_ZSEQ_RING
+// Backward bit reader over a per-lane LDS ring of ZRB / 16 stream blocks (16 B
+// each; block k at ring offset (k & 15) * 16, blocks below the input read as
+// zero).  Same bit semantics as BR; the ring is refilled once per period of ZK
+// sequences (<= 89 bits per sequence: <= 6 blocks per period), so the
+// sequence loop itself waits on LDS only.
+struct LR {
+    const gc_u4 *b16;
+    uint8_t *ring;
+    int32_t m, lowk, left, cb, lr;  // lr: lowest block resident in the ring
+    uint64_t c;
+};
+
+__device__ __forceinline__ uint32_t lr_dw(const LR &r, int32_t q) { return *(const uint32_t *)(r.ring + (q & (ZRB - 1))); }
+
+// blocks [lo, r.lr) into the ring (at most 8); r.lr = lo
+__device__ __forceinline__ void lr_load(LR &r, int32_t lo, bool on) {
+    uint4 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int32_t k = r.lr - 1 - j;
+        v[j] = make_uint4(0, 0, 0, 0);
+        if (on && k >= lo && k >= r.lowk) v[j] = r.b16[k];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int32_t k = r.lr - 1 - j;
+        if (on && k >= lo) *(uint4 *)(r.ring + ((k & (ZRB / 16 - 1)) << 4)) = v[j];
+    }
+    if (on && lo < r.lr) r.lr = lo;
+}
+
+__device__ __forceinline__ bool lr_init(LR &r, uint8_t *ring, const gc_u8 *in, const gc_u8 *p, int32_t size) {
+    const uintptr_t a = (uintptr_t)p;
+    r.ring = ring;
+    r.b16 = (const gc_u4 *)(a & ~(uintptr_t)15);
+    r.m = (int32_t)(a & 15);
+    r.lowk = -(int32_t)((((uintptr_t)r.b16) - (((uintptr_t)in) & ~(uintptr_t)15)) >> 4);
+    if (size <= 0) return false;
+    const int32_t top = r.m + size;
+    const uint32_t last = ((const gc_u8 *)r.b16)[top - 1];
+    if (last == 0) return false;
+    r.left = 8 * (top - 1) + (31 - __builtin_clz(last));
+    r.cb = ((top - 1) & ~3) - 4;
+    r.lr = ((top - 1) >> 4) + 1;  // nothing resident yet
+    return true;
+}
+
+// first fill (after lr_init; wave-uniform call, `on` = this lane reads a stream)
+__device__ __forceinline__ void lr_start(LR &r, bool on) {
+    const int32_t kt = r.lr - 1;
+    lr_load(r, kt - 7, on);
+    if (ZRB / 16 > 8) lr_load(r, kt - (ZRB / 16 - 1), on);
+    __builtin_amdgcn_wave_barrier();
+    if (on) r.c = ((uint64_t)lr_dw(r, r.cb + 4) << 32) | lr_dw(r, r.cb);
+}
+
+// start of a period: blocks [ck - 15, ck] resident, ck = block of the next dword
+__device__ __forceinline__ void lr_period(LR &r, bool on) {
+    lr_load(r, ((r.cb - 4) >> 4) - (ZRB / 16 - 1), on);
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ uint32_t lr_read(LR &r, int n) {
+    if (n == 0) return 0u;
+    const int32_t lo = r.left - n;
+    uint32_t v = (uint32_t)(r.c >> (uint32_t)(lo - 8 * r.cb)) & (uint32_t)(0xFFFFFFFFull >> (32 - n));
+    const int32_t d = 8 * r.m - lo;
+    if (d > 0) v = d >= n ? 0u : v & ~((1u << d) - 1u);
+    r.left = lo;
+    if (r.left - 8 * r.cb < 32) {
+        r.cb -= 4;
+        r.c = (r.c << 32) | lr_dw(r, r.cb);
+    }
+    return v;
+}
+#endif
+
+#if JFS_ZSEQ_ARENA > 0 || JFS_ZSEQ_RING
+// Phase B with the sequence bitstreams staged in per-lane LDS rings and the
+// items buffered in LDS: one HBM round trip per period of ZK sequences (ring
+// refill + item flush) instead of several per sequence.  TP: table cells in
+// LDS (arena) or in HBM.
+template <class TP>
+__device__ __forceinline__ void seq_periods(SeqSmem &sm, const GBlk &d, bool mine, TP tl, TP to, TP tm, uint32_t &r0,
+                                            uint32_t &r1, uint32_t &r2, uint32_t &brep) {
+    // lanes [0, g1 - g0): one block each; periods of ZK sequences, each
+    // starting with a ring refill and ending with the item flush
+    const int l = lane_id();
+    const int32_t all = d.al & 0xFF, alof = (d.al >> 8) & 0xFF, alml = (d.al >> 16) & 0xFF;
+    g_u4 *it = d.ib + d.item;
+    bool run = false;
+    LR r = {};
+    if (mine) {
+        if (d.nseq == 0) {
+            it[1] = make_uint4(0, 0, 0, IT_BREP);
+            it[2] = make_uint4(0, 0, 0, IT_BEND);
+            brep = 1;
+        } else if (!lr_init(r, sm.bring[mine ? l : 0], d.in, d.bs, d.bsz)) {
+            it[1] = make_uint4(0, 0, (uint32_t)E_CORRUPT, IT_ERR);
+        } else {
+            brep = 1;
+            run = true;
+        }
+    }
+    lr_start(r, run);
+    uint32_t sll = 0, sof = 0, sml = 0;
+    if (run) {
+        sll = lr_read(r, all);
+        sof = lr_read(r, alof);
+        sml = lr_read(r, alml);
+    }
+    const uint32_t szl = 1u << all, szo = 1u << alof, szm = 1u << alml;
+    for (int32_t i0 = 0; __ballot(run); i0 += ZK) {
+        lr_period(r, run);
+        int32_t nbuf = 0;
+        bool fin = false;
+        uint4 term = make_uint4(0, 0, 0, 0);
+        int32_t tidx = 0;
+        for (int k = 0; k < ZK; ++k) {
+            if (run) {
+                const int32_t i = i0 + k;
+                if (r.left < 8 * r.m) {  // overflow
+                    term = make_uint4(0, 0, (uint32_t)E_CORRUPT, IT_ERR);
+                    tidx = 2 + i;
+                    fin = true;
+                    run = false;
+                } else {
+                    const uint32_t cl = tl[sll], co = to[sof], cm = tm[sml];
+                    const uint32_t lv = sm.lut_ll[cl & 63], mv = sm.lut_ml[cm & 63], ofc = co & 63;
+                    const uint32_t ofv = (1u << ofc) + lr_read(r, (int)ofc);
+                    const uint32_t ml = (mv & 0xFFFFFFu) + lr_read(r, (int)(mv >> 24));
+                    const uint32_t ll = (lv & 0xFFFFFFu) + lr_read(r, (int)(lv >> 24));
+                    uint32_t off;
+                    if (ofv > 3) {
+                        off = ofv - 3;
+                        r2 = r1; r1 = r0; r0 = off;
+                    } else {
+                        const uint32_t kk = ofv - 1 + (ll == 0 ? 1u : 0u);
+                        if (kk == 0) {
+                            off = r0;
+                        } else {
+                            const uint32_t t = kk == 1 ? r1 : kk == 2 ? r2 : rep_dec(r0);
+                            if (kk != 1) r2 = r1;
+                            r1 = r0;
+                            r0 = t;
+                            off = t;
+                        }
+                    }
+                    if (i + 1 < d.nseq) {
+                        const uint32_t nsl = cl >> 6, nso = co >> 6, nsm = cm >> 6;
+                        const int nbl = all - (31 - __builtin_clz(nsl));
+                        const int nbm = alml - (31 - __builtin_clz(nsm));
+                        const int nbo = alof - (31 - __builtin_clz(nso));
+                        sll = ((nsl << nbl) - szl) + lr_read(r, nbl);
+                        sml = ((nsm << nbm) - szm) + lr_read(r, nbm);
+                        sof = ((nso << nbo) - szo) + lr_read(r, nbo);
+                    }
+                    sm.ibuf[k][l] = make_uint4(ll, ml, off, IT_SEQ);
+                    nbuf = k + 1;
+                    if (i + 1 == d.nseq) {
+                        term = r.left == 8 * r.m ? make_uint4(0, 0, 0, IT_BEND)
+                                                 : make_uint4(0, 0, (uint32_t)E_CORRUPT, IT_ERR);
+                        tidx = 2 + d.nseq;
+                        fin = true;
+                        run = false;
+                    }
+                }
+            }
+        }
+        // flush the period's items (then the block's terminal item)
+        if (mine) {
+#pragma unroll
+            for (int k = 0; k < ZK; ++k)
+                if (k < nbuf) it[2 + i0 + k] = sm.ibuf[k][l];
+            if (fin) it[tidx] = term;
+        }
+    }
+}
+
+#endif
+
 // phases B and C for the collected group
 __device__ __forceinline__ void seq_group(SeqSmem &sm, int gn, const gc_u16 *tabs, uint32_t *e0, uint32_t *e1,
                                           uint32_t *e2) {
     const int l = lane_id();
+    uint64_t zt = ZP_NOW();
+    ZS_ADD(5, 1);
     __builtin_amdgcn_wave_barrier();
     wait_vm();  // table cells written in phase A are complete before they are gathered
+#if JFS_ZSEQ_ARENA > 0
+    for (int g0 = 0; g0 < gn;) {
+    // sub-group [g0, g1): as many blocks as the arena holds; their tables are
+    // staged field by field (all loads of a block before its LDS writes)
+    int g1 = g0;
+    {
+        uint32_t used = 0;
+        while (g1 < gn) {
+            const uint32_t a = sm.g[g1].al;
+            const uint32_t nl = 1u << (a & 0xFF), no = 1u << ((a >> 8) & 0xFF), nm = 1u << ((a >> 16) & 0xFF);
+            const uint32_t sz = ((nl + 1) & ~1u) + ((no + 1) & ~1u) + ((nm + 1) & ~1u);
+            if (used + sz > (uint32_t)ZARENA || g1 - g0 >= ZSUB) break;
+            const uint32_t ol = used, oo = ol + ((nl + 1) & ~1u), om = oo + ((no + 1) & ~1u);
+            const GBlk &d = sm.g[g1];
+            const gc_u32 *ql = (const gc_u32 *)(tabs + d.tll), *qo = (const gc_u32 *)(tabs + d.tof),
+                         *qm = (const gc_u32 *)(tabs + d.tml);
+            const uint32_t dl = (nl + 1) >> 1, dof = (no + 1) >> 1, dm = (nm + 1) >> 1;  // dwords
+            uint32_t vl[4], vo[2], vm[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) vl[j] = (uint32_t)l + 64u * j < dl ? ql[l + 64 * j] : 0u;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) vo[j] = (uint32_t)l + 64u * j < dof ? qo[l + 64 * j] : 0u;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) vm[j] = (uint32_t)l + 64u * j < dm ? qm[l + 64 * j] : 0u;
+            uint32_t *ar = (uint32_t *)sm.arena;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if ((uint32_t)l + 64u * j < dl) ar[(ol >> 1) + l + 64 * j] = vl[j];
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                if ((uint32_t)l + 64u * j < dof) ar[(oo >> 1) + l + 64 * j] = vo[j];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if ((uint32_t)l + 64u * j < dm) ar[(om >> 1) + l + 64 * j] = vm[j];
+            if (l == 0) {
+                sm.aofs[g1 - g0][0] = (uint16_t)ol;
+                sm.aofs[g1 - g0][1] = (uint16_t)oo;
+                sm.aofs[g1 - g0][2] = (uint16_t)om;
+            }
+            used += sz;
+            g1++;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    ZS_ADD(4, 1);
+    { const uint64_t t = ZP_NOW(); ZS_ADD(1, t - zt); zt = t; }
+    uint32_t r0 = SYMB | (0u << 29), r1 = SYMB | (1u << 29), r2 = SYMB | (2u << 29);
+    uint32_t brep = 0;
+    const bool mine = l < g1 - g0;
+    const GBlk d = sm.g[mine ? g0 + l : g0];
+    seq_periods(sm, d, mine, (const uint16_t *)sm.arena + sm.aofs[mine ? l : 0][0],
+                (const uint16_t *)sm.arena + sm.aofs[mine ? l : 0][1], (const uint16_t *)sm.arena + sm.aofs[mine ? l : 0][2],
+                r0, r1, r2, brep);
+#elif JFS_ZSEQ_RING
+    uint32_t r0 = SYMB | (0u << 29), r1 = SYMB | (1u << 29), r2 = SYMB | (2u << 29);
+    uint32_t brep = 0;
+    {
+        const bool mine = l < gn;
+        const GBlk d = sm.g[mine ? l : 0];
+        seq_periods(sm, d, mine, tabs + d.tll, tabs + d.tof, tabs + d.tml, r0, r1, r2, brep);
+    }
+#else
     uint32_t r0 = SYMB | (0u << 29), r1 = SYMB | (1u << 29), r2 = SYMB | (2u << 29);
     uint32_t brep = 0;
     if (l < gn) {
@@ -1211,17 +1493,36 @@ __device__ __forceinline__ void seq_group(SeqSmem &sm, int gn, const gc_u16 *tab
             }
         }
     }
+#endif
+#if JFS_ZSEQ_ARENA > 0
+    if (l < g1 - g0) {
+        sm.rr[0][g0 + l] = r0;
+        sm.rr[1][g0 + l] = r1;
+        sm.rr[2][g0 + l] = r2;
+        sm.brep[g0 + l] = brep;
+    }
+    __builtin_amdgcn_wave_barrier();
+    { const uint64_t t = ZP_NOW(); ZS_ADD(2, t - zt); zt = t; }
+    g0 = g1;
+    }  // sub-groups
+#endif
     // phase C: entry states in stream order
     for (int g = 0; g < gn; g++) {
         const uint32_t al = sm.g[g].al, item = sm.g[g].item;
         g_u4 *ib = sm.g[g].ib;
         if (al >> 24) { *e0 = 1; *e1 = 4; *e2 = 8; }
+#if JFS_ZSEQ_ARENA > 0
+        const uint32_t x0 = sm.rr[0][g], x1 = sm.rr[1][g], x2 = sm.rr[2][g];
+        if (sm.brep[g] && l == 0) ib[item + 1] = make_uint4(*e0, *e1, *e2, IT_BREP);
+#else
         const uint32_t x0 = readlane(r0, g), x1 = readlane(r1, g), x2 = readlane(r2, g);
         if (readlane(brep, g) && l == 0) ib[item + 1] = make_uint4(*e0, *e1, *e2, IT_BREP);
+#endif
         const uint32_t n0 = rep_res(x0, *e0, *e1, *e2), n1 = rep_res(x1, *e0, *e1, *e2), n2 = rep_res(x2, *e0, *e1, *e2);
         *e0 = n0; *e1 = n1; *e2 = n2;
     }
     __builtin_amdgcn_wave_barrier();
+    { const uint64_t t = ZP_NOW(); ZS_ADD(3, t - zt); }
 }
 
 __global__ __launch_bounds__(64) void zseq_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
@@ -1233,6 +1534,7 @@ __global__ __launch_bounds__(64) void zseq_kernel(const jfs_dev_block *__restric
     for (int i = l; i < 53; i += 64) sm.lut_ml[i] = ML_BASE[i] | ((uint32_t)ML_BITS[i] << 24);
     int gn = 0;
     uint32_t e0 = 1, e1 = 4, e2 = 8;  // repeat offsets carried through phase C (reset at each frame)
+    uint64_t za = ZP_NOW();
     for (int f = 0; f < ZSEQ_INPUTS; ++f) {
         const int bi = blockIdx.x * ZSEQ_INPUTS + f;
         if (bi >= nblk) break;
@@ -1319,12 +1621,15 @@ __global__ __launch_bounds__(64) void zseq_kernel(const jfs_dev_block *__restric
             cur = slot + 3 + (uint32_t)nseq;
             gn++;
             if (gn == 64) {
+                ZS_ADD(0, ZP_NOW() - za);
                 seq_group(sm, gn, (const gc_u16 *)tabs_all, &e0, &e1, &e2);
+                za = ZP_NOW();
                 gn = 0;
             }
         }
         if (l == 0) zi.n_items = bug ? 0xFFFFFFFFu : cur;
     }
+    ZS_ADD(0, ZP_NOW() - za);
     if (gn) seq_group(sm, gn, (const gc_u16 *)tabs_all, &e0, &e1, &e2);
     wait_vm();
 }
@@ -1958,7 +2263,14 @@ extern "C" void jfs_zstd_plan_host(const uint8_t *const *srcs, const int32_t *le
 #ifdef JFS_PROF
 extern "C" int jfs_zprof_read(unsigned long long *out) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(jfs::zstdd::g_zprof), sizeof(unsigned long long) * 8) == hipSuccess ? 0 : -1;
+}extern "C" int jfs_zsprof_read(unsigned long long *out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(jfs::zstdd::g_zsprof), sizeof(unsigned long long) * 8) == hipSuccess ? 0 : -1;
 }
+extern "C" int jfs_zsprof_reset() {
+    unsigned long long z[8] = {0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(jfs::zstdd::g_zsprof), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+
 extern "C" int jfs_zprof_reset(void) {
     unsigned long long z[8] = {0};
     return hipMemcpyToSymbol(HIP_SYMBOL(jfs::zstdd::g_zprof), z, sizeof(z)) == hipSuccess ? 0 : -1;
