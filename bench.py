@@ -510,6 +510,28 @@ def checksum_and_aead(batch, S, world, dev):
     return out
 
 
+def other_classes(a, S, world, rank, dev, nblk=1024):
+    """SURVEY.md 8d data classes besides text: Z (zeros: a few long matches per
+    block, the copy engine's bandwidth) and R (random: stored literal runs,
+    a sanity bound near a device memcpy).  LZ4 decode of nblk x 4 MiB blocks
+    in HBM, every block verified."""
+    from juicefs_amd import device as D
+    out = {}
+    for cls in ("Z", "R"):
+        b = D.Lz4Batch(nblk, a.block_bytes, cls, seed_base=S.seed_base(rank, nblk) + 777, device=dev)
+        el, kms = timed_launches(b.decompress, 3, 1, S, world, dev)
+        if not S.all_ranks_ok(b.verify(), world, dev):
+            raise RuntimeError(f"class {cls}: decoded output mismatch")
+        C = int(b.csize.sum())
+        ach = (C + nblk * a.block_bytes) / (kms / 1e3) / 1e9
+        out[cls] = {"value": S.whole_job_gib_s(world, nblk, a.block_bytes, 3, el), "unit": "GiB/s", "kernel_ms": kms,
+                    "ratio": nblk * a.block_bytes / C, "blocks": nblk,
+                    "roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": ach / HBM_PEAK_GBS}}
+        del b
+    return out
+
+
 def measured_traffic(path, nblk, U):
     """HBM bytes per launch from profiles/traffic.json, only if it was
     measured on these kernel sources at this workload."""
@@ -615,6 +637,10 @@ def main():
             out["checksum_aead"] = checksum_and_aead(batch, S, world, dev)
         except Exception as e:
             out["checksum_aead"] = {"error": repr(e)}
+        try:
+            out["lz4_other_classes"] = other_classes(a, S, world, rank, dev)
+        except Exception as e:
+            out["lz4_other_classes"] = {"error": repr(e)}
     if rank == 0 and world == 1:
         # bounded sample for the CPU legs: 32 distinct blocks of the headline batch
         ns = min(32, nblk)

@@ -1,0 +1,25 @@
+#!/bin/bash
+# Round evidence on the GPU box (run from the repo root under gpurun):
+#   GPU parity tests, smoke, PMC traffic of the headline kernel (stamped),
+#   the full bench line (with that traffic), rocprofv3 kernel stats of the
+#   headline and of the Zstd decode.  Every step has its own time limit; the
+#   script stops at the first failure.  Output: gpurun_out/ev/.
+set -e
+export TMPDIR=/tmp
+O=gpurun_out/ev
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1
+tail -1 $O/gpu_tests.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+tail -1 $O/smoke.log
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/pf -o pf --output-format csv -- python scripts/prof_run.py 4096 1 T > $O/pf.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $O/pw -o pw --output-format csv -- python scripts/prof_run.py 4096 1 T > $O/pw.log 2>&1
+python scripts/traffic.py $(find $O/pf -name '*counter_collection.csv' | head -1) $(find $O/pw -name '*counter_collection.csv' | head -1) lz4_decode_kernel 4096 4194304 $O/traffic.json > /dev/null
+timeout -k 10 900 python bench.py --traffic-file $O/traffic.json > $O/bench.json 2> $O/bench.err
+tail -c 400 $O/bench.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt_lz4 -o kt --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-extras --no-host-path --traffic-file $O/traffic.json > $O/kt_lz4.log 2>&1
+find $O/kt_lz4 -name '*kernel_stats.csv' -exec cp {} $O/lz4_kernel_stats.csv \;
+timeout -k 10 300 python scripts/prof_run.py 4096 0 T zstd > /dev/null 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt_zstd -o kt --output-format csv -- python scripts/prof_run.py 4096 3 T zstd > $O/kt_zstd.log 2>&1
+find $O/kt_zstd -name '*kernel_stats.csv' -exec cp {} $O/zstd_kernel_stats.csv \;
+echo evidence-done

@@ -16,9 +16,11 @@ def sha(b):
     return hashlib.sha256(b).hexdigest()
 
 
-def test_compressor_contract_lz4_and_none(gpu):
-    """compress_test.go:25-64 (testCompress) for "lz4" and "none"."""
-    for name in ("lz4", "none"):
+@pytest.mark.parametrize("name", ["lz4", "none", "zstd"])
+def test_compressor_contract(gpu, name):
+    """compress_test.go:25-64 (testCompress), replayed verbatim for every
+    codec of compress_test.go:66-76 (TestUncompressed, TestZstd, TestLZ4)."""
+    for name in (name,):
         c = C.NewCompressor(name)
         src0 = c.Name().encode()
         for src in (src0, b""):
