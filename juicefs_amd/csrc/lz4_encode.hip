@@ -31,6 +31,22 @@
 namespace jfs {
 namespace lz4e {
 
+#ifdef JFS_PROF
+// diagnostic build only: per-phase s_memtime sums of the encoder wave
+__device__ unsigned long long g_eprof[12];
+#define EP_DECL uint64_t ep_t = __builtin_amdgcn_s_memtime(), ep_acc[12] = {0};
+#define EP(k) do { const uint64_t x_ = __builtin_amdgcn_s_memtime(); ep_acc[k] += x_ - ep_t; ep_t = x_; } while (0)
+#define EPC(k) (ep_acc[k] += 1)
+#define EP_FLUSH() do { if (lane_id() == 0) for (int i_ = 0; i_ < 12; ++i_) atomicAdd(&g_eprof[i_], (unsigned long long)ep_acc[i_]); } while (0)
+#else
+#define EP_DECL
+#define EP(k) do { } while (0)
+#define EPC(k) do { } while (0)
+#define EP_FLUSH() do { } while (0)
+#endif
+#ifndef JFS_LZ4E_PSEARCH
+#define JFS_LZ4E_PSEARCH 1  // lane-parallel search over the skip schedule (serial loop on shared hashes)
+#endif
 constexpr int64_t kMaxInput = 0x7E000000;
 constexpr int OB = 2048;  // output staging ring (the put_* paths assume OB >= 2 * OFLUSH + slack)
 constexpr int OBMASK = OB - 1;
@@ -235,6 +251,7 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(const jfs_dev_block *__r
     if (b >= nblk) return;
     const int l = lane_id();
     const jfs_dev_block d = ((const gc_blk *)blocks)[b];
+    EP_DECL
     Enc e;
     e.src = (const gc_u8 *)d.src;
     e.dst = (g_u8 *)d.dst;
@@ -281,10 +298,86 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(const jfs_dev_block *__r
             for (;;) {
                 int64_t match;
                 // ---- search (skip schedule: step = searchMatchNb++ >> 6)
+                bool last = false;
+#if JFS_LZ4E_PSEARCH
+                // Lane-parallel: lane j takes the j-th next position of the
+                // schedule; every lane reads its table entry before any insert
+                // of the batch, which is the serial order exactly when no two
+                // positions of the batch share a hash (checked by a tagged
+                // write + read-back).  The first lane whose candidate matches
+                // ends the search; positions up to it are inserted, the others'
+                // entries are restored.
+                int32_t k0 = 0;  // schedule index of lane 0
+                int64_t pk = ip;
+                for (;;) {
+                    const int32_t k = k0 + l;
+                    const int32_t sk = k == 0 ? 1 : (63 + k) >> 6;
+                    const uint32_t inc = dpp_scan_add((uint32_t)sk);
+                    const int64_t P = pk + (int64_t)(inc - (uint32_t)sk), Pn = pk + (int64_t)inc;
+                    const bool span = P - pk <= 512;
+                    const uint64_t endm = __ballot(span && Pn > mflimitP1), spm = __ballot(span);
+                    const int jend = endm ? (int)__builtin_ctzll(endm) : 64;
+                    const int jspan = ~spm ? (int)__builtin_ctzll(~spm) : 64;
+                    const int nl = jend < jspan ? jend : jspan;  // lanes [0, nl) are looked up
+                    const bool on = l < nl;
+                    if (nl > 0) sw_need(s, e, pk + (int64_t)readlane(inc - (uint32_t)sk, nl - 1), 8);
+                    uint32_t cv = 0, h = 0, E = 0;
+                    if (on) {
+                        const uint64_t v = sw_rd64(s, e, P);
+                        cv = (uint32_t)v;
+                        h = hash_of(v, u16);
+                        E = tget(s, h, u16);
+                    }
+                    EPC(7);
+                    // shared hashes in the batch: tag write, read back.  A lane
+                    // that reads another lane's tag shares its hash; the lowest
+                    // lane m of any such pair has no predecessor in the batch, so
+                    // lanes [0, m] are exact and the batch is cut after m.
+                    const uint32_t tag = (uint32_t)l + 1u;
+                    if (on) {
+                        if (u16) ((uint16_t *)s.table)[h] = (uint16_t)tag;
+                        else s.table[h] = tag;
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    uint32_t cm = 64u;
+                    if (on) {
+                        const uint32_t t = tget(s, h, u16);
+                        if (t != tag) cm = umin32((uint32_t)l, t - 1u);
+                    }
+                    const int ncut = (int)dwave_min(cm) + 1;  // 65: no shared hash
+                    const int nb = ncut < nl ? ncut : nl;     // lanes [0, nb) are exact
+                    if (on && l >= nb) {  // beyond the cut: pre-batch entries back (same hash, same entry)
+                        if (u16) ((uint16_t *)s.table)[h] = (uint16_t)E;
+                        else s.table[h] = E;
+                    }
+                    const int64_t cand = u16 ? (int64_t)E : (int64_t)(E & e.pmask);
+                    bool pass = l < nb && (u16 || cand + 65535 >= P) && may_match(e, E, cv, u16);
+                    if (__ballot(pass)) {
+                        EPC(9);
+                        if (pass) pass = src32(s, e, cand) == cv;
+                    }
+                    const uint64_t hm = __ballot(pass);
+                    const int jm = hm ? (int)__builtin_ctzll(hm) : 64;
+                    if (l < nb) {
+                        if (l <= jm) tput(s, e, h, (uint32_t)P, cv, u16);
+                        else if (u16) ((uint16_t *)s.table)[h] = (uint16_t)E;
+                        else s.table[h] = E;
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    if (hm) {
+                        ip = pk + (int64_t)readlane(inc - (uint32_t)sk, jm);
+                        match = (int64_t)readlane((uint32_t)cand, jm);
+                        break;
+                    }
+                    if (nb == nl && endm && jend <= jspan) { last = true; break; }  // the schedule passed mflimit
+                    pk += (int64_t)readlane(inc, nb - 1);
+                    k0 += nb;
+                }
+                if (false)
+#endif
                 {
                     int64_t fip = ip;
                     int32_t step = 1, snb = 1 << 6;
-                    bool last = false;
                     for (;;) {
                         const uint32_t h = fh;
                         const int64_t cur = fip;
@@ -298,12 +391,19 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(const jfs_dev_block *__r
                         fv = src64(s, e, fip);
                         fh = hash_of(fv, u16);
                         tput(s, e, h, (uint32_t)cur, cv, u16);
+                        EPC(7);
                         if (!u16 && match + 65535 < cur) continue;
                         if (!may_match(e, ent, cv, u16)) continue;
-                        if (src32(s, e, match) == cv) break;
+                        EP(0);
+                        EPC(9);
+                        const bool hit = src32(s, e, match) == cv;
+                        EP(1);
+                        if (hit) break;
                     }
-                    if (last) break;
                 }
+                EP(0);
+                if (last) break;
+                EPC(8);
                 // ---- catch up (backwards, 64 bytes per step)
                 {
                     int64_t lim = ip - anchor;
@@ -321,6 +421,7 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(const jfs_dev_block *__r
                     ip -= back;
                     match -= back;
                 }
+                EP(2);
                 // ---- literals
                 int64_t tp = e.op;
                 uint32_t token;
@@ -331,6 +432,7 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(const jfs_dev_block *__r
                     else token = (uint32_t)lit << 4;
                     put_lits(s, e, anchor, lit, tp);
                 }
+                EP(3);
                 for (;;) {  // next_match
                     uint32_t off = (uint32_t)(ip - match);
                     put1(s, e, off & 255);
@@ -353,15 +455,23 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(const jfs_dev_block *__r
                     } else {
                         token += (uint32_t)mc;
                     }
+                    EP(4);
                     put_token(s, e, tp, token);
                     maybe_flush(s, e, INT64_MAX);
+                    EP(5);
                     anchor = ip;
                     if (ip >= mflimitP1) break;
-                    {
-                        const uint64_t v2 = src64(s, e, ip - 2);
-                        tput(s, e, hash_of(v2, u16), (uint32_t)(ip - 2), (uint32_t)v2, u16);
+                    // bytes at ip - 2 and ip: one window check, both reads issued together
+                    uint64_t v2, vi;
+                    sw_need(s, e, ip + 2, 8);
+                    if (sw_has(e, ip - 2, 12)) {
+                        v2 = sw_rd64(s, e, ip - 2);
+                        vi = sw_rd64(s, e, ip);
+                    } else {
+                        v2 = src64(s, e, ip - 2);
+                        vi = src64(s, e, ip);
                     }
-                    const uint64_t vi = src64(s, e, ip);
+                    tput(s, e, hash_of(v2, u16), (uint32_t)(ip - 2), (uint32_t)v2, u16);
                     const uint32_t h = hash_of(vi, u16);
                     const uint32_t ent = tget(s, h, u16);
                     const uint32_t mi = u16 ? ent : (ent & e.pmask);
@@ -370,7 +480,9 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(const jfs_dev_block *__r
                     if (rm) {
                         rm = src32(s, e, mi) == (uint32_t)vi;
                     }
+                    EP(6);
                     if (rm) {
+                        EPC(10);
                         match = mi;
                         tp = e.op;
                         e.op++;
@@ -383,6 +495,7 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(const jfs_dev_block *__r
                 ++ip;
                 fv = src64(s, e, ip);
                 fh = hash_of(fv, u16);
+                EP(0);
             }
         }
         // ---- last literals
@@ -404,6 +517,7 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(const jfs_dev_block *__r
         }
     }
     if (l == 0) ret[b] = result;
+    EP_FLUSH();
 }
 
 }  // namespace lz4e
@@ -414,3 +528,13 @@ extern "C" int jfs_launch_lz4_encode(const jfs_dev_block *d_blocks, int nblk, in
     hipLaunchKernelGGL(jfs::lz4e::lz4_encode_kernel, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, d_ret);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+#ifdef JFS_PROF
+extern "C" int jfs_eprof_read(unsigned long long *out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(jfs::lz4e::g_eprof), sizeof(unsigned long long) * 12) == hipSuccess ? 0 : -1;
+}
+extern "C" int jfs_eprof_reset() {
+    unsigned long long z[12] = {0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(jfs::lz4e::g_eprof), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
