@@ -178,6 +178,9 @@ __device__ __forceinline__ uint64_t ld64u(const gc_u8 *p) {
 #ifndef JFS_ZE_HASH
 #define JFS_ZE_HASH 4  // bytes hashed for match candidates (libzstd level 1: 6)
 #endif
+#ifndef JFS_ZE_PSEARCH
+#define JFS_ZE_PSEARCH 1  // lane-parallel search (the serial loop's parse, 64 positions per step)
+#endif
 #ifndef JFS_ZE_REP
 #define JFS_ZE_REP 1   // try the repeat offset one byte ahead first (zstd_fast)
 #endif
@@ -748,6 +751,76 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(const jfs_dev_block *__
                 // 6-byte hash candidate (level 1: minMatch 6) within the window
                 int64_t cand;
                 uint32_t ofv = 0;  // Offset_Value: 1 = repeat offset 1, else offset + 3
+#if JFS_ZE_PSEARCH
+                // Lane-parallel search: lane j takes the j-th next position of
+                // the miss schedule and makes both checks of the serial loop
+                // there (repeat offset one byte ahead, then the hash candidate);
+                // the first lane with a match ends the search.  Table entries
+                // are read before any insert of the batch, which is the serial
+                // order while no two positions share a hash: the batch is cut
+                // at the first lane of a shared hash (tagged write + read-back),
+                // so the parse is the serial loop's exactly.
+                {
+                    bool done = false;
+                    for (;;) {
+                        const uint32_t st = 1u + ((miss + (uint32_t)l) >> 6);
+                        const uint32_t inc = dpp_scan_add(st);
+                        const int64_t P = ip + (int64_t)(inc - st);
+                        const uint64_t onm = __ballot(P + 8 <= be);
+                        const int nl = ~onm ? (int)__builtin_ctzll(~onm) : 64;
+                        if (nl == 0) { done = true; break; }
+                        const bool on = l < nl;
+                        bool rep = false;
+                        uint64_t v = 0;
+                        uint32_t h = 0, E = 0;
+                        if (on) {
+                            const int64_t rp = P + 1;
+                            rep = JFS_ZE_REP && rep0 <= rp && ld32u(src + rp) == ld32u(src + rp - rep0);
+                            v = ld64u(src + P);
+                            h = JFS_ZE_HASH == 6 ? hash6(v) : hash4((uint32_t)v);
+                            E = s.table[h];
+                        }
+                        const uint32_t tag = 0xFFFFFF00u | (uint32_t)l;  // never a position (inputs < 2 GiB)
+                        if (on) s.table[h] = tag;
+                        __builtin_amdgcn_wave_barrier();
+                        uint32_t cm = 64u;
+                        if (on) {
+                            const uint32_t t = s.table[h];
+                            if (t != tag) cm = umin32((uint32_t)l, t & 0xFFu);
+                        }
+                        const int ncut = (int)dwave_min(cm) + 1;
+                        const int nb = ncut < nl ? ncut : nl;  // lanes [0, nb) are exact
+                        if (on && l >= nb) s.table[h] = E;
+                        const int64_t hc = (int64_t)E;
+                        bool hit = l < nb && !rep && hc < P && P - hc <= WMAX;
+                        if (__ballot(hit)) {
+                            if (hit) hit = ld32u(src + hc) == (uint32_t)v;
+                        }
+                        const bool got = l < nb && (rep || hit);
+                        const uint64_t gm = __ballot(got);
+                        const int jm = gm ? (int)__builtin_ctzll(gm) : 64;
+                        // inserts: every position before jm, and jm itself unless its repeat check hit
+                        if (l < nb) s.table[h] = (l < jm || (l == jm && !rep)) ? (uint32_t)P : E;
+                        __builtin_amdgcn_wave_barrier();
+                        if (gm) {
+                            const int64_t pj = ip + (int64_t)readlane(inc - st, jm);
+                            if (readlane(rep ? 1u : 0u, jm)) {
+                                ip = pj + 1;
+                                cand = ip - rep0;
+                                ofv = 1;
+                            } else {
+                                ip = pj;
+                                cand = (int64_t)readlane(E, jm);
+                            }
+                            break;
+                        }
+                        ip += (int64_t)readlane(inc, nb - 1);
+                        miss += (uint32_t)nb;
+                    }
+                    if (done) break;
+                }
+                {
+#else
                 const int64_t rp = ip + 1;
                 if (JFS_ZE_REP && rep0 <= rp && ld32u(src + rp) == ld32u(src + rp - rep0)) {
                     cand = rp - rep0;
@@ -764,6 +837,7 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(const jfs_dev_block *__
                         ip += 1 + (miss++ >> 6);
                         continue;
                     }
+#endif
                 }
                 miss = 0;
                 // forward extension from +4, 64 bytes per step, up to the block end
