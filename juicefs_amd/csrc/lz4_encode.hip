@@ -218,7 +218,8 @@ __device__ __forceinline__ void put_len(Smem &s, Enc &e, uint32_t len) {
 }
 
 // copy literals src[from, from+len) into the output
-__device__ __forceinline__ void put_lits(Smem &s, Enc &e, int64_t from, int64_t len, int64_t keep_from) {
+__device__ __forceinline__ void put_lits(Smem &s, Enc &e, int64_t from, int64_t len, int64_t keep_from,
+                                         int32_t pre = -1) {
     const int l = lane_id();
     for (int64_t k = 0; k < len; k += 64) {
         maybe_flush(s, e, keep_from);
@@ -230,7 +231,7 @@ __device__ __forceinline__ void put_lits(Smem &s, Enc &e, int64_t from, int64_t 
             oflush2(s, e, to);
         }
         int64_t i = k + l;
-        if (i < len) s.ob[obidx(e, e.op + l)] = e.src[from + i];
+        if (i < len) s.ob[obidx(e, e.op + l)] = (k == 0 && pre >= 0) ? (uint8_t)pre : e.src[from + i];
         e.op += (len - k < 64 ? len - k : 64);
     }
 }
@@ -404,18 +405,36 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(const jfs_dev_block *__r
                 EP(0);
                 if (last) break;
                 EPC(8);
-                // ---- catch up (backwards, 64 bytes per step)
+                // One HBM round trip for the first 64 bytes of the three
+                // byte-parallel phases: catch-up (before ip / match), literals
+                // (from anchor) and the forward extension (from ip+4 / match+4;
+                // it does not depend on the catch-up: the match end is absolute).
+                int32_t lit_pre = -1;
+                int64_t xend;   // ip-side end of the match (first differing byte or matchlimit)
+                bool xmore;     // the first 64 extension bytes all matched
                 {
                     int64_t lim = ip - anchor;
                     if (match < lim) lim = match;
-                    int64_t back = 0;
-                    while (back < lim) {
-                        int64_t k = back + 1 + l;
-                        bool eq = k <= lim && src[ip - k] == src[match - k];
-                        uint64_t ne = ~__ballot(eq);
-                        int run = ne ? (int)__builtin_ctzll(ne) : 64;
+                    const int64_t kk = 1 + l, ax = ip + 4 + l, dlt = ip - match;
+                    uint32_t ca = 0, cb = 1, xa = 0, xb = 1;
+                    if (kk <= lim) { ca = src[ip - kk]; cb = src[match - kk]; }
+                    if (l < ip - anchor) lit_pre = src[anchor + l];
+                    if (ax < matchlimit) { xa = src[ax]; xb = src[ax - dlt]; }
+                    const uint64_t xne = ~__ballot(ax < matchlimit && xa == xb);
+                    const int xr = xne ? (int)__builtin_ctzll(xne) : 64;
+                    xend = ip + 4 + xr;
+                    xmore = xr == 64;
+                    // ---- catch up (backwards, 64 bytes per step)
+                    const uint64_t cne = ~__ballot(kk <= lim && ca == cb);
+                    int64_t back = cne ? (int)__builtin_ctzll(cne) : 64;
+                    bool cmore = back == 64;
+                    while (cmore && back < lim) {
+                        const int64_t k = back + 1 + l;
+                        const bool eq = k <= lim && src[ip - k] == src[match - k];
+                        const uint64_t ne = ~__ballot(eq);
+                        const int run = ne ? (int)__builtin_ctzll(ne) : 64;
                         back += run;
-                        if (run < 64) break;
+                        cmore = run == 64;
                     }
                     if (back > lim) back = lim;
                     ip -= back;
@@ -430,25 +449,25 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(const jfs_dev_block *__r
                     e.op++;  // token slot
                     if (lit >= 15) { token = 15u << 4; put_len(s, e, (uint32_t)(lit - 15)); }
                     else token = (uint32_t)lit << 4;
-                    put_lits(s, e, anchor, lit, tp);
+                    put_lits(s, e, anchor, lit, tp, lit_pre);
                 }
                 EP(3);
                 for (;;) {  // next_match
                     uint32_t off = (uint32_t)(ip - match);
                     put1(s, e, off & 255);
                     put1(s, e, off >> 8);
-                    // match length: count equal bytes from ip+4 / match+4 up to matchlimit
-                    int64_t a0 = ip + 4, b0 = match + 4;
-                    int64_t mc = 0;
-                    for (;;) {
-                        int64_t a = a0 + mc + l;
-                        bool eq = a < matchlimit && src[a] == src[b0 + mc + l];
-                        uint64_t ne = ~__ballot(eq);
-                        int run = ne ? (int)__builtin_ctzll(ne) : 64;
-                        mc += run;
-                        if (run < 64) break;
+                    // match length: equal bytes from ip+4 / match+4 up to matchlimit
+                    // (the first 64 were compared when the match was found)
+                    while (xmore) {
+                        const int64_t a = xend + l;
+                        const bool eq = a < matchlimit && src[a] == src[a - (int64_t)off];
+                        const uint64_t ne = ~__ballot(eq);
+                        const int run = ne ? (int)__builtin_ctzll(ne) : 64;
+                        xend += run;
+                        xmore = run == 64;
                     }
-                    ip = a0 + mc;
+                    const int64_t mc = xend - (ip + 4);
+                    ip = xend;
                     if (mc >= 15) {
                         token += 15;
                         put_len(s, e, (uint32_t)(mc - 15));
@@ -477,8 +496,15 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(const jfs_dev_block *__r
                     const uint32_t mi = u16 ? ent : (ent & e.pmask);
                     tput(s, e, h, (uint32_t)ip, (uint32_t)vi, u16);
                     bool rm = (u16 || (int64_t)mi + 65535 >= ip) && may_match(e, ent, (uint32_t)vi, u16);
-                    if (rm) {
+                    if (rm) {  // the 4-byte check and the first 64 extension bytes in one round trip
+                        const int64_t ax = ip + 4 + l, dlt = ip - (int64_t)mi;
+                        uint32_t xa = 0, xb = 1;
+                        if (ax < matchlimit) { xa = src[ax]; xb = src[ax - dlt]; }
                         rm = src32(s, e, mi) == (uint32_t)vi;
+                        const uint64_t xne = ~__ballot(ax < matchlimit && xa == xb);
+                        const int xr = xne ? (int)__builtin_ctzll(xne) : 64;
+                        xend = ip + 4 + xr;
+                        xmore = xr == 64;
                     }
                     EP(6);
                     if (rm) {
