@@ -840,29 +840,45 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(const jfs_dev_block *__
 #endif
                 }
                 miss = 0;
-                // forward extension from +4, 64 bytes per step, up to the block end
+                // forward extension from +4 (64 bytes per step, up to the block
+                // end) and backward catch-up (new offsets only): the first step
+                // of both is loaded in one HBM round trip
                 int64_t ml = 4;
-                for (;;) {
-                    const int64_t a = ip + ml + l;
-                    const bool eq = a < be && src[a] == src[cand + ml + l];
-                    const uint64_t ne = ~__ballot(eq);
+                int64_t lim = 0;
+                if (ofv == 0) {
+                    lim = ip - anchor;
+                    if (cand < lim) lim = cand;
+                }
+                const int64_t kk = 1 + l, a0 = ip + 4 + l;
+                uint32_t xa = 0, xb = 1, ca = 0, cb = 1;
+                if (a0 < be) { xa = src[a0]; xb = src[cand + 4 + l]; }
+                if (kk <= lim) { ca = src[ip - kk]; cb = src[cand - kk]; }
+                {
+                    const uint64_t ne = ~__ballot(a0 < be && xa == xb);
                     const int run = ne ? (int)__builtin_ctzll(ne) : 64;
                     ml += run;
-                    if (run < 64) break;
+                    bool more = run == 64;
+                    while (more) {
+                        const int64_t a = ip + ml + l;
+                        const bool eq = a < be && src[a] == src[cand + ml + l];
+                        const uint64_t ne2 = ~__ballot(eq);
+                        const int r2 = ne2 ? (int)__builtin_ctzll(ne2) : 64;
+                        ml += r2;
+                        more = r2 == 64;
+                    }
                 }
-                // backward catch-up into the pending literals (new offsets only)
                 int64_t m0 = cand;
                 if (ofv == 0) {
-                    int64_t lim = ip - anchor;
-                    if (m0 < lim) lim = m0;
-                    int64_t back = 0;
-                    while (back < lim) {
+                    const uint64_t cne = ~__ballot(kk <= lim && ca == cb);
+                    int64_t back = cne ? (int)__builtin_ctzll(cne) : 64;
+                    bool cmore = back == 64;
+                    while (cmore && back < lim) {
                         const int64_t k = back + 1 + l;
                         const bool eq = k <= lim && src[ip - k] == src[m0 - k];
                         const uint64_t ne = ~__ballot(eq);
                         const int run = ne ? (int)__builtin_ctzll(ne) : 64;
                         back += run;
-                        if (run < 64) break;
+                        cmore = run == 64;
                     }
                     if (back > lim) back = lim;
                     ip -= back;
