@@ -61,6 +61,9 @@ constexpr int RMASK = R - 1;
 #ifndef JFS_LZ4_NEARSER
 #define JFS_LZ4_NEARSER 1  // near matches: one lane-parallel round, the rest by the whole wave in order
 #endif
+#ifndef JFS_LZ4_LITDIRECT
+#define JFS_LZ4_LITDIRECT 1  // literal runs >= 2R copied HBM to HBM (incompressible data)
+#endif
 #ifndef JFS_LZ4_LITSER
 #define JFS_LZ4_LITSER 0  // 1: literal runs take one 16-byte lane step, longer runs by the whole wave (measured: no gain)
 #endif
@@ -346,8 +349,55 @@ __device__ __forceinline__ void need_flushed(Ctx &c, int32_t lim) {
 // ---------------------------------------------------------------------------
 // whole-wave copies (serial path and long tokens)
 // ---------------------------------------------------------------------------
+// Long literal runs (incompressible data: a 4 MiB block is one run) go HBM to
+// HBM: the ring is flushed up to op, the run except its last R bytes is
+// copied with 16-byte stores (1 KiB per wave step, 4 steps in flight), and
+// the last R bytes go through the ring as usual, so every later source inside
+// the ring's reach finds its bytes there and older ones are read from HBM
+// (F advanced; far reads wait for these stores through Fw).
+constexpr int32_t LIT_DIRECT = 2 * R;
+__device__ __forceinline__ void direct_lit(Smem &s, Ctx &c, int32_t srcpos, int32_t op, int32_t body) {
+    const int l = lane_id();
+    flush(s, c, op);
+    const gc_u8 *sp = c.src + srcpos - op;  // sp[x] = source byte of output x
+    int32_t x = op;
+    const int32_t ha = (int32_t)((16u - (((uint32_t)(uintptr_t)(c.dst + x)) & 15u)) & 15u);
+    if (l < ha) c.dst[x + l] = sp[x + l];
+    x += ha;
+    for (; x + 4096 <= body; x += 4096) {
+        u32x4 v[4];
+        uint32_t w[4];
+        const uint32_t sh = (uint32_t)((uintptr_t)(sp + x) & 3u);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uintptr_t a = (uintptr_t)(sp + x + 1024 * j + 16 * l) & ~(uintptr_t)3;
+            v[j] = *(const gc_x4 *)a;
+            w[j] = *(const gc_u32 *)(a + 16);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            uint4 o;
+            o.x = __builtin_amdgcn_alignbyte(v[j].y, v[j].x, sh);
+            o.y = __builtin_amdgcn_alignbyte(v[j].z, v[j].y, sh);
+            o.z = __builtin_amdgcn_alignbyte(v[j].w, v[j].z, sh);
+            o.w = __builtin_amdgcn_alignbyte(w[j], v[j].w, sh);
+            *(g_u4 *)(c.dst + x + 1024 * j + 16 * l) = o;
+        }
+    }
+    for (; x < body; x += 64)
+        if (x + l < body) c.dst[x + l] = sp[x + l];
+    c.F = body;
+}
+
 __device__ __forceinline__ void coop_lit(Smem &s, Ctx &c, int32_t srcpos, int32_t op, int32_t len) {
     const int l = lane_id();
+    if (JFS_LZ4_LITDIRECT && len >= LIT_DIRECT) {
+        const int32_t body = op + len - R;
+        direct_lit(s, c, srcpos, op, body);
+        srcpos += body - op;
+        len -= body - op;
+        op = body;
+    }
     for (int32_t k = 0; k < len; k += 64) {
         if (op + k - c.F >= FLUSH_T) flush_to_line(s, c, op + k);
         int32_t i = k + l;
@@ -355,8 +405,52 @@ __device__ __forceinline__ void coop_lit(Smem &s, Ctx &c, int32_t srcpos, int32_
     }
 }
 
+// Long matches whose offset divides 16 (runs of one byte or of a 2/4/8/16-byte
+// pattern: zero-filled regions) are pure stores: every 16-byte-aligned chunk
+// of the run holds the same 16 bytes.  The run except its last R bytes is
+// written straight to HBM (4 KiB per wave step), the 16 bytes before the tail
+// are put in the ring (the tail's period source) and the tail goes through
+// the ring as usual.  Returns the output position where the ring part starts.
+__device__ __forceinline__ int32_t direct_fill(Smem &s, Ctx &c, int32_t op, int32_t off, int32_t len) {
+    const int l = lane_id();
+    const int32_t body = op + len - R;
+    flush(s, c, op);
+    const uint32_t amis = (uint32_t)(uintptr_t)(c.dst + op) & 15u;
+    const int32_t x0 = op + (int32_t)((16u - amis) & 15u);  // first 16-byte aligned output position
+    // byte b of every aligned chunk = P[(x0 - op + b) mod off], P = the off bytes before op (in the ring)
+    uint32_t q[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+        const uint32_t v = s.ring[slot(c, op - off + (int32_t)(((uint32_t)(x0 - op) + (uint32_t)b) % (uint32_t)off))];
+        q[b >> 2] |= v << (8 * (b & 3));
+    }
+    const uint4 chunk = make_uint4(q[0], q[1], q[2], q[3]);
+    if (op + l < x0) c.dst[op + l] = s.ring[slot(c, op - off + (l % off))];  // head (< 16 bytes)
+    int32_t x = x0;
+    for (; x + 4096 <= body; x += 4096) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) *(g_u4 *)(c.dst + x + 1024 * j + 16 * l) = chunk;
+    }
+    for (; x + 16 <= body; x += 1024)
+        if (x + 16 * l + 16 <= body) *(g_u4 *)(c.dst + x + 16 * l) = chunk;
+    const int32_t xe = x0 + ((body - x0) & ~15);  // end of the aligned chunks written
+    if (xe + l < body) c.dst[xe + l] = (uint8_t)(q[l >> 2 & 3] >> (8 * (l & 3)));  // (< 16 bytes, same phase)
+    // the ring gets the 16 bytes before `body` (the tail's source period)
+    if (l < 16) {
+        const int32_t y = body - 16 + l;
+        s.ring[slot(c, y)] = s.ring[slot(c, op - off + (int32_t)((uint32_t)(y - op) % (uint32_t)off))];
+    }
+    c.F = body;
+    return body;
+}
+
 __device__ __forceinline__ void coop_match(Smem &s, Ctx &c, int32_t op, int32_t off, int32_t len) {
     const int l = lane_id();
+    if (JFS_LZ4_LITDIRECT && len >= LIT_DIRECT && off > 0 && off <= 16 && (16 % off) == 0) {
+        const int32_t b = direct_fill(s, c, op, off, len);
+        len -= b - op;
+        op = b;
+    }
     int32_t m = 0, step = 0;
     if (off > 0 && off < 64) { m = l % off; step = 64 % off; }
     for (int32_t k = 0; k < len; k += 64) {

@@ -336,3 +336,63 @@ def test_lz4_encode_long_literal_runs(gpu, oracle):
     for s, (d, _), (n, err) in zip(srcs, pairs, res):
         m, ref = oracle.lz4_compress(s)
         assert err is None and n == m and bytes(d[:n]) == ref
+
+
+def test_lz4_long_literal_runs_then_far_and_near_matches(gpu, oracle):
+    """Literal runs >= 8 KiB take the HBM-to-HBM path (lz4_decode.hip
+    direct_lit); later matches must find the run's bytes in the ring (last 4 KiB)
+    and in HBM (older), right after the run and far behind it; short
+    destinations must still fail exactly where liblz4 fails."""
+    rng = np.random.default_rng(77)
+    c = C.LZ4()
+    pairs, want = [], []
+    for k, run in enumerate((8192, 8193, 12345, 40000, 65536, 200000)):
+        r = rng.integers(0, 256, run, dtype=np.uint8).tobytes()
+        text = gen_block("T", 300 + k, 3000)
+        # copies out of the run: just behind its end (ring), mid-run and near its start (HBM, < 64 KiB back)
+        src = (r + r[-600:-100] + text + r[run // 2:run // 2 + 700] + text[:900] + r[max(0, run - 60000):][:1500]
+               + gen_block("R", 400 + k, 9000 + 37 * k) + text)
+        _, comp = oracle.lz4_compress(src)
+        n = len(src)
+        for cap in (n, n + 5):
+            pairs.append((bytearray(cap), comp))
+            want.append((n, src))
+        rr, _ = oracle.lz4_decompress(comp, n - 1)
+        pairs.append((bytearray(n - 1), comp))
+        want.append((rr, None))
+    res = c.DecompressBatch(pairs)
+    for (dst, comp), (n_exp, src), (n, err) in zip(pairs, want, res):
+        if n_exp >= 0:
+            assert err is None and n == n_exp
+            assert bytes(dst[:n]) == src
+        else:
+            assert err is not None and n == n_exp
+
+
+def test_lz4_long_periodic_matches(gpu, oracle):
+    """Long matches with offsets 1/2/4/8/16 are written as pure stores
+    (lz4_decode.hip direct_fill); other offsets take the ring path.  Text
+    around the runs makes later tokens read both the run's tail (ring) and
+    its body (HBM); short destinations fail where liblz4 fails."""
+    c = C.LZ4()
+    pairs, want = [], []
+    for k, (period, reps) in enumerate(((1, 20000), (2, 9000), (4, 5000), (8, 3000), (16, 1500), (3, 7000),
+                                        (16, 300), (1, 70000))):
+        pat = gen_block("R", 500 + k, period)
+        text = gen_block("T", 600 + k, 2500)
+        src = text[:700] + pat * reps + text + (pat * reps)[:5000 + 13 * k] + text[1000:2400] + pat * 40 + text[:300]
+        _, comp = oracle.lz4_compress(src)
+        n = len(src)
+        for cap in (n, n + 9):
+            pairs.append((bytearray(cap), comp))
+            want.append((n, src))
+        rr, _ = oracle.lz4_decompress(comp, n - 3)
+        pairs.append((bytearray(n - 3), comp))
+        want.append((rr, None))
+    res = c.DecompressBatch(pairs)
+    for (dst, comp), (n_exp, src), (n, err) in zip(pairs, want, res):
+        if n_exp >= 0:
+            assert err is None and n == n_exp
+            assert bytes(dst[:n]) == src
+        else:
+            assert err is not None and n == n_exp
