@@ -1362,7 +1362,7 @@ __device__ __forceinline__ void seq_periods(SeqSmem &sm, const GBlk &d, bool min
 __device__ __forceinline__ void seq_group(SeqSmem &sm, int gn, const gc_u16 *tabs, uint32_t *e0, uint32_t *e1,
                                           uint32_t *e2) {
     const int l = lane_id();
-    uint64_t zt = ZP_NOW();
+    [[maybe_unused]] uint64_t zt = ZP_NOW();
     ZS_ADD(5, 1);
     __builtin_amdgcn_wave_barrier();
     wait_vm();  // table cells written in phase A are complete before they are gathered
@@ -1534,7 +1534,7 @@ __global__ __launch_bounds__(64) void zseq_kernel(const jfs_dev_block *__restric
     for (int i = l; i < 53; i += 64) sm.lut_ml[i] = ML_BASE[i] | ((uint32_t)ML_BITS[i] << 24);
     int gn = 0;
     uint32_t e0 = 1, e1 = 4, e2 = 8;  // repeat offsets carried through phase C (reset at each frame)
-    uint64_t za = ZP_NOW();
+    [[maybe_unused]] uint64_t za = ZP_NOW();
     for (int f = 0; f < ZSEQ_INPUTS; ++f) {
         const int bi = blockIdx.x * ZSEQ_INPUTS + f;
         if (bi >= nblk) break;
