@@ -300,6 +300,13 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(const jfs_dev_block *__r
                 int64_t match;
                 // ---- search (skip schedule: step = searchMatchNb++ >> 6)
                 bool last = false;
+                // bytes for the match's catch-up / literals / extension, loaded
+                // together with the candidate checks for the first lane whose
+                // check bits pass (nearly always the match): one round trip less
+                bool pre_ok = false;
+                int64_t pre_ip = -1, pre_m = -1;
+                uint32_t p_ca = 0, p_cb = 1, p_xa = 0, p_xb = 1;
+                int32_t p_lit = -1;
 #if JFS_LZ4E_PSEARCH
                 // Lane-parallel: lane j takes the j-th next position of the
                 // schedule; every lane reads its table entry before any insert
@@ -353,8 +360,19 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(const jfs_dev_block *__r
                     }
                     const int64_t cand = u16 ? (int64_t)E : (int64_t)(E & e.pmask);
                     bool pass = l < nb && (u16 || cand + 65535 >= P) && may_match(e, E, cv, u16);
-                    if (__ballot(pass)) {
+                    const uint64_t pm0 = __ballot(pass);
+                    if (pm0) {
                         EPC(9);
+                        const int j0 = (int)__builtin_ctzll(pm0);
+                        pre_ip = pk + (int64_t)readlane(inc - (uint32_t)sk, j0);
+                        pre_m = (int64_t)readlane((uint32_t)cand, j0);
+                        int64_t lim = pre_ip - anchor;
+                        if (pre_m < lim) lim = pre_m;
+                        const int64_t kk = 1 + l, ax = pre_ip + 4 + l, dlt = pre_ip - pre_m;
+                        p_ca = 0; p_cb = 1; p_xa = 0; p_xb = 1; p_lit = -1;
+                        if (kk <= lim) { p_ca = src[pre_ip - kk]; p_cb = src[pre_m - kk]; }
+                        if (l < pre_ip - anchor) p_lit = src[anchor + l];
+                        if (ax < matchlimit) { p_xa = src[ax]; p_xb = src[ax - dlt]; }
                         if (pass) pass = src32(s, e, cand) == cv;
                     }
                     const uint64_t hm = __ballot(pass);
@@ -368,6 +386,7 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(const jfs_dev_block *__r
                     if (hm) {
                         ip = pk + (int64_t)readlane(inc - (uint32_t)sk, jm);
                         match = (int64_t)readlane((uint32_t)cand, jm);
+                        pre_ok = ip == pre_ip && match == pre_m;
                         break;
                     }
                     if (nb == nl && endm && jend <= jspan) { last = true; break; }  // the schedule passed mflimit
@@ -416,10 +435,14 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(const jfs_dev_block *__r
                     int64_t lim = ip - anchor;
                     if (match < lim) lim = match;
                     const int64_t kk = 1 + l, ax = ip + 4 + l, dlt = ip - match;
-                    uint32_t ca = 0, cb = 1, xa = 0, xb = 1;
-                    if (kk <= lim) { ca = src[ip - kk]; cb = src[match - kk]; }
-                    if (l < ip - anchor) lit_pre = src[anchor + l];
-                    if (ax < matchlimit) { xa = src[ax]; xb = src[ax - dlt]; }
+                    uint32_t ca = p_ca, cb = p_cb, xa = p_xa, xb = p_xb;
+                    lit_pre = p_lit;
+                    if (!pre_ok) {
+                        ca = 0; cb = 1; xa = 0; xb = 1; lit_pre = -1;
+                        if (kk <= lim) { ca = src[ip - kk]; cb = src[match - kk]; }
+                        if (l < ip - anchor) lit_pre = src[anchor + l];
+                        if (ax < matchlimit) { xa = src[ax]; xb = src[ax - dlt]; }
+                    }
                     const uint64_t xne = ~__ballot(ax < matchlimit && xa == xb);
                     const int xr = xne ? (int)__builtin_ctzll(xne) : 64;
                     xend = ip + 4 + xr;
