@@ -295,7 +295,8 @@ def oneshot_concurrency(comp_blocks, raw_blocks, U, n_dec=200, n_enc=20, rounds=
         ddst[t] == raw_blocks[(t + r) % nc]
     edst = [bytearray(bound) for _ in range(n_enc)]
     enc = lambda t, r: c.Compress(edst[t], raw_blocks[(t + r) % nc])[0] > 0
-    run(4, 1, dec)  # warm the coalescer and staging
+    run(n_dec, 1, dec)  # warm the coalescer and its staging (pinned once, then reused)
+    run(n_enc, 1, enc)
     out = {"decompress_lone": run(1, 5, dec), "compress_lone": run(1, 2, enc),
            f"decompress_{n_dec}_concurrent": run(n_dec, rounds, dec),
            f"compress_{n_enc}_concurrent": run(n_enc, 1, enc),

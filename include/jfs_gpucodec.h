@@ -99,9 +99,15 @@ int64_t jfs_decompress_batch(int algo, int nblk, const jfs_iov *iov, int64_t *ou
 
 /* ---- Device-resident surface (inputs/outputs already in HBM) ------------
  * One descriptor per block; all pointers are device pointers on the calling
- * thread's current device, and `stream` (0 = the null stream) belongs to it.
- * ret[i] is written with the single-block result.  The LZ4 calls and the Zstd
- * decompress call are asynchronous on `stream` (they only enqueue work);
+ * thread's current device, which must be a device this library selected
+ * (gfx950, in JFS_GPU_DEVICES; else JFS_ERR_NO_DEVICE), and `stream`
+ * (0 = the null stream) belongs to it.  ret[i] is written with the
+ * single-block result -- exactly the value jfs_decompress/jfs_compress's
+ * codec call would produce for that block (see each call below); no other
+ * value is ever written.  The LZ4 calls only enqueue work on `stream`.
+ * jfs_zstd_decompress_device enqueues too, but first waits on the host for
+ * its header-scan kernels (microseconds after the work already on `stream`)
+ * so it can size its scratch: it never asks the caller to resubmit.
  * jfs_zstd_compress_device is host-synchronous (per-device scratch, locked). */
 typedef struct jfs_dev_block {
     const uint8_t *src;
@@ -110,8 +116,15 @@ typedef struct jfs_dev_block {
     int32_t dst_cap;
 } jfs_dev_block;
 
+/* ret[i] = LZ4_decompress_safe(src, dst, src_len, dst_cap): bytes written, or
+ * its negative error value. */
 int64_t jfs_lz4_decompress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream);
+/* ret[i] = LZ4_compress_default(src, dst, src_len, dst_cap): compressed size,
+ * or 0 when it does not fit dst_cap. */
 int64_t jfs_lz4_compress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream);
+/* ret[i]: decoded bytes, -1 malformed frame (ZSTD error), -2 output larger
+ * than dst_cap ("Destination buffer is too small"), -3 src size incorrect
+ * (truncated / trailing bytes). */
 int64_t jfs_zstd_decompress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream);
 /* Zstd frame per block; ret[i] = frame size, or -2 when dst_cap < CompressBound(src_len).
  * Synchronous with respect to `stream` (it uses per-device scratch). */
@@ -135,8 +148,8 @@ int64_t jfs_crc32c_device(const jfs_dev_block *d_blocks, int nblk, int32_t seg_b
  * additional data.  Seal (Encrypt :226-257): dst = ciphertext || tag,
  * ret = src_len + 16 (dst_cap must hold it).  Open (Decrypt :259-284):
  * src = ciphertext || tag, dst = plaintext, ret = src_len - 16, or -1 when the
- * tag does not verify ("cipher: message authentication failed"; dst is then
- * not to be used).  ret = -2 for a bad descriptor.  The random key/nonce, the
+ * tag does not verify ("cipher: message authentication failed"; dst[0, n)
+ * is then zeroed, as Go's gcm.Open clears its output).  ret = -2 for a bad descriptor.  The random key/nonce, the
  * RSA wrap of the key and the object header (:230-252) are the caller's.
  * Asynchronous on `stream`; key and nonce are device pointers. */
 typedef struct jfs_aead_block {
@@ -202,11 +215,23 @@ typedef struct jfs_op_stats {
     uint64_t bytes_out; /* output bytes of host-path blocks that succeeded */
     uint64_t errors;    /* host-path blocks that returned an error code */
     uint64_t nanos;     /* wall time spent inside host-path calls */
+    uint64_t batches;   /* device batches the host path ran (coalesced one-call
+                           batches, or per-device parts of a jfs_*_batch call) */
 } jfs_op_stats;
 #define JFS_STATS_N 6
 /* Copy min(n, JFS_STATS_N) entries to out; returns JFS_STATS_N. */
 int jfs_stats(jfs_op_stats *out, int n);
-void jfs_stats_reset(void);
+void jfs_stats_reset(void);  /* also zeroes the per-device counters below */
+/* Per-device host-path counters (where the round-robin deal put
+ * the blocks): one entry per usable device, in jfs_device_count() order. */
+typedef struct jfs_device_stat {
+    int32_t device;   /* HIP device ordinal */
+    int32_t pad_;
+    uint64_t batches; /* device batches run */
+    uint64_t blocks;  /* blocks in them */
+} jfs_device_stat;
+/* Copy min(n, devices) entries to out; returns the number of devices. */
+int jfs_device_stats(jfs_device_stat *out, int n);
 /* Free the batch path's pinned host + HBM staging now (it is also released
  * after JFS_STAGING_IDLE_MS, default 15000, of no batch activity). */
 void jfs_release_staging(void);

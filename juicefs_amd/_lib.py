@@ -32,7 +32,7 @@ EXPORTS = [
     "jfs_zstd_decompress_device", "jfs_zstd_compress_device", "jfs_device_count", "jfs_version", "jfs_gen_blocks_device",
     "jfs_gen_block_host", "jfs_release_staging", "jfs_crc32c_device", "jfs_aes256gcm_seal_device",
     "jfs_aes256gcm_open_device", "jfs_lz4_compress_seal_device", "jfs_open_lz4_decompress_device",
-    "jfs_gpu_mode", "jfs_stats", "jfs_stats_reset",
+    "jfs_gpu_mode", "jfs_stats", "jfs_stats_reset", "jfs_device_stats",
 ]
 
 MODE_OFF, MODE_AUTO, MODE_FORCE = 0, 1, 2
@@ -45,7 +45,13 @@ class JfsIov(ctypes.Structure):
 
 
 class JfsOpStats(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_uint64) for n in ("calls", "blocks", "bytes_in", "bytes_out", "errors", "nanos")]
+    _fields_ = [(n, ctypes.c_uint64) for n in ("calls", "blocks", "bytes_in", "bytes_out", "errors", "nanos",
+                                               "batches")]
+
+
+class JfsDeviceStat(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("pad_", ctypes.c_int32), ("batches", ctypes.c_uint64),
+                ("blocks", ctypes.c_uint64)]
 
 
 class JfsDevBlock(ctypes.Structure):
@@ -97,6 +103,8 @@ def load() -> ctypes.CDLL:
     lib.jfs_gpu_mode.restype = ctypes.c_int
     lib.jfs_stats.argtypes = [ctypes.POINTER(JfsOpStats), ctypes.c_int]
     lib.jfs_stats.restype = ctypes.c_int
+    lib.jfs_device_stats.argtypes = [ctypes.POINTER(JfsDeviceStat), ctypes.c_int]
+    lib.jfs_device_stats.restype = ctypes.c_int
     lib.jfs_stats_reset.argtypes = []
     lib.jfs_stats_reset.restype = None
     lib.jfs_version.argtypes = []

@@ -337,7 +337,18 @@ __global__ __launch_bounds__(LANES) void gcm_kernel(const jfs_aead_block *__rest
             uint32_t diff = 0;
             for (int k = 0; k < 16; k++) diff |= (uint32_t)src[n + k] ^ ((tag.w[k >> 2] >> (24 - 8 * (k & 3))) & 255u);
             ret[b] = diff ? -1 : (int32_t)n;
+            s.tag_ok = diff == 0;
         }
+    }
+    if (mode == 1) {
+        // Go's gcm.Open clears its output when the tag does not verify: no
+        // unauthenticated plaintext is left in dst (only the failure path pays)
+        __syncthreads();
+        if (!s.tag_ok)
+            for (int64_t i = t; i < nb; i += LANES) {
+                const int len = n - 16 * i < 16 ? (int)(n - 16 * i) : 16;
+                store_part(dst + 16 * i, make_uint4(0, 0, 0, 0), len, aligned);
+            }
     }
 }
 

@@ -8,10 +8,11 @@
 //
 // Concurrency model (pkg/chunk runs up to 20 Compress + 200 Decompress calls
 // at once, cmd/flags.go:133-139): single-block calls enqueue on a per-process
-// coalescer; one worker thread per device drains the queue, so calls that
-// arrive while a batch is running ride the next batch (no artificial delay).
-// Batches go host -> pinned staging -> HBM -> kernel -> HBM -> pinned -> host,
-// pipelined in chunks over two streams (run_batch).
+// coalescer; NLANE worker threads per device drain the queue, each gathering a
+// burst of calls (a short gather window, Gather below) into one batch, and a
+// device runs the next batch while the previous one is in flight (one lane of
+// staging and streams per worker).  Batches go host -> pinned staging -> HBM
+// -> kernel -> HBM -> pinned -> host, pipelined in chunks (run_batch).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -39,9 +40,9 @@ constexpr int64_t LZ4_MAX_INPUT = 0x7E000000;
 
 inline int64_t align16(int64_t x) { return (x + 15) & ~(int64_t)15; }
 
-// One pinned host + device staging area with its own kernel stream: chunk k
-// of a batch uses slot k % NSLOT, so chunk k+1's H2D and chunk k-1's D2H run
-// while chunk k's kernel runs (and kernels of neighbouring chunks overlap).
+// One pinned host + device staging area: chunk k of a batch uses slot
+// k % NSLOT, so chunk k+1's H2D and chunk k-1's D2H run while chunk k's
+// kernel runs.
 constexpr int NSLOT = 3;
 
 // Upper bound on one slot's staging (JFS_STAGING_MAX_MB; default none): a
@@ -55,7 +56,6 @@ int64_t staging_max_bytes() {
 }
 
 struct Slot {
-    hipStream_t st = nullptr;  // this slot's kernels
     hipEvent_t ev_in = nullptr, ev_k = nullptr, ev = nullptr;  // H2D done, kernel done, D2H done
     uint8_t *h = nullptr;
     int64_t h_cap = 0;
@@ -82,7 +82,10 @@ struct Slot {
     }
 
     bool ensure(int64_t bytes) {
-        const int64_t want = (bytes + (64ll << 20) - 1) & ~((64ll << 20) - 1);  // grow in 64 MiB steps
+        // grow to the next power of two (at least 64 MiB): pinning costs about
+        // 0.1 s per GiB, so a growing workload should re-pin rarely
+        int64_t want = 64ll << 20;
+        while (want < bytes) want <<= 1;
         if (bytes > staging_max_bytes()) return false;
         if (bytes > h_cap) {
             if (h) (void)hipHostFree(h);
@@ -106,16 +109,20 @@ struct Slot {
     }
 };
 
-struct DevCtx {
-    int id = -1;
-    std::mutex mu;  // serialises use of the staging slots below
+// Streams: a process gets GPU_MAX_HW_QUEUES (4 by default) hardware queues
+// per device, and work on two streams that share one runs in submission
+// order -- kernels "on different streams" then serialise (measured: five
+// streams of one 0.5 s kernel each take 1.0 s; scripts/stream_probe.py).  So
+// the library uses exactly four streams per device: one for every H2D copy,
+// one for every D2H copy (a D2H waiting for its kernel must not hold up the
+// next chunk's H2D), and one kernel stream per lane.
+// A lane is one staging pipeline (NSLOT slots + its kernel stream); a device
+// has NLANE of them, so a second batch (the coalescer's next one, or another
+// caller's jfs_*_batch) runs while the first is still in flight.
+struct Lane {
+    std::mutex mu;  // serialises use of this lane's slots
     Slot slot[NSLOT];
-    // All H2D copies go on s_in and all D2H copies on s_out, ordered by events:
-    // a D2H waiting for its kernel must not hold up the next chunk's H2D.
-    hipStream_t s_in = nullptr, s_out = nullptr;
-    uint8_t *d_vocab = nullptr;
-    std::atomic<int64_t> last_use_ms{0};  // staging janitor: release after an idle period
-
+    hipStream_t s_k = nullptr;  // this lane's kernels, in chunk order
     // free the pinned host and HBM staging (caller holds mu)
     void release_staging() {
         for (Slot &sl : slot) {
@@ -129,6 +136,37 @@ struct DevCtx {
             sl.h_cap = sl.d_cap = 0;
             sl.z_lit_cap = sl.z_items_cap = sl.z_tabs_cap = 0;
         }
+    }
+    bool holds_staging() const {
+        for (const Slot &sl : slot)
+            if (sl.h || sl.d || sl.z_items) return true;
+        return false;
+    }
+};
+constexpr int NLANE = 2;
+
+struct DevCtx {
+    int id = -1;
+    Lane lane[NLANE];
+    hipStream_t s_in = nullptr, s_out = nullptr;  // all H2D / all D2H copies of the device
+    std::atomic<unsigned> next_lane{0};
+    std::mutex vocab_mu;
+    uint8_t *d_vocab = nullptr;
+    std::atomic<int64_t> last_use_ms{0};  // staging janitor: release after an idle period
+    std::atomic<uint64_t> batches{0}, blocks{0};  // per-device counters (jfs_device_stats)
+
+    // a lane for a batch call: a free one if any, else wait for one
+    Lane &acquire_lane(std::unique_lock<std::mutex> &lk) {
+        for (int k = 0; k < NLANE; k++) {
+            std::unique_lock<std::mutex> t(lane[k].mu, std::try_to_lock);
+            if (t.owns_lock()) {
+                lk = std::move(t);
+                return lane[k];
+            }
+        }
+        Lane &l = lane[next_lane.fetch_add(1) % NLANE];
+        lk = std::unique_lock<std::mutex>(l.mu);
+        return l;
     }
 };
 
@@ -177,7 +215,7 @@ uint64_t device_select_mask() {
 
 // per-(algo, dir) counters behind jfs_stats()
 struct OpStats {
-    std::atomic<uint64_t> calls{0}, blocks{0}, bytes_in{0}, bytes_out{0}, errors{0}, nanos{0};
+    std::atomic<uint64_t> calls{0}, blocks{0}, bytes_in{0}, bytes_out{0}, errors{0}, nanos{0}, batches{0};
 };
 OpStats g_stats[JFS_STATS_N];
 
@@ -232,11 +270,13 @@ void init_devices() {
         bool ok = true;
         ok = ok && hipStreamCreateWithFlags(&d->s_in, hipStreamNonBlocking) == hipSuccess;
         ok = ok && hipStreamCreateWithFlags(&d->s_out, hipStreamNonBlocking) == hipSuccess;
-        for (Slot &sl : d->slot) {
-            ok = ok && hipStreamCreateWithFlags(&sl.st, hipStreamNonBlocking) == hipSuccess;
-            ok = ok && hipEventCreateWithFlags(&sl.ev_in, hipEventDisableTiming) == hipSuccess;
-            ok = ok && hipEventCreateWithFlags(&sl.ev_k, hipEventDisableTiming) == hipSuccess;
-            ok = ok && hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming) == hipSuccess;
+        for (Lane &ln : d->lane) {
+            ok = ok && hipStreamCreateWithFlags(&ln.s_k, hipStreamNonBlocking) == hipSuccess;
+            for (Slot &sl : ln.slot) {
+                ok = ok && hipEventCreateWithFlags(&sl.ev_in, hipEventDisableTiming) == hipSuccess;
+                ok = ok && hipEventCreateWithFlags(&sl.ev_k, hipEventDisableTiming) == hipSuccess;
+                ok = ok && hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming) == hipSuccess;
+            }
         }
         if (!ok) {
             delete d;
@@ -267,19 +307,20 @@ int64_t staging_idle_ms() {
     return v;
 }
 
-void release_dev_staging(DevCtx *d) {
+void release_lane_staging(DevCtx *d, Lane &ln) {
     (void)hipSetDevice(d->id);  // janitor thread / explicit release: no caller device to keep
-    d->release_staging();
+    ln.release_staging();
 }
 
 // At exit the janitor must not call into a HIP runtime that is being torn
-// down: the handler raises g_exiting and then takes every device lock once,
+// down: the handler raises g_exiting and then takes every lane lock once,
 // which waits out a release already in progress.
 void on_exit_handler() {
     g_exiting = true;
-    for (DevCtx *d : g_devs) {
-        std::lock_guard<std::mutex> lk(d->mu);
-    }
+    for (DevCtx *d : g_devs)
+        for (Lane &ln : d->lane) {
+            std::lock_guard<std::mutex> lk(ln.mu);
+        }
 }
 
 void start_janitor() {
@@ -292,11 +333,11 @@ void start_janitor() {
                 std::this_thread::sleep_for(std::chrono::milliseconds(std::min<int64_t>(1000, staging_idle_ms())));
                 for (DevCtx *d : g_devs) {
                     if (steady_ms() - d->last_use_ms.load() < staging_idle_ms()) continue;
-                    std::unique_lock<std::mutex> lk(d->mu, std::try_to_lock);
-                    if (!lk.owns_lock() || g_exiting) continue;
-                    bool any = false;
-                    for (Slot &sl : d->slot) any |= sl.h != nullptr || sl.d != nullptr || sl.z_items != nullptr;
-                    if (any) release_dev_staging(d);
+                    for (Lane &ln : d->lane) {
+                        std::unique_lock<std::mutex> lk(ln.mu, std::try_to_lock);
+                        if (!lk.owns_lock() || g_exiting) continue;
+                        if (ln.holds_staging()) release_lane_staging(d, ln);
+                    }
                 }
             }
         }).detach();
@@ -304,6 +345,7 @@ void start_janitor() {
 }
 
 enum Dir { COMPRESS = 0, DECOMPRESS = 1 };
+constexpr int COMPRESS_DIR = COMPRESS, DECOMPRESS_DIR = DECOMPRESS;
 
 // Per-block result conversion from the kernel's raw value to the C-ABI value.
 // DataDog/zstd v1.5.6 decompressSizeHint: the first frame's content size if
@@ -417,18 +459,23 @@ int launch_kernel(int algo, int dir, const jfs_dev_block *d_desc, int nblk, int3
     return -1;
 }
 
-// Run blocks [0,nblk) of iov on one device; returns when every result is in
-// out[].  Blocks that the C-ABI answers without a kernel (empty input, noOp)
-// are handled by the caller.  The batch is cut into chunks of about
-// chunk_limit() staging bytes, pipelined over NSLOT (stream, pinned, HBM)
-// slots: host copy-in of chunk k (threads) | H2D k+1, kernel k, D2H k-1
-// (streams) | host copy-out of chunk k-NSLOT.
-int64_t run_batch(DevCtx *dev, int algo, int dir, int nblk, const jfs_iov *iov, int64_t *out) {
+// Run blocks [0,nblk) of iov on one device through one lane (the caller holds
+// ln.mu); returns when every result is in out[].  Blocks that the C-ABI
+// answers without a kernel (empty input, noOp) are handled by the caller.  The
+// batch is cut into chunks pipelined over the lane's NSLOT (stream, pinned,
+// HBM) slots: host copy-in of chunk k (threads) | H2D k+1, kernel k, D2H k-1
+// (streams) | host copy-out of chunk k-NSLOT.  A chunk holds at most
+// chunk_limit() staging bytes; the lane's kernels run in chunk order, so a
+// batch is not cut finer than that (a decode kernel over fewer blocks than
+// CUs lasts about one block's latency whatever its size).
+int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_iov *iov, int64_t *out) {
     if (nblk <= 0) return JFS_OK;
-    std::lock_guard<std::mutex> lk(dev->mu);
     DevGuard guard;
     (void)hipSetDevice(dev->id);
     dev->last_use_ms = steady_ms();
+    dev->batches.fetch_add(1, std::memory_order_relaxed);
+    dev->blocks.fetch_add((uint64_t)nblk, std::memory_order_relaxed);
+    if (OpStats *st = op_stats(algo, dir)) st->batches.fetch_add(1, std::memory_order_relaxed);
     start_janitor();
     struct Touch {  // the idle clock starts when the batch ends
         DevCtx *d;
@@ -478,7 +525,7 @@ int64_t run_batch(DevCtx *dev, int algo, int dir, int nblk, const jfs_iov *iov, 
                align16((int64_t)(c.e - c.s) * 4) + align16((int64_t)(c.e - c.s) * zib);
     };
     auto launch = [&](const Chunk &c) -> int64_t {
-        Slot &sl = dev->slot[c.slot];
+        Slot &sl = ln.slot[c.slot];
         if (!sl.ensure(chunk_bytes(c))) return JFS_ERR_NO_MEMORY;
         uint8_t *h_in, *h_out, *d_in, *d_out, *h_zi, *d_zi;
         jfs_dev_block *h_desc, *d_desc;
@@ -519,11 +566,11 @@ int64_t run_batch(DevCtx *dev, int algo, int dir, int nblk, const jfs_iov *iov, 
         if (zplan && hipMemcpyAsync(d_zi, h_zi, (size_t)(n * zib), hipMemcpyHostToDevice, dev->s_in) != hipSuccess)
             return JFS_ERR_HIP;
         if (hipEventRecord(sl.ev_in, dev->s_in) != hipSuccess) return JFS_ERR_HIP;
-        if (hipStreamWaitEvent(sl.st, sl.ev_in, 0) != hipSuccess) return JFS_ERR_HIP;
-        const int lk = zplan ? jfs_launch_zstd_decode_planned(d_desc, n, d_ret, d_zi, sl.z_lit, sl.z_tabs, sl.z_items, sl.st)
-                             : launch_kernel(algo, dir, d_desc, n, d_ret, sl.st);
+        if (hipStreamWaitEvent(ln.s_k, sl.ev_in, 0) != hipSuccess) return JFS_ERR_HIP;
+        const int lk = zplan ? jfs_launch_zstd_decode_planned(d_desc, n, d_ret, d_zi, sl.z_lit, sl.z_tabs, sl.z_items, ln.s_k)
+                             : launch_kernel(algo, dir, d_desc, n, d_ret, ln.s_k);
         if (lk != 0) return JFS_ERR_HIP;
-        if (hipEventRecord(sl.ev_k, sl.st) != hipSuccess) return JFS_ERR_HIP;
+        if (hipEventRecord(sl.ev_k, ln.s_k) != hipSuccess) return JFS_ERR_HIP;
         if (hipStreamWaitEvent(dev->s_out, sl.ev_k, 0) != hipSuccess) return JFS_ERR_HIP;
         if (hipMemcpyAsync(h_ret, d_ret, (size_t)n * 4, hipMemcpyDeviceToHost, dev->s_out) != hipSuccess)
             return JFS_ERR_HIP;
@@ -533,7 +580,7 @@ int64_t run_batch(DevCtx *dev, int algo, int dir, int nblk, const jfs_iov *iov, 
         return JFS_OK;
     };
     auto finish = [&](const Chunk &c) -> int64_t {
-        Slot &sl = dev->slot[c.slot];
+        Slot &sl = ln.slot[c.slot];
         const double t0 = host_trace() ? now_ms() : 0.0;
         if (hipEventSynchronize(sl.ev) != hipSuccess) return JFS_ERR_HIP;
         const double t1 = host_trace() ? now_ms() : 0.0;
@@ -563,7 +610,7 @@ int64_t run_batch(DevCtx *dev, int algo, int dir, int nblk, const jfs_iov *iov, 
     while (done < nch && rc == JFS_OK) rc = finish(ch[done++]);
     if (rc != JFS_OK) {  // leave no copy in flight into the staging slots
         (void)hipStreamSynchronize(dev->s_in);
-        for (Slot &sl : dev->slot) (void)hipStreamSynchronize(sl.st);
+        (void)hipStreamSynchronize(ln.s_k);
         (void)hipStreamSynchronize(dev->s_out);
     }
     return rc;
@@ -571,20 +618,29 @@ int64_t run_batch(DevCtx *dev, int algo, int dir, int nblk, const jfs_iov *iov, 
 
 // run_batch with per-block error isolation (a GPU codec
 // reports per-block errors): when a batch fails as a whole (staging
-// allocation, a copy or launch error), every block is re-run on its own, so a
-// failure is charged only to the blocks that fail alone.
-void run_isolated(DevCtx *dev, int algo, int dir, int nblk, const jfs_iov *iov, int64_t *out) {
+// allocation, a copy or launch error), it is split in halves and each half
+// re-run, down to single blocks, so a failure is charged only to the blocks
+// that fail alone and a few bad blocks cost O(log n) re-runs, not n.  After a
+// sticky HIP error (the lane's streams no longer synchronise) nothing is
+// re-run: the remaining blocks report JFS_ERR_HIP at once.
+bool lane_healthy(DevCtx *dev, Lane &ln) {
+    DevGuard guard;
+    (void)hipSetDevice(dev->id);
+    return hipStreamSynchronize(dev->s_in) == hipSuccess && hipStreamSynchronize(ln.s_k) == hipSuccess &&
+           hipStreamSynchronize(dev->s_out) == hipSuccess;
+}
+
+void run_isolated(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_iov *iov, int64_t *out) {
     if (nblk <= 0) return;
-    const int64_t rc = run_batch(dev, algo, dir, nblk, iov, out);
+    const int64_t rc = run_batch(dev, ln, algo, dir, nblk, iov, out);
     if (rc == JFS_OK) return;
-    if (nblk == 1) {
-        out[0] = rc;
+    if (nblk == 1 || (rc == JFS_ERR_HIP && !lane_healthy(dev, ln))) {
+        for (int i = 0; i < nblk; i++) out[i] = rc;
         return;
     }
-    for (int i = 0; i < nblk; i++) {
-        const int64_t r1 = run_batch(dev, algo, dir, 1, iov + i, out + i);
-        if (r1 != JFS_OK) out[i] = r1;
-    }
+    const int h = nblk / 2;
+    run_isolated(dev, ln, algo, dir, h, iov, out);
+    run_isolated(dev, ln, algo, dir, nblk - h, iov + h, out + h);
 }
 
 // ---------------------------------------------------------------------------
@@ -596,6 +652,31 @@ struct Pending {
     int64_t res;
     bool done;
 };
+
+// Gather window (microseconds): a worker that finds work waits until no new
+// call has arrived for `gap` (or `max` has passed since it started), so a
+// burst of concurrent calls (pkg/chunk runs up to 20 uploads and 200
+// downloads at once, cmd/flags.go:133-139) becomes one batch.  A lone call
+// pays `gap`.  JFS_GATHER_US=<decompress gap>,<compress gap> overrides the
+// gaps (max = 16 x gap).
+struct Gather {
+    int64_t gap_us, max_us;
+};
+Gather gather_window(int dir) {
+    static int64_t g[2] = {-1, -1};
+    static std::once_flag once;
+    std::call_once(once, [] {
+        g[DECOMPRESS_DIR] = 300;  // a lone 4 MiB decode takes milliseconds
+        g[COMPRESS_DIR] = 2000;   // an encode takes ~0.1-0.5 s: gather generously
+        if (const char *e = getenv("JFS_GATHER_US")) {
+            char *end = nullptr;
+            g[DECOMPRESS_DIR] = std::max(0ll, strtoll(e, &end, 10));
+            if (end && *end == ',') g[COMPRESS_DIR] = std::max(0ll, strtoll(end + 1, nullptr, 10));
+        }
+    });
+    const int64_t gap = g[dir == DECOMPRESS_DIR ? DECOMPRESS_DIR : COMPRESS_DIR];
+    return {gap, gap * 16};
+}
 
 class Coalescer {
    public:
@@ -610,54 +691,83 @@ class Coalescer {
         Pending p{algo, dir, iov, 0, false};
         std::unique_lock<std::mutex> lk(mu_);
         q_.push_back(&p);
-        cv_work_.notify_one();
+        arrivals_++;
+        cv_work_.notify_all();
         cv_done_.wait(lk, [&] { return p.done; });
         return p.res;
     }
 
    private:
-    static constexpr int kMaxBlocks = 256;
-    static constexpr int64_t kMaxBytes = 256ll << 20;
+    // A batch holds every queued call of one codec and direction, up to a
+    // decode launch's worth of resident blocks; run_batch cuts it into
+    // pipelined chunks of at most chunk_limit() staging bytes.
+    static constexpr int kMaxBlocks = 4096;
     std::mutex mu_;
     std::condition_variable cv_work_, cv_done_;
     std::deque<Pending *> q_;
+    uint64_t arrivals_ = 0;
+    bool gathering_ = false;  // one worker gathers at a time; the others run batches
     std::once_flag started_;
 
     void start(std::vector<DevCtx *> &ds) {
         std::call_once(started_, [&] {
-            for (DevCtx *d : ds) std::thread([this, d] { worker(d); }).detach();
+            // NLANE workers per device: a device runs the next batch while the
+            // previous one is still in flight (each worker owns one lane)
+            for (DevCtx *d : ds)
+                for (int k = 0; k < NLANE; k++) std::thread([this, d, k] { worker(d, d->lane[k]); }).detach();
         });
     }
-    void worker(DevCtx *dev) {
+    int queued_like(int algo, int dir) const {
+        int n = 0;
+        for (const Pending *p : q_) n += p->algo == algo && p->dir == dir;
+        return n;
+    }
+    void worker(DevCtx *dev, Lane &ln) {
         std::vector<Pending *> batch;
         std::vector<jfs_iov> iov;
         std::vector<int64_t> out;
+        double t_gather = 0.0;
         for (;;) {
             {
                 std::unique_lock<std::mutex> lk(mu_);
-                cv_work_.wait(lk, [&] { return !q_.empty(); });
-                int algo = q_.front()->algo, dir = q_.front()->dir;
-                int64_t bytes = 0;
+                cv_work_.wait(lk, [&] { return !q_.empty() && !gathering_; });
+                gathering_ = true;
+                t_gather = host_trace() ? now_ms() : 0.0;
+                const int algo = q_.front()->algo, dir = q_.front()->dir;
+                const Gather gw = gather_window(dir);
+                const auto t_end = std::chrono::steady_clock::now() + std::chrono::microseconds(gw.max_us);
+                uint64_t seen = arrivals_;
+                while (gw.gap_us > 0 && queued_like(algo, dir) < kMaxBlocks) {
+                    const auto until = std::min(t_end, std::chrono::steady_clock::now() +
+                                                           std::chrono::microseconds(gw.gap_us));
+                    cv_work_.wait_until(lk, until, [&] { return arrivals_ != seen; });
+                    if (arrivals_ == seen || std::chrono::steady_clock::now() >= t_end) break;
+                    seen = arrivals_;
+                }
                 batch.clear();
-                // same codec and direction; at most kMaxBytes of staging (the
-                // quantity run_batch stages); a request over the limit rides alone
                 for (auto it = q_.begin(); it != q_.end() && (int)batch.size() < kMaxBlocks;) {
-                    Pending *p = *it;
-                    const int64_t b = staged_bytes(p->algo, p->dir, p->iov);
-                    if (p->algo == algo && p->dir == dir && (batch.empty() || bytes + b <= kMaxBytes)) {
-                        batch.push_back(p);
-                        bytes += b;
+                    if ((*it)->algo == algo && (*it)->dir == dir) {
+                        batch.push_back(*it);
                         it = q_.erase(it);
-                        if (bytes > kMaxBytes) break;
                     } else {
                         ++it;
                     }
                 }
+                gathering_ = false;
             }
+            cv_work_.notify_all();  // the next worker may start gathering
             iov.resize(batch.size());
             out.assign(batch.size(), 0);
             for (size_t i = 0; i < batch.size(); i++) iov[i] = batch[i]->iov;
-            run_isolated(dev, batch[0]->algo, batch[0]->dir, (int)batch.size(), iov.data(), out.data());
+            {
+                const double t0 = host_trace() ? now_ms() : 0.0;
+                std::lock_guard<std::mutex> llk(ln.mu);
+                run_isolated(dev, ln, batch[0]->algo, batch[0]->dir, (int)batch.size(), iov.data(), out.data());
+                if (host_trace())
+                    fprintf(stderr, "[jfs coalescer] dev %d lane %d algo %d dir %d: %zu calls, gathered %.2f ms, ran %.2f ms\n",
+                            dev->id, (int)(&ln - dev->lane), batch[0]->algo, batch[0]->dir, batch.size(), t0 - t_gather,
+                            now_ms() - t0);
+            }
             {
                 std::lock_guard<std::mutex> lk(mu_);
                 for (size_t i = 0; i < batch.size(); i++) {
@@ -712,7 +822,9 @@ int64_t batch_common(int algo, int dir, int nblk, const jfs_iov *iov, int64_t *o
     std::vector<std::vector<int64_t>> res(G);
     auto work = [&](size_t g) {
         res[g].assign(part[g].size(), 0);
-        run_isolated(ds[g], algo, dir, (int)part[g].size(), part[g].data(), res[g].data());
+        std::unique_lock<std::mutex> lk;
+        Lane &ln = ds[g]->acquire_lane(lk);
+        run_isolated(ds[g], ln, algo, dir, (int)part[g].size(), part[g].data(), res[g].data());
     };
     if (G == 1) work(0);
     else {
@@ -806,53 +918,64 @@ int64_t jfs_decompress_batch(int algo, int nblk, const jfs_iov *iov, int64_t *ou
     return batch_call(algo, DECOMPRESS, nblk, iov, out_n, device_mask);
 }
 
+// The device-resident entry points launch on the caller's current device; it
+// must be one the library selected (gfx950, in JFS_GPU_DEVICES).
+static bool current_device_ok() {
+    std::vector<DevCtx *> &ds = devices();
+    int cur = -1;
+    if (ds.empty() || hipGetDevice(&cur) != hipSuccess) return false;
+    for (DevCtx *d : ds)
+        if (d->id == cur) return true;
+    return false;
+}
+
 int64_t jfs_lz4_decompress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream) {
-    if (devices().empty()) return JFS_ERR_NO_DEVICE;
+    if (!current_device_ok()) return JFS_ERR_NO_DEVICE;
     stat_launch(JFS_ALGO_LZ4, DECOMPRESS, nblk);
     return jfs_launch_lz4_decode(d_blocks, nblk, d_ret, (hipStream_t)stream) == 0 ? JFS_OK : JFS_ERR_HIP;
 }
 
 int64_t jfs_lz4_compress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream) {
-    if (devices().empty()) return JFS_ERR_NO_DEVICE;
+    if (!current_device_ok()) return JFS_ERR_NO_DEVICE;
     stat_launch(JFS_ALGO_LZ4, COMPRESS, nblk);
     return jfs_launch_lz4_encode(d_blocks, nblk, d_ret, (hipStream_t)stream) == 0 ? JFS_OK : JFS_ERR_HIP;
 }
 
 int64_t jfs_zstd_compress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream) {
-    if (devices().empty()) return JFS_ERR_NO_DEVICE;
+    if (!current_device_ok()) return JFS_ERR_NO_DEVICE;
     stat_launch(JFS_ALGO_ZSTD, COMPRESS, nblk);
     return jfs_launch_zstd_encode(d_blocks, nblk, d_ret, (hipStream_t)stream) == 0 ? JFS_OK : JFS_ERR_HIP;
 }
 
 int64_t jfs_zstd_decompress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream) {
-    if (devices().empty()) return JFS_ERR_NO_DEVICE;
+    if (!current_device_ok()) return JFS_ERR_NO_DEVICE;
     stat_launch(JFS_ALGO_ZSTD, DECOMPRESS, nblk);
     return jfs_launch_zstd_decode(d_blocks, nblk, d_ret, nullptr, (hipStream_t)stream) == 0 ? JFS_OK : JFS_ERR_HIP;
 }
 
 int64_t jfs_crc32c_device(const jfs_dev_block *d_blocks, int nblk, int32_t seg_bytes, uint32_t *d_crc,
                           int32_t *d_ret, void *stream) {
-    if (devices().empty()) return JFS_ERR_NO_DEVICE;
+    if (!current_device_ok()) return JFS_ERR_NO_DEVICE;
     if (nblk < 0 || seg_bytes < 0 || (seg_bytes > 0 && seg_bytes % 4096 != 0)) return JFS_ERR_INVALID;
     return jfs_launch_crc32c(d_blocks, nblk, seg_bytes, d_crc, d_ret, (hipStream_t)stream) == 0 ? JFS_OK
                                                                                               : JFS_ERR_HIP;
 }
 
 int64_t jfs_aes256gcm_seal_device(const jfs_aead_block *d_blocks, int nblk, int32_t *d_ret, void *stream) {
-    if (devices().empty()) return JFS_ERR_NO_DEVICE;
+    if (!current_device_ok()) return JFS_ERR_NO_DEVICE;
     if (nblk < 0) return JFS_ERR_INVALID;
     return jfs_launch_aes256gcm(d_blocks, nblk, 0, d_ret, nullptr, (hipStream_t)stream) == 0 ? JFS_OK : JFS_ERR_HIP;
 }
 
 int64_t jfs_aes256gcm_open_device(const jfs_aead_block *d_blocks, int nblk, int32_t *d_ret, void *stream) {
-    if (devices().empty()) return JFS_ERR_NO_DEVICE;
+    if (!current_device_ok()) return JFS_ERR_NO_DEVICE;
     if (nblk < 0) return JFS_ERR_INVALID;
     return jfs_launch_aes256gcm(d_blocks, nblk, 1, d_ret, nullptr, (hipStream_t)stream) == 0 ? JFS_OK : JFS_ERR_HIP;
 }
 
 int64_t jfs_lz4_compress_seal_device(const jfs_dev_block *d_comp, const jfs_aead_block *d_aead, int nblk,
                                      int32_t *d_ret_comp, int32_t *d_ret, void *stream) {
-    if (devices().empty()) return JFS_ERR_NO_DEVICE;
+    if (!current_device_ok()) return JFS_ERR_NO_DEVICE;
     if (nblk < 0) return JFS_ERR_INVALID;
     hipStream_t st = (hipStream_t)stream;
     if (jfs_launch_lz4_encode(d_comp, nblk, d_ret_comp, st) != 0) return JFS_ERR_HIP;
@@ -861,7 +984,7 @@ int64_t jfs_lz4_compress_seal_device(const jfs_dev_block *d_comp, const jfs_aead
 
 int64_t jfs_open_lz4_decompress_device(const jfs_aead_block *d_aead, const jfs_dev_block *d_dec, int nblk,
                                        int32_t *d_ret_open, int32_t *d_ret, void *stream) {
-    if (devices().empty()) return JFS_ERR_NO_DEVICE;
+    if (!current_device_ok()) return JFS_ERR_NO_DEVICE;
     if (nblk < 0) return JFS_ERR_INVALID;
     hipStream_t st = (hipStream_t)stream;
     if (jfs_launch_aes256gcm(d_aead, nblk, 1, d_ret_open, nullptr, st) != 0) return JFS_ERR_HIP;
@@ -881,6 +1004,7 @@ int jfs_stats(jfs_op_stats *out, int n) {
         out[i].bytes_out = g.bytes_out.load(std::memory_order_relaxed);
         out[i].errors = g.errors.load(std::memory_order_relaxed);
         out[i].nanos = g.nanos.load(std::memory_order_relaxed);
+        out[i].batches = g.batches.load(std::memory_order_relaxed);
     }
     return JFS_STATS_N;
 }
@@ -893,14 +1017,31 @@ void jfs_stats_reset(void) {
         g.bytes_out = 0;
         g.errors = 0;
         g.nanos = 0;
+        g.batches = 0;
     }
+    for (DevCtx *d : devices()) {
+        d->batches = 0;
+        d->blocks = 0;
+    }
+}
+
+int jfs_device_stats(jfs_device_stat *out, int n) {
+    std::vector<DevCtx *> &ds = devices();
+    for (int i = 0; out && i < n && i < (int)ds.size(); i++) {
+        out[i].device = ds[i]->id;
+        out[i].batches = ds[i]->batches.load(std::memory_order_relaxed);
+        out[i].blocks = ds[i]->blocks.load(std::memory_order_relaxed);
+    }
+    return (int)ds.size();
 }
 
 void jfs_release_staging(void) {
     for (DevCtx *d : devices()) {
         DevGuard guard;
-        std::lock_guard<std::mutex> lk(d->mu);
-        release_dev_staging(d);
+        for (Lane &ln : d->lane) {
+            std::lock_guard<std::mutex> lk(ln.mu);
+            release_lane_staging(d, ln);
+        }
     }
 }
 
@@ -917,7 +1058,7 @@ int64_t jfs_gen_blocks_device(uint8_t *d_dst, int nblk, int64_t block_bytes, cha
         if (d->id == cur) dev = d;
     if (!dev) return JFS_ERR_NO_DEVICE;
     {
-        std::lock_guard<std::mutex> lk(dev->mu);
+        std::lock_guard<std::mutex> lk(dev->vocab_mu);
         if (!dev->d_vocab) {
             std::vector<uint8_t> v(JFS_VOCAB_WORDS * 16);
             jfs_build_vocab(v.data());

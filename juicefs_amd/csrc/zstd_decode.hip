@@ -2127,12 +2127,10 @@ struct ZScratch {
     size_t items_cap = 0;
     uint16_t *d_tabs = nullptr;
     size_t tabs_cap = 0;
-    // device API only: the totals the previous launch needed (read once its
-    // copy has landed; no host wait), and the event that orders launches that
-    // share this scratch on different streams
+    // device API only: the totals a launch needs (zplan -> pinned record), and
+    // the event that orders launches sharing this scratch on different streams
     uint64_t *d_need = nullptr, *h_need = nullptr;
     hipEvent_t ev_need = nullptr, ev_done = nullptr;
-    bool pending = false;
     std::mutex mu;
 };
 ZScratch g_scr[16];
@@ -2164,11 +2162,12 @@ int launch_entropy_exec(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret,
 }
 }  // namespace
 
-// Device API: zscan -> zplan -> entropy -> execute, all enqueued on `stream`
-// with no host wait.  An input that does not fit the device's scratch gets
-// ret = -4 (E_SCRATCH); the totals the launch needed come back through a
-// pinned copy and the next call grows the scratch before it launches (the
-// only host wait: freeing scratch an earlier launch may still use).
+// Device API: zscan -> zplan -> entropy -> execute on `stream`.  The call
+// waits once on the host for zscan/zplan (the inputs' frame headers: a few
+// microseconds of kernel time after whatever `stream` already holds) to learn
+// the scratch the launch needs, grows the device's scratch if it is short and
+// re-plans, then enqueues the entropy and execute kernels without waiting.
+// So every input fits its scratch and ret is never E_SCRATCH.
 extern "C" int jfs_launch_zstd_decode(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, uint8_t *,
                                       hipStream_t stream) {
     using namespace jfs::zstdd;
@@ -2184,26 +2183,9 @@ extern "C" int jfs_launch_zstd_decode(const jfs_dev_block *d_blocks, int nblk, i
         if (hipEventCreateWithFlags(&z.ev_done, hipEventDisableTiming) != hipSuccess) return -1;
         z.h_need[0] = z.h_need[1] = z.h_need[2] = 0;
     }
-    // what the previous launch needed, if its copy has landed
-    uint64_t want_items = 0, want_lits = 0, want_tabs = 0;
-    if (z.pending && hipEventQuery(z.ev_need) == hipSuccess) {
-        want_items = z.h_need[0];
-        want_lits = z.h_need[1];
-        want_tabs = z.h_need[2];
-        z.pending = false;
-    }
-    // a first sizing guess: 4 KiB of items and 1 KiB of literals per input
-    want_items = std::max<uint64_t>(want_items + 64, (uint64_t)nblk * 256);
-    want_lits = std::max<uint64_t>(want_lits + 4096 + 64, (uint64_t)nblk * 1024);
-    want_tabs = std::max<uint64_t>(want_tabs + 64, (uint64_t)nblk * 4 * TAB_CELLS);
-    const bool grow = want_items > z.items_cap || want_lits > z.lit_cap || want_tabs > z.tabs_cap ||
-                      (size_t)nblk > z.info_cap;
-    if (grow) {
+    if ((size_t)nblk > z.info_cap) {
         // earlier launches (any stream) may still read the old scratch
         if (hipEventSynchronize(z.ev_done) != hipSuccess) return -1;
-        if (!grow_dev(&z.d_items, &z.items_cap, want_items)) return -1;
-        if (!grow_dev(&z.d_lit, &z.lit_cap, want_lits)) return -1;
-        if (!grow_dev(&z.d_tabs, &z.tabs_cap, want_tabs)) return -1;
         if (!grow_dev(&z.d_info, &z.info_cap, (size_t)nblk)) return -1;
     }
     // launches that share the scratch run in call order across streams
@@ -2213,11 +2195,21 @@ extern "C" int jfs_launch_zstd_decode(const jfs_dev_block *d_blocks, int nblk, i
     hipLaunchKernelGGL(zplan_kernel, dim3(1), dim3(PLAN_T), 0, stream, z.d_info, nblk, (uint64_t)z.items_cap,
                        (uint64_t)z.lit_cap, (uint64_t)z.tabs_cap, z.d_need);
     if (hipGetLastError() != hipSuccess) return -1;
-    if (!z.pending) {  // report the totals back (the pinned record is free again)
-        if (hipMemcpyAsync(z.h_need, z.d_need, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, stream) != hipSuccess)
-            return -1;
-        if (hipEventRecord(z.ev_need, stream) != hipSuccess) return -1;
-        z.pending = true;
+    if (hipMemcpyAsync(z.h_need, z.d_need, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, stream) != hipSuccess)
+        return -1;
+    if (hipEventRecord(z.ev_need, stream) != hipSuccess) return -1;
+    if (hipEventSynchronize(z.ev_need) != hipSuccess) return -1;
+    // zplan's overflow test: total + 64 items, + 4160 literal bytes, + 64 cells
+    const uint64_t want_items = z.h_need[0] + 64, want_lits = z.h_need[1] + 4096 + 64, want_tabs = z.h_need[2] + 64;
+    if (want_items > z.items_cap || want_lits > z.lit_cap || want_tabs > z.tabs_cap) {
+        // every earlier launch on the scratch is done: ev_done was waited for
+        // on `stream` ahead of ev_need
+        if (!grow_dev(&z.d_items, &z.items_cap, want_items)) return -1;
+        if (!grow_dev(&z.d_lit, &z.lit_cap, want_lits)) return -1;
+        if (!grow_dev(&z.d_tabs, &z.tabs_cap, want_tabs)) return -1;
+        hipLaunchKernelGGL(zplan_kernel, dim3(1), dim3(PLAN_T), 0, stream, z.d_info, nblk, (uint64_t)z.items_cap,
+                           (uint64_t)z.lit_cap, (uint64_t)z.tabs_cap, z.d_need);
+        if (hipGetLastError() != hipSuccess) return -1;
     }
     if (launch_entropy_exec(d_blocks, nblk, d_ret, z.d_info, z.d_lit, z.d_tabs, z.d_items, stream) != 0) return -1;
     return hipEventRecord(z.ev_done, stream) == hipSuccess ? 0 : -1;

@@ -59,19 +59,11 @@ def zstd_decompress(desc: torch.Tensor, ret: torch.Tensor, stream=None):
            "jfs_zstd_decompress_device")
 
 
-ZSTD_ERR_SCRATCH = -4  # the device's scratch was too small for this input: submit it again
-
-
-def zstd_decompress_sync(desc: torch.Tensor, ret: torch.Tensor, stream=None, tries: int = 3):
-    """zstd_decompress, waited for; inputs answered ZSTD_ERR_SCRATCH (the
-    library sizes its scratch from the previous call's needs, asynchronously)
-    are submitted again."""
-    for _ in range(tries):
-        zstd_decompress(desc, ret, stream)
-        torch.cuda.synchronize()
-        if not bool((ret == ZSTD_ERR_SCRATCH).any().item()):
-            return
-    raise RuntimeError("jfs_zstd_decompress_device: scratch did not grow")
+def zstd_decompress_sync(desc: torch.Tensor, ret: torch.Tensor, stream=None):
+    """zstd_decompress, waited for.  The library sizes its scratch inside the
+    call (include/jfs_gpucodec.h), so there is never anything to resubmit."""
+    zstd_decompress(desc, ret, stream)
+    torch.cuda.synchronize()
 
 
 def zstd_compress(desc: torch.Tensor, ret: torch.Tensor, stream=None):

@@ -94,8 +94,9 @@ def test_oracle_open_rejects_tampering(oracle):
     assert oracle.aes256gcm_open(key, nonce, b"\x00" * 15) is None
 
 
-def _run(gpu, items, seal, mis=0):
-    """items: list of (key, nonce, data); returns (ret list, outputs)."""
+def _run(gpu, items, seal, mis=0, raw=False):
+    """items: list of (key, nonce, data); returns (ret list, outputs) and, with
+    raw=True, also every block's whole dst region."""
     import torch
     from juicefs_amd import device as D
     so, off = [], 0
@@ -129,6 +130,8 @@ def _run(gpu, items, seal, mis=0):
     outs = [dh[o:o + max(x, 0)].tobytes() for o, x in zip(do, r)]
     for o, c in zip(do, caps):  # nothing written past the output
         assert (dh[o + c:o + c + 16] == 0xEE).all()
+    if raw:
+        return r, outs, [dh[o:o + c].tobytes() for o, c in zip(do, caps)]
     return r, outs
 
 
@@ -165,8 +168,12 @@ def test_gcm_gpu_open_rejects_tampering(gpu, oracle):
         b[pos] ^= 0x40
         bad.append((key, nonce, bytes(b)))
     bad.append((bytes(32), nonce, ct))  # wrong key
-    r, _ = _run(gpu, [(key, nonce, ct)] + bad, False)
+    r, _, regions = _run(gpu, [(key, nonce, ct)] + bad, False, raw=True)
     assert r[0] == len(pt) and r[1:] == [-1] * len(bad)
+    # like Go's gcm.Open, a failed open leaves no plaintext behind: dst is zeroed
+    assert regions[0] == pt
+    for reg in regions[1:]:
+        assert reg == bytes(len(pt))
 
 
 @pytest.mark.gpu

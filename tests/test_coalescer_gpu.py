@@ -1,0 +1,208 @@
+"""GPU: the one-call API under pkg/chunk's concurrency (cmd/flags.go:133-139:
+max-downloads 200, max-uploads 20).  cachedStore.load / upload
+(pkg/chunk/cached_store.go:755-823, :356-398) call Decompress / Compress once
+per block from that many goroutines; the library's coalescer must turn such a
+burst into a few device batches (jfs_stats().batches) and every caller must
+still get exactly its own block's result (checked against the CPU oracle).
+
+Also here: the device-resident surface refuses a current device the library
+did not select, and a fresh process's first Zstd device call sizes its own
+scratch (never asks for a resubmit)."""
+import ctypes
+import os
+import subprocess
+import sys
+import threading
+
+import numpy as np
+import pytest
+
+from juicefs_amd import _lib as L
+from juicefs_amd.blockgen import gen_block
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+U = 4 << 20
+
+
+def _stats(lib):
+    arr = (L.JfsOpStats * L.STATS_N)()
+    lib.jfs_stats(arr, L.STATS_N)
+    return arr
+
+
+def _burst(n, call):
+    """n threads released together; call(t) -> bool.  Returns failures."""
+    bar = threading.Barrier(n)
+    bad = []
+
+    def work(t):
+        bar.wait()
+        if not call(t):
+            bad.append(t)
+    th = [threading.Thread(target=work, args=(t,)) for t in range(n)]
+    [x.start() for x in th]
+    [x.join() for x in th]
+    return bad
+
+
+@pytest.fixture(scope="module")
+def blocks(oracle):
+    raws = [gen_block("T", 5000 + i, U) for i in range(8)]
+    comps = [oracle.lz4_compress(r)[1] for r in raws]
+    return raws, comps
+
+
+def test_200_concurrent_decodes_coalesce(gpu, lib, blocks):
+    raws, comps = blocks
+    n = 200
+    srcs = [ctypes.create_string_buffer(comps[t % 8], len(comps[t % 8])) for t in range(n)]
+    dsts = [ctypes.create_string_buffer(U) for _ in range(n)]
+    res = [None] * n
+
+    def call(t):
+        res[t] = lib.jfs_decompress(L.ALGO_LZ4, dsts[t], U, srcs[t], len(comps[t % 8]))
+        return res[t] == U and dsts[t].raw == raws[t % 8]
+    call(0)  # warm the coalescer and the staging
+    lib.jfs_stats_reset()
+    bad = _burst(n, call)
+    assert not bad, [(t, res[t]) for t in bad[:5]]
+    st = _stats(lib)[L.ALGO_LZ4 * 2 + 1]
+    assert st.calls == n and st.blocks == n and st.errors == 0
+    # 200 calls released together: a handful of device batches, not 200 (the
+    # first arrivals may ride a batch of their own while the rest gather)
+    assert 1 <= st.batches <= 4, st.batches
+    ds = (L.JfsDeviceStat * 16)()
+    nd = lib.jfs_device_stats(ds, 16)
+    assert nd >= 1 and sum(ds[i].blocks for i in range(nd)) == n
+    assert sum(ds[i].batches for i in range(nd)) == st.batches
+
+
+def test_20_concurrent_compresses_coalesce(gpu, lib, blocks, oracle):
+    raws, comps = blocks
+    n = 20
+    bound = lib.jfs_compress_bound(L.ALGO_LZ4, U)
+    srcs = [ctypes.create_string_buffer(raws[t % 8], U) for t in range(n)]
+    dsts = [ctypes.create_string_buffer(bound) for _ in range(n)]
+    res = [None] * n
+
+    def call(t):
+        res[t] = lib.jfs_compress(L.ALGO_LZ4, dsts[t], bound, srcs[t], U)
+        c = comps[t % 8]
+        return res[t] == len(c) and dsts[t].raw[:len(c)] == c  # byte-identical to LZ4_compress_default
+    lib.jfs_stats_reset()
+    bad = _burst(n, call)
+    assert not bad, [(t, res[t]) for t in bad[:5]]
+    st = _stats(lib)[L.ALGO_LZ4 * 2]
+    assert st.calls == n and st.errors == 0
+    assert 1 <= st.batches <= 2, st.batches
+
+
+def test_mixed_codecs_and_errors_in_one_burst(gpu, lib, blocks, oracle):
+    """LZ4 and Zstd decodes, good and corrupt, interleaved from 64 threads:
+    each caller gets its own block's result."""
+    from juicefs_amd import compress as C
+    raws, comps = blocks
+    zs = C.ZStandard()
+    small = [gen_block("T", 9000 + i, 300000 + 1000 * i) for i in range(4)]
+    zframes = []
+    for s in small:
+        d = bytearray(zs.CompressBound(len(s)))
+        k, e = zs.Compress(d, s)
+        assert e is None
+        zframes.append(bytes(d[:k]))
+    bad_lz4 = comps[0][:len(comps[0]) // 3]
+    want_bad, _ = oracle.lz4_decompress(bad_lz4, U)
+    assert want_bad < 0
+    n = 64
+    jobs = []
+    for t in range(n):
+        k = t % 4
+        if k == 0:
+            jobs.append((L.ALGO_LZ4, comps[t % 8], U, raws[t % 8]))
+        elif k == 1:
+            jobs.append((L.ALGO_ZSTD, zframes[t % 4], len(small[t % 4]), small[t % 4]))
+        elif k == 2:
+            jobs.append((L.ALGO_LZ4, bad_lz4, U, None))
+        else:
+            jobs.append((L.ALGO_LZ4, comps[t % 8], U - 1, None))  # dst one byte short
+    srcs = [ctypes.create_string_buffer(j[1], len(j[1])) for j in jobs]
+    dsts = [ctypes.create_string_buffer(max(j[2], 1)) for j in jobs]
+    want_short = {t % 8: oracle.lz4_decompress(comps[t % 8], U - 1)[0] for t in range(3, n, 4)}
+    res = [None] * n
+
+    def call(t):
+        algo, c, cap, want = jobs[t]
+        res[t] = lib.jfs_decompress(algo, dsts[t], cap, srcs[t], len(c))
+        if want is not None:
+            return res[t] == len(want) and dsts[t].raw[:len(want)] == want
+        if cap == U:
+            return res[t] == want_bad
+        return res[t] == want_short[t % 8]
+    bad = _burst(n, call)
+    assert not bad, [(t, res[t]) for t in bad[:5]]
+
+
+CHILD_ZSTD_FIRST = r'''
+import sys, numpy as np, torch
+sys.path.insert(0, sys.argv[1])
+from juicefs_amd import device as D, _lib as L
+from juicefs_amd.blockgen import gen_block
+dev = torch.device("cuda:0")
+n, U = 48, 4 << 20
+raw = np.concatenate([np.frombuffer(gen_block("T", 70 + i, U), dtype=np.uint8) for i in range(n)])
+src = torch.from_numpy(raw).to(dev)
+bound = U + (U >> 8) + 64
+comp = torch.zeros(n * bound, dtype=torch.uint8, device=dev)
+offs = np.arange(n, dtype=np.int64)
+ret = torch.zeros(n, dtype=torch.int32, device=dev)
+D.zstd_compress(D.make_desc(src, offs * U, [U] * n, comp, offs * bound, [bound] * n), ret)
+torch.cuda.synchronize()
+sizes = ret.cpu().tolist()
+assert all(s > 0 for s in sizes), sizes
+out = torch.zeros(n * U, dtype=torch.uint8, device=dev)
+desc = D.make_desc(comp, offs * bound, sizes, out, offs * U, [U] * n)
+ret.zero_()
+# the process's very first decompress call: one call, no resubmit
+assert L.load().jfs_zstd_decompress_device(desc.data_ptr(), n, ret.data_ptr(), None) == 0
+torch.cuda.synchronize()
+r = ret.cpu().tolist()
+assert r == [U] * n, sorted(set(r))
+assert torch.equal(out, src)
+print("OK")
+'''
+
+
+def test_zstd_device_first_call_needs_no_resubmit(gpu):
+    r = subprocess.run([sys.executable, "-c", CHILD_ZSTD_FIRST, ROOT], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "OK" in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])
+
+
+CHILD_DEVSEL = r'''
+import sys, torch
+sys.path.insert(0, sys.argv[1])
+from juicefs_amd import device as D, _lib as L
+lib = L.load()
+torch.cuda.set_device(0)
+buf = torch.zeros(64, dtype=torch.uint8, device="cuda:0")
+ret = torch.zeros(1, dtype=torch.int32, device="cuda:0")
+desc = D.make_desc(buf, [0], [4], buf, [32], [16])
+rc = [lib.jfs_lz4_decompress_device(desc.data_ptr(), 1, ret.data_ptr(), None),
+      lib.jfs_zstd_decompress_device(desc.data_ptr(), 1, ret.data_ptr(), None),
+      lib.jfs_crc32c_device(desc.data_ptr(), 1, 0, None, ret.data_ptr(), None)]
+print(lib.jfs_device_count(), *rc)
+'''
+
+
+def test_device_api_refuses_unselected_device(gpu):
+    """JFS_GPU_DEVICES also binds the device-resident surface: with device 0
+    excluded, a launch on device 0 is JFS_ERR_NO_DEVICE."""
+    env = dict(os.environ, JFS_GPU_DEVICES="7")
+    r = subprocess.run([sys.executable, "-c", CHILD_DEVSEL, ROOT], env=env, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    vals = [int(x) for x in r.stdout.split()]
+    import torch
+    if torch.cuda.device_count() <= 7:
+        assert vals[0] == 0
+    assert vals[1:] == [L.JFS_ERR_NO_DEVICE] * 3
