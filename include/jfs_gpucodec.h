@@ -119,6 +119,24 @@ typedef struct jfs_dev_block {
 /* ret[i] = LZ4_decompress_safe(src, dst, src_len, dst_cap): bytes written, or
  * its negative error value. */
 int64_t jfs_lz4_decompress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream);
+/* The same result for a FEW blocks at low latency (cachedStore.load decodes one
+ * block per cache miss, pkg/chunk/cached_store.go:755-823): every block is
+ * spread over the whole GPU instead of one workgroup.  src_len / dst_cap are
+ * HOST copies of the descriptors' sizes (they size the launch without a device
+ * round trip) and must match d_blocks.  Asynchronous on `stream`; per-device
+ * scratch of about 4 bytes per dst_cap byte, reused across calls.  Best below
+ * ~128-192 blocks of 4 MiB; jfs_lz4_decompress_device is faster for large batches. */
+int64_t jfs_lz4_decompress_device_small(const jfs_dev_block *d_blocks, const int32_t *src_len, const int32_t *dst_cap,
+                                        int nblk, int32_t *d_ret, void *stream);
+/* Diagnostics for the small-batch path (used by it, by jfs_decompress and by
+ * small jfs_decompress_batch calls), six counters: out[0] = blocks it decoded
+ * itself, out[1] = blocks it handed to the one-workgroup kernel (inputs outside
+ * its proven cases), and why: out[2] the token-chain fix-up did not converge
+ * (e.g. literal runs spanning many segments), out[3] the byte-origin pointer
+ * jumping did not converge, out[4] a token outside the proven acceptance
+ * conditions (malformed or edge-of-buffer), out[5] no final literal run; on
+ * the current device since the last reset.  Synchronous; 0 on success. */
+int jfs_lz4_split_counts(uint64_t *out, int reset);
 /* ret[i] = LZ4_compress_default(src, dst, src_len, dst_cap): compressed size,
  * or 0 when it does not fit dst_cap. */
 int64_t jfs_lz4_compress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream);

@@ -32,7 +32,8 @@ EXPORTS = [
     "jfs_zstd_decompress_device", "jfs_zstd_compress_device", "jfs_device_count", "jfs_version", "jfs_gen_blocks_device",
     "jfs_gen_block_host", "jfs_release_staging", "jfs_crc32c_device", "jfs_aes256gcm_seal_device",
     "jfs_aes256gcm_open_device", "jfs_lz4_compress_seal_device", "jfs_open_lz4_decompress_device",
-    "jfs_gpu_mode", "jfs_stats", "jfs_stats_reset", "jfs_device_stats",
+    "jfs_gpu_mode", "jfs_stats", "jfs_stats_reset", "jfs_device_stats", "jfs_lz4_decompress_device_small",
+    "jfs_lz4_split_counts",
 ]
 
 MODE_OFF, MODE_AUTO, MODE_FORCE = 0, 1, 2
@@ -87,6 +88,10 @@ def load() -> ctypes.CDLL:
               lib.jfs_zstd_compress_device):
         f.argtypes = [vp, ctypes.c_int, vp, vp]
         f.restype = i64
+    lib.jfs_lz4_decompress_device_small.argtypes = [vp, vp, vp, ctypes.c_int, vp, vp]
+    lib.jfs_lz4_decompress_device_small.restype = i64
+    lib.jfs_lz4_split_counts.argtypes = [vp, ctypes.c_int]
+    lib.jfs_lz4_split_counts.restype = ctypes.c_int
     lib.jfs_crc32c_device.argtypes = [vp, ctypes.c_int, ctypes.c_int32, vp, vp, vp]
     lib.jfs_crc32c_device.restype = i64
     for f in (lib.jfs_aes256gcm_seal_device, lib.jfs_aes256gcm_open_device):

@@ -65,6 +65,21 @@ struct Slot {
     uint8_t *z_lit = nullptr, *z_items = nullptr;
     uint16_t *z_tabs = nullptr;
     uint64_t z_lit_cap = 0, z_items_cap = 0, z_tabs_cap = 0;
+    // small-batch LZ4 decode scratch (lz4_split.hip)
+    uint8_t *sp = nullptr;
+    int64_t sp_cap = 0;
+
+    bool ensure_split(int64_t bytes) {
+        if (bytes <= sp_cap) return true;
+        if (sp) (void)hipFree(sp);
+        sp = nullptr;
+        sp_cap = 0;
+        int64_t want = 64ll << 20;
+        while (want < bytes) want <<= 1;
+        if (hipMalloc((void **)&sp, (size_t)want) != hipSuccess) return false;
+        sp_cap = want;
+        return true;
+    }
 
     bool ensure_zstd(const uint64_t *t) {  // t: items, literal bytes, table cells
         auto grow = [](auto **p, uint64_t *cap, uint64_t want, size_t elem) {
@@ -131,6 +146,9 @@ struct Lane {
             if (sl.z_lit) (void)hipFree(sl.z_lit);
             if (sl.z_items) (void)hipFree(sl.z_items);
             if (sl.z_tabs) (void)hipFree(sl.z_tabs);
+            if (sl.sp) (void)hipFree(sl.sp);
+            sl.sp = nullptr;
+            sl.sp_cap = 0;
             sl.h = sl.d = sl.z_lit = sl.z_items = nullptr;
             sl.z_tabs = nullptr;
             sl.h_cap = sl.d_cap = 0;
@@ -139,7 +157,7 @@ struct Lane {
     }
     bool holds_staging() const {
         for (const Slot &sl : slot)
-            if (sl.h || sl.d || sl.z_items) return true;
+            if (sl.h || sl.d || sl.z_items || sl.sp) return true;
         return false;
     }
 };
@@ -413,6 +431,17 @@ int64_t chunk_limit() {
     return v;
 }
 
+// Batches of at most this many LZ4 decode blocks take the small-batch path
+// (lz4_split.hip: every block spread over the whole GPU) instead of one
+// workgroup per block; JFS_LZ4_SPLIT_MAX overrides (0 = never).
+int split_max() {
+    static int v = [] {
+        const char *e = getenv("JFS_LZ4_SPLIT_MAX");
+        return e ? std::max(0, atoi(e)) : 128;
+    }();
+    return v;
+}
+
 // memcpy jobs spread over host threads (pageable <-> pinned is CPU-bound)
 struct CopyJob {
     uint8_t *dst;
@@ -567,8 +596,23 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
             return JFS_ERR_HIP;
         if (hipEventRecord(sl.ev_in, dev->s_in) != hipSuccess) return JFS_ERR_HIP;
         if (hipStreamWaitEvent(ln.s_k, sl.ev_in, 0) != hipSuccess) return JFS_ERR_HIP;
-        const int lk = zplan ? jfs_launch_zstd_decode_planned(d_desc, n, d_ret, d_zi, sl.z_lit, sl.z_tabs, sl.z_items, ln.s_k)
-                             : launch_kernel(algo, dir, d_desc, n, d_ret, ln.s_k);
+        int lk;
+        if (zplan) {
+            lk = jfs_launch_zstd_decode_planned(d_desc, n, d_ret, d_zi, sl.z_lit, sl.z_tabs, sl.z_items, ln.s_k);
+        } else if (algo == JFS_ALGO_LZ4 && dir == DECOMPRESS && n <= split_max()) {
+            std::vector<int32_t> lens(n), caps(n);
+            int64_t nseg = 0, max_cap = 0;
+            for (int k = 0; k < n; k++) {
+                lens[k] = h_desc[k].src_len;
+                caps[k] = h_desc[k].dst_cap;
+                nseg += (std::max(lens[k], 0) + JFS_LZ4_SPLIT_SEG - 1) / JFS_LZ4_SPLIT_SEG;
+                max_cap = std::max<int64_t>(max_cap, caps[k]);
+            }
+            if (!sl.ensure_split(jfs_lz4_split_scratch_bytes(n, lens.data(), caps.data()))) return JFS_ERR_NO_MEMORY;
+            lk = jfs_launch_lz4_split(d_desc, n, d_ret, sl.sp, nseg, max_cap, ln.s_k);
+        } else {
+            lk = launch_kernel(algo, dir, d_desc, n, d_ret, ln.s_k);
+        }
         if (lk != 0) return JFS_ERR_HIP;
         if (hipEventRecord(sl.ev_k, ln.s_k) != hipSuccess) return JFS_ERR_HIP;
         if (hipStreamWaitEvent(dev->s_out, sl.ev_k, 0) != hipSuccess) return JFS_ERR_HIP;
@@ -933,6 +977,49 @@ int64_t jfs_lz4_decompress_device(const jfs_dev_block *d_blocks, int nblk, int32
     if (!current_device_ok()) return JFS_ERR_NO_DEVICE;
     stat_launch(JFS_ALGO_LZ4, DECOMPRESS, nblk);
     return jfs_launch_lz4_decode(d_blocks, nblk, d_ret, (hipStream_t)stream) == 0 ? JFS_OK : JFS_ERR_HIP;
+}
+
+// Small-batch device decode: per-device scratch shared by every caller,
+// ordered across streams by an event (like the Zstd device decoder's).
+struct SplitScratch {
+    std::mutex mu;
+    uint8_t *p = nullptr;
+    int64_t cap = 0;
+    hipEvent_t ev_done = nullptr;
+};
+SplitScratch g_split[64];
+
+int64_t jfs_lz4_decompress_device_small(const jfs_dev_block *d_blocks, const int32_t *src_len, const int32_t *dst_cap,
+                                        int nblk, int32_t *d_ret, void *stream) {
+    if (!current_device_ok()) return JFS_ERR_NO_DEVICE;
+    if (nblk < 0 || (nblk > 0 && (!src_len || !dst_cap))) return JFS_ERR_INVALID;
+    if (nblk == 0) return JFS_OK;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return JFS_ERR_HIP;
+    stat_launch(JFS_ALGO_LZ4, DECOMPRESS, nblk);
+    int64_t nseg = 0, max_cap = 0;
+    for (int k = 0; k < nblk; k++) {
+        nseg += (std::max(src_len[k], 0) + JFS_LZ4_SPLIT_SEG - 1) / JFS_LZ4_SPLIT_SEG;
+        max_cap = std::max<int64_t>(max_cap, dst_cap[k]);
+    }
+    const int64_t need = jfs_lz4_split_scratch_bytes(nblk, src_len, dst_cap);
+    SplitScratch &z = g_split[dev];
+    std::lock_guard<std::mutex> lk(z.mu);
+    if (!z.ev_done && hipEventCreateWithFlags(&z.ev_done, hipEventDisableTiming) != hipSuccess) return JFS_ERR_HIP;
+    if (need > z.cap) {
+        if (hipEventSynchronize(z.ev_done) != hipSuccess) return JFS_ERR_HIP;  // earlier launches may still use it
+        if (z.p) (void)hipFree(z.p);
+        z.p = nullptr;
+        z.cap = 0;
+        int64_t want = 64ll << 20;
+        while (want < need) want <<= 1;
+        if (hipMalloc((void **)&z.p, (size_t)want) != hipSuccess) return JFS_ERR_NO_MEMORY;
+        z.cap = want;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    if (hipStreamWaitEvent(st, z.ev_done, 0) != hipSuccess) return JFS_ERR_HIP;
+    if (jfs_launch_lz4_split(d_blocks, nblk, d_ret, z.p, nseg, max_cap, st) != 0) return JFS_ERR_HIP;
+    return hipEventRecord(z.ev_done, st) == hipSuccess ? JFS_OK : JFS_ERR_HIP;
 }
 
 int64_t jfs_lz4_compress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream) {

@@ -1404,12 +1404,16 @@ __device__ __forceinline__ void copier_wave(Smem &s, Ctx &c, int32_t *retp PROF_
 #define JFS_LZ4_ATTR __attribute__((amdgpu_num_sgpr(JFS_LZ4_NSGPR), amdgpu_waves_per_eu(8)))
 // lens (optional): per-block input lengths produced on the device by the
 // previous kernel of a fused chain (AES-GCM open); < 0 = that step failed.
+// todo (optional): only the blocks with todo[b] != 0 are decoded (the others
+// were decoded by lz4_split.hip and keep its results).
 __global__ __launch_bounds__(128) JFS_LZ4_ATTR void lz4_decode_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
                                                         int32_t *__restrict__ ret,
-                                                        const int32_t *__restrict__ lens) {
+                                                        const int32_t *__restrict__ lens,
+                                                        const int32_t *__restrict__ todo) {
     __shared__ Smem s;
     const int b = blockIdx.x;
     if (b >= nblk) return;
+    if (todo && !todo[b]) return;
     const int wave = (int)uniform(threadIdx.x >> 6);
     jfs_dev_block d = ((const gc_blk *)blocks)[b];
     Ctx c;
@@ -1468,6 +1472,15 @@ extern "C" int jfs_launch_lz4_decode(const jfs_dev_block *d_blocks, int nblk, in
 extern "C" int jfs_launch_lz4_decode_lens(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, const int32_t *d_lens,
                                           hipStream_t stream) {
     if (nblk <= 0) return 0;
-    hipLaunchKernelGGL(jfs::lz4d::lz4_decode_kernel, dim3(nblk), dim3(128), 0, stream, d_blocks, nblk, d_ret, d_lens);
+    hipLaunchKernelGGL(jfs::lz4d::lz4_decode_kernel, dim3(nblk), dim3(128), 0, stream, d_blocks, nblk, d_ret, d_lens,
+                       (const int32_t *)nullptr);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int jfs_launch_lz4_decode_todo(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, const int32_t *d_todo,
+                                          hipStream_t stream) {
+    if (nblk <= 0) return 0;
+    hipLaunchKernelGGL(jfs::lz4d::lz4_decode_kernel, dim3(nblk), dim3(128), 0, stream, d_blocks, nblk, d_ret,
+                       (const int32_t *)nullptr, d_todo);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -53,6 +53,25 @@ def lz4_compress(desc: torch.Tensor, ret: torch.Tensor, stream=None):
            "jfs_lz4_compress_device")
 
 
+def lz4_decompress_small(desc: torch.Tensor, ret: torch.Tensor, src_lens, dst_caps, stream=None):
+    """jfs_lz4_decompress_device_small: few blocks, each spread over the GPU;
+    src_lens / dst_caps are host copies of the descriptors' sizes."""
+    n = desc.numel() // DESC_DTYPE.itemsize
+    sl = (ctypes.c_int32 * max(n, 1))(*[int(x) for x in src_lens])
+    dc = (ctypes.c_int32 * max(n, 1))(*[int(x) for x in dst_caps])
+    _check(L.load().jfs_lz4_decompress_device_small(desc.data_ptr(), sl, dc, n, ret.data_ptr(), _stream_ptr(stream)),
+           "jfs_lz4_decompress_device_small")
+
+
+def lz4_split_counts(reset: bool = False):
+    """(blocks the small-batch path decoded itself, blocks it handed to the
+    one-workgroup kernel, ... the reasons: fix-up, jumping, token, no last run)
+    on the current device."""
+    out = (ctypes.c_uint64 * 6)()
+    _check(L.load().jfs_lz4_split_counts(out, 1 if reset else 0), "jfs_lz4_split_counts")
+    return tuple(int(x) for x in out)
+
+
 def zstd_decompress(desc: torch.Tensor, ret: torch.Tensor, stream=None):
     n = desc.numel() // DESC_DTYPE.itemsize
     _check(L.load().jfs_zstd_decompress_device(desc.data_ptr(), n, ret.data_ptr(), _stream_ptr(stream)),
