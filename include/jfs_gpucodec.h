@@ -182,6 +182,19 @@ typedef struct jfs_aead_block {
 int64_t jfs_aes256gcm_seal_device(const jfs_aead_block *d_blocks, int nblk, int32_t *d_ret, void *stream);
 int64_t jfs_aes256gcm_open_device(const jfs_aead_block *d_blocks, int nblk, int32_t *d_ret, void *stream);
 
+/* The three data ciphers of NewDataEncryptor (pkg/object/encrypt.go:176-202).
+ * Same seal/open contract as above (ret, zeroed dst on a failed open, no
+ * additional data); the key is jfs_cipher_key_size(cipher) bytes. */
+#define JFS_CIPHER_AES256GCM 0        /* "aes256gcm-rsa" (and ""), encrypt.go:179-188: 32-byte key */
+#define JFS_CIPHER_CHACHA20POLY1305 1 /* "chacha20-rsa", encrypt.go:190: 32-byte key (RFC 8439) */
+#define JFS_CIPHER_SM4GCM 2           /* "sm4gcm", encrypt.go:192-201: 16-byte key (GB/T 32907 + GCM) */
+/* NewDataEncryptor's names -> cipher id, or -1 ("unsupport cipher") */
+int jfs_cipher_from_name(const char *name);
+/* keyLen of dataEncryptor (32 / 32 / 16), or -1 */
+int jfs_cipher_key_size(int cipher);
+int64_t jfs_aead_seal_device(int cipher, const jfs_aead_block *d_blocks, int nblk, int32_t *d_ret, void *stream);
+int64_t jfs_aead_open_device(int cipher, const jfs_aead_block *d_blocks, int nblk, int32_t *d_ret, void *stream);
+
 /* Fused object paths (compression runs before encryption on PUT and after
  * decryption on GET, cmd/format.go:289-302, docs internals.md:920), chained on
  * `stream` with no host round trip: the second kernel reads each block's

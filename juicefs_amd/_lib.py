@@ -33,10 +33,12 @@ EXPORTS = [
     "jfs_gen_block_host", "jfs_release_staging", "jfs_crc32c_device", "jfs_aes256gcm_seal_device",
     "jfs_aes256gcm_open_device", "jfs_lz4_compress_seal_device", "jfs_open_lz4_decompress_device",
     "jfs_gpu_mode", "jfs_stats", "jfs_stats_reset", "jfs_device_stats", "jfs_lz4_decompress_device_small",
-    "jfs_lz4_split_counts",
+    "jfs_lz4_split_counts", "jfs_cipher_from_name", "jfs_cipher_key_size", "jfs_aead_seal_device",
+    "jfs_aead_open_device",
 ]
 
 MODE_OFF, MODE_AUTO, MODE_FORCE = 0, 1, 2
+CIPHER_AES256GCM, CIPHER_CHACHA20POLY1305, CIPHER_SM4GCM = 0, 1, 2
 STATS_N = 6  # index algo * 2 + dir (0 compress, 1 decompress)
 
 
@@ -92,6 +94,13 @@ def load() -> ctypes.CDLL:
     lib.jfs_lz4_decompress_device_small.restype = i64
     lib.jfs_lz4_split_counts.argtypes = [vp, ctypes.c_int]
     lib.jfs_lz4_split_counts.restype = ctypes.c_int
+    lib.jfs_cipher_from_name.argtypes = [ctypes.c_char_p]
+    lib.jfs_cipher_from_name.restype = ctypes.c_int
+    lib.jfs_cipher_key_size.argtypes = [ctypes.c_int]
+    lib.jfs_cipher_key_size.restype = ctypes.c_int
+    for f in (lib.jfs_aead_seal_device, lib.jfs_aead_open_device):
+        f.argtypes = [ctypes.c_int, vp, ctypes.c_int, vp, vp]
+        f.restype = i64
     lib.jfs_crc32c_device.argtypes = [vp, ctypes.c_int, ctypes.c_int32, vp, vp, vp]
     lib.jfs_crc32c_device.restype = i64
     for f in (lib.jfs_aes256gcm_seal_device, lib.jfs_aes256gcm_open_device):

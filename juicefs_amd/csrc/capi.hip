@@ -1060,6 +1060,37 @@ int64_t jfs_aes256gcm_open_device(const jfs_aead_block *d_blocks, int nblk, int3
     return jfs_launch_aes256gcm(d_blocks, nblk, 1, d_ret, nullptr, (hipStream_t)stream) == 0 ? JFS_OK : JFS_ERR_HIP;
 }
 
+int jfs_cipher_from_name(const char *name) {
+    if (!name) return -1;
+    std::string v(name);
+    for (auto &ch : v) ch = (char)tolower((unsigned char)ch);
+    if (v.empty() || v == "aes256gcm-rsa") return JFS_CIPHER_AES256GCM;  // encrypt.go:178
+    if (v == "chacha20-rsa") return JFS_CIPHER_CHACHA20POLY1305;           // :190
+    if (v == "sm4gcm") return JFS_CIPHER_SM4GCM;                            // :191
+    return -1;
+}
+
+int jfs_cipher_key_size(int cipher) {
+    switch (cipher) {
+        case JFS_CIPHER_AES256GCM: return 32;
+        case JFS_CIPHER_CHACHA20POLY1305: return 32;
+        case JFS_CIPHER_SM4GCM: return 16;
+        default: return -1;
+    }
+}
+
+int64_t jfs_aead_seal_device(int cipher, const jfs_aead_block *d_blocks, int nblk, int32_t *d_ret, void *stream) {
+    if (!current_device_ok()) return JFS_ERR_NO_DEVICE;
+    if (nblk < 0 || jfs_cipher_key_size(cipher) < 0) return JFS_ERR_INVALID;
+    return jfs_launch_aead(cipher, d_blocks, nblk, 0, d_ret, nullptr, (hipStream_t)stream) == 0 ? JFS_OK : JFS_ERR_HIP;
+}
+
+int64_t jfs_aead_open_device(int cipher, const jfs_aead_block *d_blocks, int nblk, int32_t *d_ret, void *stream) {
+    if (!current_device_ok()) return JFS_ERR_NO_DEVICE;
+    if (nblk < 0 || jfs_cipher_key_size(cipher) < 0) return JFS_ERR_INVALID;
+    return jfs_launch_aead(cipher, d_blocks, nblk, 1, d_ret, nullptr, (hipStream_t)stream) == 0 ? JFS_OK : JFS_ERR_HIP;
+}
+
 int64_t jfs_lz4_compress_seal_device(const jfs_dev_block *d_comp, const jfs_aead_block *d_aead, int nblk,
                                      int32_t *d_ret_comp, int32_t *d_ret, void *stream) {
     if (!current_device_ok()) return JFS_ERR_NO_DEVICE;

@@ -37,6 +37,8 @@ int jfs_launch_crc32c(const jfs_dev_block *d_blocks, int nblk, int32_t seg_bytes
                       hipStream_t stream);
 int jfs_launch_aes256gcm(const jfs_aead_block *d_blocks, int nblk, int mode, int32_t *d_ret, const int32_t *d_lens,
                          hipStream_t stream);
+int jfs_launch_aead(int cipher, const jfs_aead_block *d_blocks, int nblk, int mode, int32_t *d_ret,
+                    const int32_t *d_lens, hipStream_t stream);
 int jfs_launch_lz4_decode_lens(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, const int32_t *d_lens,
                                hipStream_t stream);
 int jfs_launch_lz4_decode_todo(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, const int32_t *d_todo,

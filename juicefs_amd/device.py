@@ -126,6 +126,18 @@ def aes256gcm(desc: torch.Tensor, ret: torch.Tensor, seal: bool, stream=None):
     _check(fn(desc.data_ptr(), n, ret.data_ptr(), _stream_ptr(stream)), "jfs_aes256gcm")
 
 
+CIPHERS = {"aes256gcm": L.CIPHER_AES256GCM, "chacha20": L.CIPHER_CHACHA20POLY1305, "sm4gcm": L.CIPHER_SM4GCM}
+
+
+def aead(cipher: str, desc: torch.Tensor, ret: torch.Tensor, seal: bool, stream=None):
+    """Seal (True) or open (False) with aes256gcm / chacha20 / sm4gcm per descriptor
+    (jfs_aead_{seal,open}_device)."""
+    n = desc.numel() // AEAD_DTYPE.itemsize
+    lib = L.load()
+    fn = lib.jfs_aead_seal_device if seal else lib.jfs_aead_open_device
+    _check(fn(CIPHERS[cipher], desc.data_ptr(), n, ret.data_ptr(), _stream_ptr(stream)), "jfs_aead")
+
+
 JFS_CHAIN_FAILED = -(1 << 31)  # the first step of a fused chain failed for this block
 
 

@@ -21,6 +21,19 @@ class Oracle:
         for f in (lib.oracle_aes256gcm_seal, lib.oracle_aes256gcm_open):
             f.argtypes = [vp, vp, vp, i64, vp]
             f.restype = i64
+        lib.oracle_sm4_encrypt_block.argtypes = [vp, vp, vp]
+        for f in (lib.oracle_sm4gcm_seal, lib.oracle_sm4gcm_open):
+            f.argtypes = [vp, vp, vp, i64, vp]
+            f.restype = i64
+        for f in (lib.oracle_chacha20poly1305_seal, lib.oracle_chacha20poly1305_open):
+            f.argtypes = [vp, vp, vp, i64, vp, i64, vp]
+            f.restype = i64
+        lib.oracle_chacha20_block.argtypes = [vp, ctypes.c_uint32, vp, vp]
+        lib.oracle_poly1305.argtypes = [vp, vp, i64, vp]
+        lib.oracle_envelope_write.argtypes = [vp, i64, vp, i64, vp, i64, vp]
+        lib.oracle_envelope_write.restype = i64
+        lib.oracle_envelope_parse.argtypes = [vp, i64, ctypes.POINTER(i64), ctypes.POINTER(i64)]
+        lib.oracle_envelope_parse.restype = i64
         self.has_zstd = hasattr(lib, "oracle_zstd_decompress")
         if self.has_zstd:
             lib.oracle_zstd_decompress.argtypes = [vp, i64, vp, i64]
@@ -79,3 +92,55 @@ class Oracle:
 
     def xxh64(self, b: bytes, seed: int = 0) -> int:
         return self.lib.oracle_xxh64(b, len(b), seed)
+
+    # ---- SM4-GCM / ChaCha20-Poly1305 / the object envelope (aead_oracle.c) ----
+    def sm4_block(self, key: bytes, block: bytes) -> bytes:
+        out = ctypes.create_string_buffer(16)
+        self.lib.oracle_sm4_encrypt_block(key, block, out)
+        return out.raw
+
+    def seal(self, cipher: str, key: bytes, nonce: bytes, pt: bytes, aad: bytes = b"") -> bytes:
+        """aead.Seal(nil, nonce, pt, aad) for cipher in aes256gcm / chacha20 / sm4gcm"""
+        out = ctypes.create_string_buffer(len(pt) + 16)
+        if cipher == "aes256gcm":
+            assert not aad
+            n = self.lib.oracle_aes256gcm_seal(key, nonce, pt, len(pt), out)
+        elif cipher == "sm4gcm":
+            assert not aad
+            n = self.lib.oracle_sm4gcm_seal(key, nonce, pt, len(pt), out)
+        else:
+            n = self.lib.oracle_chacha20poly1305_seal(key, nonce, aad, len(aad), pt, len(pt), out)
+        return out.raw[:n]
+
+    def open(self, cipher: str, key: bytes, nonce: bytes, ct: bytes, aad: bytes = b""):
+        """aead.Open; None when the tag does not verify"""
+        out = ctypes.create_string_buffer(max(len(ct) - 16, 1))
+        if cipher == "aes256gcm":
+            n = self.lib.oracle_aes256gcm_open(key, nonce, ct, len(ct), out)
+        elif cipher == "sm4gcm":
+            n = self.lib.oracle_sm4gcm_open(key, nonce, ct, len(ct), out)
+        else:
+            n = self.lib.oracle_chacha20poly1305_open(key, nonce, aad, len(aad), ct, len(ct), out)
+        return None if n < 0 else out.raw[:n]
+
+    def chacha20_block(self, key: bytes, counter: int, nonce: bytes) -> bytes:
+        out = ctypes.create_string_buffer(64)
+        self.lib.oracle_chacha20_block(key, counter, nonce, out)
+        return out.raw
+
+    def poly1305(self, key: bytes, msg: bytes) -> bytes:
+        out = ctypes.create_string_buffer(16)
+        self.lib.oracle_poly1305(key, msg, len(msg), out)
+        return out.raw
+
+    def envelope(self, wrapped: bytes, nonce: bytes, sealed: bytes) -> bytes:
+        """dataEncryptor.Encrypt's output for a given wrapped key, nonce and sealed payload"""
+        out = ctypes.create_string_buffer(3 + len(wrapped) + len(nonce) + len(sealed))
+        n = self.lib.oracle_envelope_write(wrapped, len(wrapped), nonce, len(nonce), sealed, len(sealed), out)
+        return out.raw[:n]
+
+    def envelope_parse(self, env: bytes):
+        """(payload offset or -1/-2, wrapped-key length, nonce length)"""
+        w, nl = ctypes.c_int64(), ctypes.c_int64()
+        r = self.lib.oracle_envelope_parse(env, len(env), ctypes.byref(w), ctypes.byref(nl))
+        return r, w.value, nl.value
