@@ -45,6 +45,7 @@ extern "C" {
 #define JFS_ERR_INVALID (JFS_ERR_BASE - 7)       /* bad argument (unknown algo, negative size, ...) */
 #define JFS_ERR_HIP (JFS_ERR_BASE - 8)           /* HIP runtime failure */
 #define JFS_ERR_NO_MEMORY (JFS_ERR_BASE - 9)     /* pinned/HBM staging for this block could not be allocated */
+#define JFS_ERR_AUTH (JFS_ERR_BASE - 10)         /* "cipher: message authentication failed" (aead.Open, encrypt.go:283) */
 
 /* ---- Compressor surface (one synchronous call per block) ---------------- */
 
@@ -96,6 +97,44 @@ typedef struct jfs_iov {
 
 int64_t jfs_compress_batch(int algo, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t device_mask);
 int64_t jfs_decompress_batch(int algo, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t device_mask);
+
+/* ---- Encrypted objects (host buffers): compress + seal, open + decompress --
+ * The PUT path of an encrypted volume is Compress (cached_store.go:372) and
+ * then dataEncryptor.Encrypt (pkg/object/encrypt.go:226-257), which writes
+ *     be16(len(wrapped)) | u8(len(nonce)) | wrapped key | nonce | sealed
+ * with sealed = aead.Seal(nonce, compressed, nil) = ciphertext || 16-byte tag.
+ * jfs_compress_seal_batch does both on the GPU per block: iov[i].src is the raw
+ * block, iov[i].dst receives the whole envelope (dst_cap must be at least
+ * jfs_envelope_bound), out_n[i] = envelope bytes or the codec's error.  The
+ * random data key and nonce and the key wrap (RSA / SM2, keyEncryptor) are
+ * the caller's: p[i] carries them.  algo may be JFS_ALGO_NONE (encryption
+ * without compression).
+ * The GET path is Decrypt (:259-284) then Decompress (:814):
+ * jfs_open_decompress_batch takes the envelope in iov[i].src and the data key
+ * the caller unwrapped from its header (jfs_envelope_parse) in keys[i], and
+ * writes the block to iov[i].dst: out_n[i] = what jfs_decompress returns, or
+ * JFS_ERR_AUTH when the tag does not verify, or JFS_ERR_CORRUPT for a
+ * malformed header.  Errors are per block; the call returns JFS_OK,
+ * JFS_ERR_INVALID or JFS_ERR_NO_DEVICE like the plain batch calls. */
+typedef struct jfs_seal_param {
+    const uint8_t *key;     /* data key, jfs_cipher_key_size(cipher) bytes */
+    const uint8_t *nonce;   /* 12 bytes */
+    const uint8_t *wrapped; /* keyEncryptor.Encrypt(key) (encrypt.go:234) */
+    int32_t wrapped_len;    /* 0 .. 65535 */
+    int32_t reserved;
+} jfs_seal_param;
+
+/* 3 + wrapped_len + 12 + CompressBound(n) (n for "none") + 16 */
+int64_t jfs_envelope_bound(int algo, int64_t n, int32_t wrapped_len);
+/* Decrypt's header checks (encrypt.go:260-267): returns the offset of the sealed
+ * payload and the wrapped key / nonce positions, or JFS_ERR_CORRUPT when
+ * n < 3 or 3 + wrapped_len + nonce_len >= n. */
+int64_t jfs_envelope_parse(const uint8_t *src, int64_t n, int64_t *wrapped_off, int64_t *wrapped_len,
+                           int64_t *nonce_off, int64_t *nonce_len);
+int64_t jfs_compress_seal_batch(int algo, int cipher, int nblk, const jfs_iov *iov, const jfs_seal_param *p,
+                                int64_t *out_n, uint32_t device_mask);
+int64_t jfs_open_decompress_batch(int algo, int cipher, int nblk, const jfs_iov *iov, const uint8_t *const *keys,
+                                  int64_t *out_n, uint32_t device_mask);
 
 /* ---- Device-resident surface (inputs/outputs already in HBM) ------------
  * One descriptor per block; all pointers are device pointers on the calling

@@ -24,6 +24,7 @@ JFS_ERR_NO_DEVICE = JFS_ERR_BASE - 6
 JFS_ERR_INVALID = JFS_ERR_BASE - 7
 JFS_ERR_HIP = JFS_ERR_BASE - 8
 JFS_ERR_NO_MEMORY = JFS_ERR_BASE - 9
+JFS_ERR_AUTH = JFS_ERR_BASE - 10
 
 # every symbol include/jfs_gpucodec.h declares
 EXPORTS = [
@@ -34,7 +35,8 @@ EXPORTS = [
     "jfs_aes256gcm_open_device", "jfs_lz4_compress_seal_device", "jfs_open_lz4_decompress_device",
     "jfs_gpu_mode", "jfs_stats", "jfs_stats_reset", "jfs_device_stats", "jfs_lz4_decompress_device_small",
     "jfs_lz4_split_counts", "jfs_cipher_from_name", "jfs_cipher_key_size", "jfs_aead_seal_device",
-    "jfs_aead_open_device",
+    "jfs_aead_open_device", "jfs_envelope_bound", "jfs_envelope_parse", "jfs_compress_seal_batch",
+    "jfs_open_decompress_batch",
 ]
 
 MODE_OFF, MODE_AUTO, MODE_FORCE = 0, 1, 2
@@ -55,6 +57,11 @@ class JfsOpStats(ctypes.Structure):
 class JfsDeviceStat(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("pad_", ctypes.c_int32), ("batches", ctypes.c_uint64),
                 ("blocks", ctypes.c_uint64)]
+
+
+class JfsSealParam(ctypes.Structure):
+    _fields_ = [("key", ctypes.c_void_p), ("nonce", ctypes.c_void_p), ("wrapped", ctypes.c_void_p),
+                ("wrapped_len", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 class JfsDevBlock(ctypes.Structure):
@@ -101,6 +108,16 @@ def load() -> ctypes.CDLL:
     for f in (lib.jfs_aead_seal_device, lib.jfs_aead_open_device):
         f.argtypes = [ctypes.c_int, vp, ctypes.c_int, vp, vp]
         f.restype = i64
+    lib.jfs_envelope_bound.argtypes = [ctypes.c_int, i64, i32]
+    lib.jfs_envelope_bound.restype = i64
+    lib.jfs_envelope_parse.argtypes = [vp, i64] + [ctypes.POINTER(i64)] * 4
+    lib.jfs_envelope_parse.restype = i64
+    lib.jfs_compress_seal_batch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(JfsIov),
+                                            ctypes.POINTER(JfsSealParam), ctypes.POINTER(i64), u32]
+    lib.jfs_compress_seal_batch.restype = i64
+    lib.jfs_open_decompress_batch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(JfsIov),
+                                              ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(i64), u32]
+    lib.jfs_open_decompress_batch.restype = i64
     lib.jfs_crc32c_device.argtypes = [vp, ctypes.c_int, ctypes.c_int32, vp, vp, vp]
     lib.jfs_crc32c_device.restype = i64
     for f in (lib.jfs_aes256gcm_seal_device, lib.jfs_aes256gcm_open_device):

@@ -488,6 +488,31 @@ int launch_kernel(int algo, int dir, const jfs_dev_block *d_desc, int nblk, int3
     return -1;
 }
 
+// Object encryption around the codec (pkg/object/encrypt.go
+// dataEncryptor, installed after compression on PUT and before decompression
+// on GET, cmd/format.go:289-302).  Arrays are parallel to the iov run_batch
+// gets (whose src/src_len/dst_cap are the staged payload and capacity); orig
+// holds the caller's buffers, which receive the envelope (seal) or the
+// plaintext block (open).
+struct Aead {
+    int cipher;
+    bool seal;
+    const jfs_iov *orig;
+    const uint8_t *const *key;    // data key per block
+    const uint8_t *const *nonce;  // 12-byte nonce per block
+    const jfs_seal_param *sp;     // seal: wrapped key per block
+    const int64_t *hdr;           // seal: header bytes per block
+    Aead at(int64_t h) const {
+        Aead a = *this;
+        a.orig += h;
+        a.key += h;
+        a.nonce += h;
+        if (a.sp) a.sp += h;
+        if (a.hdr) a.hdr += h;
+        return a;
+    }
+};
+
 // Run blocks [0,nblk) of iov on one device through one lane (the caller holds
 // ln.mu); returns when every result is in out[].  Blocks that the C-ABI
 // answers without a kernel (empty input, noOp) are handled by the caller.  The
@@ -497,7 +522,8 @@ int launch_kernel(int algo, int dir, const jfs_dev_block *d_desc, int nblk, int3
 // chunk_limit() staging bytes; the lane's kernels run in chunk order, so a
 // batch is not cut finer than that (a decode kernel over fewer blocks than
 // CUs lasts about one block's latency whatever its size).
-int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_iov *iov, int64_t *out) {
+int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_iov *iov, int64_t *out,
+                  const Aead *ae = nullptr) {
     if (nblk <= 0) return JFS_OK;
     DevGuard guard;
     (void)hipSetDevice(dev->id);
@@ -522,7 +548,7 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
         while (s < nblk) {
             Chunk c{s, s, (int)(ch.size() % NSLOT), 0, 0};
             while (c.e < nblk) {
-                const int64_t ci = staged_cap(algo, dir, iov[c.e]);
+                const int64_t ci = ae ? iov[c.e].dst_cap : staged_cap(algo, dir, iov[c.e]);
                 const int64_t ib = align16(iov[c.e].src_len), ob = align16(ci);  // = staged_bytes()
                 if (c.e > s && c.tin + c.tout + ib + ob > limit) break;
                 cap[c.e] = ci;
@@ -537,8 +563,10 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
         }
     }
     // Zstd decode: the per-input scratch plan (ZInfo) rides in the chunk
-    const bool zplan = algo == JFS_ALGO_ZSTD && dir == DECOMPRESS;
+    const bool zplan = algo == JFS_ALGO_ZSTD && dir == DECOMPRESS && !ae;
     const int64_t zib = zplan ? (int64_t)jfs_zstd_info_bytes() : 0;
+    // aead extras per block: descriptor, second result, 64 bytes of key (32) + nonce (12)
+    const int64_t aeb = ae ? (int64_t)sizeof(jfs_aead_block) + 4 + 64 : 0;
     auto layout = [&](const Chunk &c, uint8_t *base, uint8_t **in, uint8_t **outp, jfs_dev_block **desc, int32_t **ret,
                       uint8_t **zinfo) {
         const int64_t desc_bytes = align16((int64_t)(c.e - c.s) * (int64_t)sizeof(jfs_dev_block));
@@ -549,9 +577,106 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
         *ret = (int32_t *)(base + c.tin + c.tout + desc_bytes);
         *zinfo = base + c.tin + c.tout + desc_bytes + ret_bytes;
     };
+    // the aead area follows the Zstd plan area: descriptors, results, key+nonce slots
+    auto aead_layout = [&](const Chunk &c, uint8_t *base, jfs_aead_block **ad, int32_t **ret2, uint8_t **kn) {
+        const int64_t nb = c.e - c.s;
+        uint8_t *p = base + c.tin + c.tout + align16(nb * (int64_t)sizeof(jfs_dev_block)) + align16(nb * 4) +
+                     align16(nb * zib);
+        *ad = (jfs_aead_block *)p;
+        p += align16(nb * (int64_t)sizeof(jfs_aead_block));
+        *ret2 = (int32_t *)p;
+        p += align16(nb * 4);
+        *kn = p;
+    };
     auto chunk_bytes = [&](const Chunk &c) {
-        return c.tin + c.tout + align16((int64_t)(c.e - c.s) * (int64_t)sizeof(jfs_dev_block)) +
-               align16((int64_t)(c.e - c.s) * 4) + align16((int64_t)(c.e - c.s) * zib);
+        const int64_t nb = c.e - c.s;
+        return c.tin + c.tout + align16(nb * (int64_t)sizeof(jfs_dev_block)) + align16(nb * 4) + align16(nb * zib) +
+               (ae ? align16(nb * (int64_t)sizeof(jfs_aead_block)) + align16(nb * 4) + nb * 64 : 0);
+    };
+    (void)aeb;
+    // compress -> seal, or open -> decompress (the staged inputs and the
+    // codec descriptors are already in place; run on the lane's kernel stream)
+    auto launch_aead = [&](const Chunk &c, Slot &sl, uint8_t *h_in, uint8_t *h_out, jfs_dev_block *h_desc,
+                           int32_t *h_ret, uint8_t *d_in, uint8_t *d_out, jfs_dev_block *d_desc,
+                           int32_t *d_ret) -> int64_t {
+        const int n = c.e - c.s;
+        jfs_aead_block *h_ad, *d_ad;
+        int32_t *h_r2, *d_r2;
+        uint8_t *h_kn, *d_kn;
+        aead_layout(c, sl.h, &h_ad, &h_r2, &h_kn);
+        aead_layout(c, sl.d, &d_ad, &d_r2, &d_kn);
+        const int klen = jfs_cipher_key_size(ae->cipher);
+        for (int k = 0; k < n; k++) {
+            const int i = c.s + k;
+            memcpy(h_kn + 64 * k, ae->key[i], (size_t)klen);
+            memcpy(h_kn + 64 * k + 32, ae->nonce[i], 12);
+            jfs_aead_block &a = h_ad[k];
+            a.key = d_kn + 64 * k;
+            a.nonce = d_kn + 64 * k + 32;
+            if (ae->seal) {
+                // the codec writes the payload area; the seal runs in place over it
+                h_desc[k].dst_cap = (int32_t)(cap[i] - 16);
+                a.src = algo == JFS_ALGO_NONE ? d_in + in_off[i] : d_out + out_off[i];
+                a.dst = d_out + out_off[i];
+                a.src_len = (int32_t)iov[i].src_len;
+                a.dst_cap = (int32_t)cap[i];
+            } else {
+                // open in place over the staged payload (into the output for "none"),
+                // then the codec reads the plaintext: the payload minus its tag
+                h_desc[k].src_len = (int32_t)std::max<int64_t>(iov[i].src_len - 16, 0);
+                a.src = d_in + in_off[i];
+                a.dst = algo == JFS_ALGO_NONE ? d_out + out_off[i] : d_in + in_off[i];
+                a.src_len = (int32_t)iov[i].src_len;
+                a.dst_cap = algo == JFS_ALGO_NONE ? (int32_t)cap[i] : (int32_t)iov[i].src_len;
+            }
+        }
+        const int64_t ab = align16((int64_t)n * (int64_t)sizeof(jfs_aead_block)) + align16((int64_t)n * 4) + n * 64;
+        if (hipMemcpyAsync(d_in, h_in, (size_t)c.tin, hipMemcpyHostToDevice, dev->s_in) != hipSuccess) return JFS_ERR_HIP;
+        if (hipMemcpyAsync(d_desc, h_desc, (size_t)n * sizeof(jfs_dev_block), hipMemcpyHostToDevice, dev->s_in) !=
+            hipSuccess)
+            return JFS_ERR_HIP;
+        if (hipMemcpyAsync(d_ad, h_ad, (size_t)ab, hipMemcpyHostToDevice, dev->s_in) != hipSuccess) return JFS_ERR_HIP;
+        if (hipEventRecord(sl.ev_in, dev->s_in) != hipSuccess) return JFS_ERR_HIP;
+        if (hipStreamWaitEvent(ln.s_k, sl.ev_in, 0) != hipSuccess) return JFS_ERR_HIP;
+        int lk = 0;
+        if (ae->seal) {
+            if (algo != JFS_ALGO_NONE) lk = launch_kernel(algo, COMPRESS, d_desc, n, d_ret, ln.s_k);
+            if (lk == 0)
+                lk = jfs_launch_aead(ae->cipher, d_ad, n, 0, d_r2, algo != JFS_ALGO_NONE ? d_ret : nullptr, ln.s_k);
+        } else {
+            lk = jfs_launch_aead(ae->cipher, d_ad, n, 1, d_r2, nullptr, ln.s_k);
+            if (lk == 0 && algo == JFS_ALGO_LZ4) {
+                if (n <= split_max()) {
+                    std::vector<int32_t> lens(n), caps(n);
+                    int64_t nseg = 0, max_cap = 0;
+                    for (int k = 0; k < n; k++) {
+                        lens[k] = h_desc[k].src_len;
+                        caps[k] = h_desc[k].dst_cap;
+                        nseg += (std::max(lens[k], 0) + JFS_LZ4_SPLIT_SEG - 1) / JFS_LZ4_SPLIT_SEG;
+                        max_cap = std::max<int64_t>(max_cap, caps[k]);
+                    }
+                    if (!sl.ensure_split(jfs_lz4_split_scratch_bytes(n, lens.data(), caps.data())))
+                        return JFS_ERR_NO_MEMORY;
+                    lk = jfs_launch_lz4_split(d_desc, n, d_ret, sl.sp, nseg, max_cap, ln.s_k);
+                } else {
+                    lk = jfs_launch_lz4_decode(d_desc, n, d_ret, ln.s_k);
+                }
+            } else if (lk == 0 && algo == JFS_ALGO_ZSTD) {
+                // the host holds ciphertext only: the device API plans the scratch itself
+                lk = jfs_launch_zstd_decode(d_desc, n, d_ret, nullptr, ln.s_k);
+            }
+        }
+        if (lk != 0) return JFS_ERR_HIP;
+        if (hipEventRecord(sl.ev_k, ln.s_k) != hipSuccess) return JFS_ERR_HIP;
+        if (hipStreamWaitEvent(dev->s_out, sl.ev_k, 0) != hipSuccess) return JFS_ERR_HIP;
+        if (hipMemcpyAsync(h_ret, d_ret, (size_t)n * 4, hipMemcpyDeviceToHost, dev->s_out) != hipSuccess)
+            return JFS_ERR_HIP;
+        if (hipMemcpyAsync(h_r2, d_r2, (size_t)n * 4, hipMemcpyDeviceToHost, dev->s_out) != hipSuccess)
+            return JFS_ERR_HIP;
+        if (hipMemcpyAsync(h_out, d_out, (size_t)c.tout, hipMemcpyDeviceToHost, dev->s_out) != hipSuccess)
+            return JFS_ERR_HIP;
+        if (hipEventRecord(sl.ev, dev->s_out) != hipSuccess) return JFS_ERR_HIP;
+        return JFS_OK;
     };
     auto launch = [&](const Chunk &c) -> int64_t {
         Slot &sl = ln.slot[c.slot];
@@ -575,6 +700,7 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
         if (host_trace())
             fprintf(stderr, "[jfs host] chunk %d-%d stage-in %.1f MiB %.2f ms\n", c.s, c.e, c.tin / 1048576.0, now_ms() - t0);
         const int n = c.e - c.s;
+        if (ae) return launch_aead(c, sl, h_in, h_out, h_desc, h_ret, d_in, d_out, d_desc, d_ret);
         if (algo != JFS_ALGO_LZ4 && algo != JFS_ALGO_ZSTD) return JFS_ERR_UNSUPPORTED;
         if (zplan) {  // plan the Zstd scratch from the staged inputs: no device round trip
             std::vector<const uint8_t *> srcs(n);
@@ -633,10 +759,49 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
         int32_t *h_ret;
         layout(c, sl.h, &h_in, &h_out, &h_desc, &h_ret, &h_zi);
         std::vector<CopyJob> jobs;
-        for (int i = c.s; i < c.e; i++) {
-            const int64_t r = finish_result(algo, dir, h_ret[i - c.s]);
-            if (r > 0) jobs.push_back({iov[i].dst, h_out + out_off[i], r});
-            out[i] = r;
+        if (ae) {
+            jfs_aead_block *h_ad;
+            int32_t *h_r2;
+            uint8_t *h_kn;
+            aead_layout(c, sl.h, &h_ad, &h_r2, &h_kn);
+            for (int i = c.s; i < c.e; i++) {
+                const int k = i - c.s;
+                const jfs_iov &o = ae->orig[i];
+                if (ae->seal) {
+                    // encrypt.go:244-254: be16(len(wrapped)) | len(nonce) | wrapped | nonce | sealed
+                    const int64_t rc = algo == JFS_ALGO_NONE ? iov[i].src_len : finish_result(algo, COMPRESS, h_ret[k]);
+                    const int64_t hdr = ae->hdr[i];
+                    if (rc < 0) {
+                        out[i] = rc;
+                    } else if (h_r2[k] != rc + 16) {
+                        out[i] = JFS_ERR_HIP;
+                    } else if (hdr + rc + 16 > o.dst_cap) {
+                        out[i] = JFS_ERR_SHORT_BUFFER;
+                    } else {
+                        const jfs_seal_param &p = ae->sp[i];
+                        o.dst[0] = (uint8_t)(p.wrapped_len >> 8);
+                        o.dst[1] = (uint8_t)(p.wrapped_len & 0xFF);
+                        o.dst[2] = 12;
+                        if (p.wrapped_len > 0) memcpy(o.dst + 3, p.wrapped, (size_t)p.wrapped_len);
+                        memcpy(o.dst + 3 + p.wrapped_len, ae->nonce[i], 12);
+                        jobs.push_back({o.dst + hdr, h_out + out_off[i], rc + 16});
+                        out[i] = hdr + rc + 16;
+                    }
+                } else {
+                    // aead.Open first (encrypt.go:283), then the codec
+                    const int64_t r = h_r2[k] < 0 ? JFS_ERR_AUTH
+                                      : algo == JFS_ALGO_NONE ? (int64_t)h_r2[k]
+                                                              : finish_result(algo, DECOMPRESS, h_ret[k]);
+                    if (r > 0) jobs.push_back({o.dst, h_out + out_off[i], r});
+                    out[i] = r;
+                }
+            }
+        } else {
+            for (int i = c.s; i < c.e; i++) {
+                const int64_t r = finish_result(algo, dir, h_ret[i - c.s]);
+                if (r > 0) jobs.push_back({iov[i].dst, h_out + out_off[i], r});
+                out[i] = r;
+            }
         }
         par_copy(jobs);
         if (host_trace())
@@ -674,17 +839,23 @@ bool lane_healthy(DevCtx *dev, Lane &ln) {
            hipStreamSynchronize(dev->s_out) == hipSuccess;
 }
 
-void run_isolated(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_iov *iov, int64_t *out) {
+void run_isolated(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_iov *iov, int64_t *out,
+                  const Aead *ae = nullptr) {
     if (nblk <= 0) return;
-    const int64_t rc = run_batch(dev, ln, algo, dir, nblk, iov, out);
+    const int64_t rc = run_batch(dev, ln, algo, dir, nblk, iov, out, ae);
     if (rc == JFS_OK) return;
     if (nblk == 1 || (rc == JFS_ERR_HIP && !lane_healthy(dev, ln))) {
         for (int i = 0; i < nblk; i++) out[i] = rc;
         return;
     }
     const int h = nblk / 2;
-    run_isolated(dev, ln, algo, dir, h, iov, out);
-    run_isolated(dev, ln, algo, dir, nblk - h, iov + h, out + h);
+    run_isolated(dev, ln, algo, dir, h, iov, out, ae);
+    if (ae) {
+        const Aead a2 = ae->at(h);
+        run_isolated(dev, ln, algo, dir, nblk - h, iov + h, out + h, &a2);
+    } else {
+        run_isolated(dev, ln, algo, dir, nblk - h, iov + h, out + h);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -842,33 +1013,48 @@ bool pre_answer(int algo, int dir, const jfs_iov &v, int64_t *res) {
     return false;
 }
 
-int64_t batch_common(int algo, int dir, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t mask) {
-    if (nblk < 0 || (nblk > 0 && (!iov || !out_n))) return JFS_ERR_INVALID;
-    if (algo != JFS_ALGO_NONE && algo != JFS_ALGO_LZ4 && algo != JFS_ALGO_ZSTD) return JFS_ERR_INVALID;
-    std::vector<int> todo;
-    for (int i = 0; i < nblk; i++) {
-        if (!pre_answer(algo, dir, iov[i], &out_n[i])) todo.push_back(i);
-    }
-    if (todo.empty()) return JFS_OK;
+// Deal the todo blocks round-robin over the selected devices
+// and run them; ae_all (optional) is parallel to iov2.
+int64_t deal(int algo, int dir, const std::vector<int> &todo, const std::vector<jfs_iov> &iov2, int64_t *out_n,
+             uint32_t mask, const Aead *ae_all) {
     std::vector<DevCtx *> &all = devices();
     std::vector<DevCtx *> ds;
     for (DevCtx *d : all)
         if (mask == 0 || (d->id < 32 && (mask >> d->id) & 1u)) ds.push_back(d);
     if (ds.empty()) return JFS_ERR_NO_DEVICE;
-    // round-robin deal of blocks to devices
-    size_t G = std::min(ds.size(), todo.size());
-    std::vector<std::vector<jfs_iov>> part(G);
-    std::vector<std::vector<int>> idx(G);
+    const size_t G = std::min(ds.size(), todo.size());
+    struct Part {
+        std::vector<jfs_iov> iov, orig;
+        std::vector<const uint8_t *> key, nonce;
+        std::vector<jfs_seal_param> sp;
+        std::vector<int64_t> hdr, res;
+        std::vector<int> idx;
+    };
+    std::vector<Part> part(G);
     for (size_t k = 0; k < todo.size(); k++) {
-        part[k % G].push_back(iov[todo[k]]);
-        idx[k % G].push_back(todo[k]);
+        Part &p = part[k % G];
+        p.iov.push_back(iov2[k]);
+        p.idx.push_back(todo[k]);
+        if (ae_all) {
+            p.orig.push_back(ae_all->orig[k]);
+            p.key.push_back(ae_all->key[k]);
+            p.nonce.push_back(ae_all->nonce[k]);
+            if (ae_all->sp) p.sp.push_back(ae_all->sp[k]);
+            if (ae_all->hdr) p.hdr.push_back(ae_all->hdr[k]);
+        }
     }
-    std::vector<std::vector<int64_t>> res(G);
     auto work = [&](size_t g) {
-        res[g].assign(part[g].size(), 0);
+        Part &p = part[g];
+        p.res.assign(p.iov.size(), 0);
         std::unique_lock<std::mutex> lk;
         Lane &ln = ds[g]->acquire_lane(lk);
-        run_isolated(ds[g], ln, algo, dir, (int)part[g].size(), part[g].data(), res[g].data());
+        if (ae_all) {
+            Aead a{ae_all->cipher, ae_all->seal, p.orig.data(), p.key.data(), p.nonce.data(),
+                   ae_all->sp ? p.sp.data() : nullptr, ae_all->hdr ? p.hdr.data() : nullptr};
+            run_isolated(ds[g], ln, algo, dir, (int)p.iov.size(), p.iov.data(), p.res.data(), &a);
+        } else {
+            run_isolated(ds[g], ln, algo, dir, (int)p.iov.size(), p.iov.data(), p.res.data());
+        }
     };
     if (G == 1) work(0);
     else {
@@ -877,8 +1063,32 @@ int64_t batch_common(int algo, int dir, int nblk, const jfs_iov *iov, int64_t *o
         for (auto &t : th) t.join();
     }
     for (size_t g = 0; g < G; g++)
-        for (size_t k = 0; k < idx[g].size(); k++) out_n[idx[g][k]] = res[g][k];
+        for (size_t k = 0; k < part[g].idx.size(); k++) out_n[part[g].idx[k]] = part[g].res[k];
     return JFS_OK;
+}
+
+int64_t envelope_parse(const uint8_t *src, int64_t n, int64_t *woff, int64_t *wlen, int64_t *noff, int64_t *nlen) {
+    if (!src || n < 3) return JFS_ERR_CORRUPT;  // "received encrypted text length is less than 3"
+    const int64_t kl = ((int64_t)src[0] << 8) + src[1], nl = src[2];
+    if (3 + kl + nl >= n) return JFS_ERR_CORRUPT;  // "malformed ciphertext"
+    if (woff) *woff = 3;
+    if (wlen) *wlen = kl;
+    if (noff) *noff = 3 + kl;
+    if (nlen) *nlen = nl;
+    return 3 + kl + nl;
+}
+
+int64_t batch_common(int algo, int dir, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t mask) {
+    if (nblk < 0 || (nblk > 0 && (!iov || !out_n))) return JFS_ERR_INVALID;
+    if (algo != JFS_ALGO_NONE && algo != JFS_ALGO_LZ4 && algo != JFS_ALGO_ZSTD) return JFS_ERR_INVALID;
+    std::vector<int> todo;
+    for (int i = 0; i < nblk; i++) {
+        if (!pre_answer(algo, dir, iov[i], &out_n[i])) todo.push_back(i);
+    }
+    if (todo.empty()) return JFS_OK;
+    std::vector<jfs_iov> iov2(todo.size());
+    for (size_t k = 0; k < todo.size(); k++) iov2[k] = iov[todo[k]];
+    return deal(algo, dir, todo, iov2, out_n, mask, nullptr);
 }
 
 }  // namespace
@@ -952,6 +1162,135 @@ static int64_t batch_call(int algo, int dir, int nblk, const jfs_iov *iov, int64
         st->nanos.fetch_add((uint64_t)(steady_ns() - t0), std::memory_order_relaxed);
     }
     return r;
+}
+
+int64_t jfs_envelope_bound(int algo, int64_t n, int32_t wrapped_len) {
+    if (n < 0 || wrapped_len < 0 || wrapped_len > 65535) return JFS_ERR_INVALID;
+    const int64_t b = algo == JFS_ALGO_NONE ? n : jfs_compress_bound(algo, n);
+    if (b < 0) return b;
+    return 3 + wrapped_len + 12 + b + 16;
+}
+
+int64_t jfs_envelope_parse(const uint8_t *src, int64_t n, int64_t *wrapped_off, int64_t *wrapped_len,
+                           int64_t *nonce_off, int64_t *nonce_len) {
+    return envelope_parse(src, n, wrapped_off, wrapped_len, nonce_off, nonce_len);
+}
+
+int64_t jfs_compress_seal_batch(int algo, int cipher, int nblk, const jfs_iov *iov, const jfs_seal_param *p,
+                                int64_t *out_n, uint32_t device_mask) {
+    if (nblk < 0 || (nblk > 0 && (!iov || !out_n || !p))) return JFS_ERR_INVALID;
+    if (algo != JFS_ALGO_NONE && algo != JFS_ALGO_LZ4 && algo != JFS_ALGO_ZSTD) return JFS_ERR_INVALID;
+    if (jfs_cipher_key_size(cipher) < 0) return JFS_ERR_INVALID;
+    const int64_t t0 = steady_ns();
+    std::vector<int> todo;
+    std::vector<jfs_iov> iov2, orig;
+    std::vector<const uint8_t *> key, nonce;
+    std::vector<jfs_seal_param> sp;
+    std::vector<int64_t> hdr;
+    for (int i = 0; i < nblk; i++) {
+        const jfs_iov &v = iov[i];
+        const jfs_seal_param &q = p[i];
+        const int64_t bound = jfs_envelope_bound(algo, v.src_len, q.wrapped_len);
+        if (v.src_len < 0 || v.dst_cap < 0 || !q.key || !q.nonce || bound < 0 || (q.wrapped_len > 0 && !q.wrapped) ||
+            (v.src_len > 0 && !v.src)) {
+            out_n[i] = JFS_ERR_INVALID;
+            continue;
+        }
+        if (algo == JFS_ALGO_LZ4 && v.src_len > LZ4_MAX_INPUT) {
+            out_n[i] = JFS_ERR_COMPRESS_FAIL;
+            continue;
+        }
+        if (v.dst_cap < bound) {
+            out_n[i] = JFS_ERR_SHORT_BUFFER;
+            continue;
+        }
+        todo.push_back(i);
+        const int64_t pay = bound - (3 + q.wrapped_len + 12);  // codec bound + tag
+        iov2.push_back(jfs_iov{v.src, v.src_len, nullptr, pay});
+        orig.push_back(v);
+        key.push_back(q.key);
+        nonce.push_back(q.nonce);
+        sp.push_back(q);
+        hdr.push_back(3 + q.wrapped_len + 12);
+    }
+    int64_t rc = JFS_OK;
+    if (!todo.empty()) {
+        Aead ae{cipher, true, orig.data(), key.data(), nonce.data(), sp.data(), hdr.data()};
+        rc = deal(algo, COMPRESS, todo, iov2, out_n, device_mask, &ae);
+    }
+    if (OpStats *st = op_stats(algo, COMPRESS)) {
+        st->calls.fetch_add(1, std::memory_order_relaxed);
+        if (rc == JFS_OK)
+            for (int i = 0; i < nblk; i++) stat_block(st, iov[i].src_len, out_n[i]);
+        st->nanos.fetch_add((uint64_t)(steady_ns() - t0), std::memory_order_relaxed);
+    }
+    return rc;
+}
+
+int64_t jfs_open_decompress_batch(int algo, int cipher, int nblk, const jfs_iov *iov, const uint8_t *const *keys,
+                                  int64_t *out_n, uint32_t device_mask) {
+    if (nblk < 0 || (nblk > 0 && (!iov || !out_n || !keys))) return JFS_ERR_INVALID;
+    if (algo != JFS_ALGO_NONE && algo != JFS_ALGO_LZ4 && algo != JFS_ALGO_ZSTD) return JFS_ERR_INVALID;
+    if (jfs_cipher_key_size(cipher) < 0) return JFS_ERR_INVALID;
+    const int64_t t0 = steady_ns();
+    std::vector<int> todo;
+    std::vector<jfs_iov> iov2, orig;
+    std::vector<const uint8_t *> key, nonce;
+    for (int i = 0; i < nblk; i++) {
+        const jfs_iov &v = iov[i];
+        int64_t noff = 0, nlen = 0;
+        const int64_t off = envelope_parse(v.src, v.src_len, nullptr, nullptr, &noff, &nlen);
+        if (v.dst_cap < 0 || !keys[i]) {
+            out_n[i] = JFS_ERR_INVALID;
+            continue;
+        }
+        if (off < 0 || nlen != 12) {  // the AEADs here all take 12-byte nonces
+            out_n[i] = JFS_ERR_CORRUPT;
+            continue;
+        }
+        const int64_t pay = v.src_len - off;  // ciphertext || tag
+        if (pay < 16) {
+            out_n[i] = JFS_ERR_AUTH;  // aead.Open rejects a payload shorter than the tag
+            continue;
+        }
+        if (algo != JFS_ALGO_NONE && pay == 16) {  // the codec would see an empty input
+            out_n[i] = JFS_ERR_EMPTY_INPUT;
+            continue;
+        }
+        int64_t cap;
+        if (algo == JFS_ALGO_NONE) {
+            if (v.dst_cap < pay - 16) {  // noOp.Decompress: "buffer too short" (compress.go:63-65)
+                out_n[i] = JFS_ERR_SHORT_BUFFER;
+                continue;
+            }
+            cap = pay - 16;
+        } else if (algo == JFS_ALGO_ZSTD) {
+            // DataDog's size hint reads the frame header, which is still
+            // ciphertext here: stage dst_cap (frames from pkg/compress carry
+            // their content size, for which both rules agree)
+            cap = std::min<int64_t>(v.dst_cap, INT32_MAX);
+        } else {
+            jfs_iov pv{v.src + off, pay - 16, v.dst, v.dst_cap};
+            cap = staged_cap(algo, DECOMPRESS, pv);
+        }
+        todo.push_back(i);
+        iov2.push_back(jfs_iov{v.src + off, pay, nullptr, cap});
+        orig.push_back(v);
+        key.push_back(keys[i]);
+        nonce.push_back(v.src + noff);
+    }
+    int64_t rc = JFS_OK;
+    if (!todo.empty()) {
+        Aead ae{cipher, false, orig.data(), key.data(), nonce.data(), nullptr, nullptr};
+        rc = deal(algo, DECOMPRESS, todo, iov2, out_n, device_mask, &ae);
+    }
+    if (OpStats *st = op_stats(algo, DECOMPRESS)) {
+        st->calls.fetch_add(1, std::memory_order_relaxed);
+        if (rc == JFS_OK)
+            for (int i = 0; i < nblk; i++) stat_block(st, iov[i].src_len, out_n[i]);
+        st->nanos.fetch_add((uint64_t)(steady_ns() - t0), std::memory_order_relaxed);
+    }
+    return rc;
 }
 
 int64_t jfs_compress_batch(int algo, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t device_mask) {
