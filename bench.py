@@ -49,6 +49,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+ZSTD_FRAMES = []  # configs[3]'s distinct frames (host copies) for its CPU leg
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 METRIC = "device-resident GiB/s (de)compress, 4 MiB blocks, LZ4+Zstd, 1/2/4/8 MI355X"
 KERNEL_SOURCES = ("juicefs_amd/csrc/lz4_decode.hip", "juicefs_amd/csrc/wave.cuh", "juicefs_amd/csrc/jfs_internal.h")
@@ -210,6 +211,57 @@ def libzstd_baseline(comp_blocks, U, seconds):
     nb, dt = _timed_threads(one, T, seconds)
     return {"value": nb * U / dt / 2**30, "unit": "GiB/s", "cores": T, "kind": "reference",
             "library": f"{z.path} v{z.ZSTD_versionNumber()}"}
+
+
+def cpu_codec_legs(raw_blocks, comp_blocks, zstd_frames, U, seconds):
+    """The C routines pkg/compress reaches, on this host's cores (one block
+    stream per thread; 16 threads and 1 core), beside every GPU leg -- the
+    reference's own harness times both directions of both codecs
+    (pkg/compress/compress_test.go:78-151): LZ4_compress_default,
+    ZSTD_compress(level 1), ZSTD_decompress (the configs[3] level-3 frames).
+    GiB/s of uncompressed bytes."""
+    from juicefs_amd.device import _libzstd
+    lz, z = _liblz4(), _libzstd()
+    out = {}
+    T = host_threads()
+    bound = U + U // 255 + 16
+    zbound = U + (U >> 8) + 64
+    raws = [ctypes.create_string_buffer(r, len(r)) for r in raw_blocks]
+
+    def leg(one, threads, secs):
+        nb, dt = _timed_threads(one, threads, secs)
+        return nb * U / dt / 2**30
+
+    if lz is not None:
+        outs = [ctypes.create_string_buffer(bound) for _ in range(T)]
+
+        def lz4c(t, k):
+            r = raws[k % len(raws)]
+            assert lz.LZ4_compress_default(r, outs[t], U, bound) > 0
+        out["lz4_compress"] = {"value": leg(lz4c, T, seconds), "unit": "GiB/s", "cores": T,
+                               "one_core": leg(lz4c, 1, seconds / 3), "library": f"{lz.path}"}
+    if z is not None:
+        z.ZSTD_compress.restype = ctypes.c_size_t
+        zouts = [ctypes.create_string_buffer(zbound) for _ in range(T)]
+
+        def zc(t, k):
+            r = raws[k % len(raws)]
+            assert z.ZSTD_compress(zouts[t], zbound, r, U, 1) < (1 << 40)
+        out["zstd1_compress"] = {"value": leg(zc, T, seconds), "unit": "GiB/s", "cores": T,
+                                 "one_core": leg(zc, 1, seconds / 3), "library": f"{z.path}"}
+        if zstd_frames:
+            fr = [ctypes.create_string_buffer(f, len(f)) for f in zstd_frames]
+            douts = [ctypes.create_string_buffer(U) for _ in range(T)]
+
+            def zd(t, k):
+                f = fr[k % len(fr)]
+                assert z.ZSTD_decompress(douts[t], U, f, len(f)) == U
+            out["zstd_decompress_configs3"] = {"value": leg(zd, T, seconds), "unit": "GiB/s", "cores": T,
+                                               "one_core": leg(zd, 1, seconds / 3), "library": f"{z.path}",
+                                               "sample": f"{len(fr)} distinct level-3 frames of configs[3]"}
+    out["note"] = ("host C libraries (liblz4 1.9.3 / libzstd 1.4.9 of this image; the reference pins go-lz4 2017 "
+                   "and zstd 1.5.6), bounded samples of 32 distinct 4 MiB text blocks")
+    return out
 
 
 # ---------------------------------------------------------------------------
@@ -435,6 +487,9 @@ def configs3_zstd(a, S, world, rank, dev):
     if not S.all_ranks_ok(zb.verify(), world, dev):
         raise RuntimeError("configs[3] decoded output mismatch")
     U = a.block_bytes
+    global ZSTD_FRAMES
+    ZSTD_FRAMES = [zb.comp[i * zb.slot:i * zb.slot + int(zb.csize[i])].cpu().numpy().tobytes()
+                   for i in range(min(16, a.blocks))]
     return {"config": f"Zstd level-{a.level} decode, {a.blocks}x4MiB frames in HBM per GPU (BASELINE configs[3])",
             "value": S.whole_job_gib_s(world, a.blocks, U, a.zstd_steps, el), "unit": "GiB/s",
             "ms_per_step": el / a.zstd_steps * 1e3, "steps": a.zstd_steps, "n_gpus": world,
@@ -503,6 +558,17 @@ def checksum_and_aead(batch, S, world, dev):
     if not bool((aret.cpu().numpy().astype(np.int64) == batch.csize + 16).all()):
         raise RuntimeError("AES-GCM seal failed")
     C = int(batch.csize.sum())
+    for name in ("chacha20", "sm4gcm"):
+        r2 = torch.empty(n, dtype=torch.int32, device=dev)
+        el2, kms2 = timed_launches(lambda st, nm=name: D.aead(nm, adesc, r2, True, stream=st), 3, 1, S, world, dev)
+        if not bool((r2.cpu().numpy().astype(np.int64) == batch.csize + 16).all()):
+            raise RuntimeError(f"{name} seal failed")
+        out[f"{name}_seal"] = {"value": world * C * 3 / el2 / 2**30, "unit": "GiB/s", "kernel_ms": kms2,
+                               "roofline": {"bound": "hbm", "achieved": 2 * C / (kms2 / 1e3) / 1e9,
+                                            "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                            "frac": 2 * C / (kms2 / 1e3) / 1e9 / HBM_PEAK_GBS},
+                               "workload": f"{n} compressed blocks, one key/nonce per block (encrypt.go "
+                                           f"{'CHACHA20_RSA' if name == 'chacha20' else 'SM4GCM'}); GiB/s of plaintext"}
     out["aes256gcm_seal"] = {"value": world * C * 3 / el / 2**30, "unit": "GiB/s", "kernel_ms": kms,
                              "roofline": {"bound": "hbm", "achieved": 2 * C / (kms / 1e3) / 1e9, "peak": HBM_PEAK_GBS,
                                           "unit": "GB/s", "frac": 2 * C / (kms / 1e3) / 1e9 / HBM_PEAK_GBS},
@@ -671,6 +737,12 @@ def main():
             except Exception as e:  # report, never fake
                 ex["zstd_compress"] = {"error": repr(e)}
             out["compress"] = ex
+            if not a.no_cpu_baseline:
+                try:
+                    rb = [batch.raw[i * U:(i + 1) * U].cpu().numpy().tobytes() for i in range(ns)]
+                    out["cpu_codecs"] = cpu_codec_legs(rb, comp_blocks, ZSTD_FRAMES, U, a.cpu_seconds / 2)
+                except Exception as e:
+                    out["cpu_codecs"] = {"error": repr(e)}
             if not a.no_host_path:
                 raw_blocks = [batch.raw[i * U:(i + 1) * U].cpu().numpy().tobytes() for i in range(ns)]
                 try:

@@ -96,6 +96,12 @@ typedef struct jfs_iov {
 } jfs_iov;
 
 int64_t jfs_compress_batch(int algo, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t device_mask);
+/* jfs_compress_batch plus crc[i] = crc32.Update(0, crc32c, dst[0:out_n[i]]) -- the
+ * object checksum generateChecksum attaches to the PUT (pkg/object/checksum.go:
+ * 30-45) -- computed on the GPU over the compressed payload before it leaves
+ * HBM (0 for a block that failed).  For "none" the payload is the block itself. */
+int64_t jfs_compress_batch_crc(int algo, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t *crc,
+                               uint32_t device_mask);
 int64_t jfs_decompress_batch(int algo, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t device_mask);
 
 /* ---- Encrypted objects (host buffers): compress + seal, open + decompress --
@@ -131,8 +137,10 @@ int64_t jfs_envelope_bound(int algo, int64_t n, int32_t wrapped_len);
  * n < 3 or 3 + wrapped_len + nonce_len >= n. */
 int64_t jfs_envelope_parse(const uint8_t *src, int64_t n, int64_t *wrapped_off, int64_t *wrapped_len,
                            int64_t *nonce_off, int64_t *nonce_len);
+/* crc (optional, may be NULL): per block the CRC-32C of the whole envelope
+ * (generateChecksum of the PUT payload), computed on the GPU. */
 int64_t jfs_compress_seal_batch(int algo, int cipher, int nblk, const jfs_iov *iov, const jfs_seal_param *p,
-                                int64_t *out_n, uint32_t device_mask);
+                                int64_t *out_n, uint32_t *crc, uint32_t device_mask);
 int64_t jfs_open_decompress_batch(int algo, int cipher, int nblk, const jfs_iov *iov, const uint8_t *const *keys,
                                   int64_t *out_n, uint32_t device_mask);
 

@@ -112,6 +112,11 @@ class Compressor:
     def DecompressBatch(self, pairs, device_mask: int = 0):
         return _batch(self.algo, pairs, device_mask, compress=False)
 
+    def CompressBatchChecksum(self, pairs, device_mask: int = 0):
+        """CompressBatch plus each payload's CRC-32C (generateChecksum,
+        pkg/object/checksum.go:30-45): [(n, err, crc)]"""
+        return _batch(self.algo, pairs, device_mask, compress=True, with_crc=True)
+
 
 class noOp(Compressor):  # noqa: N801  (reference name, compress.go:51)
     algo = L.ALGO_NONE
@@ -144,7 +149,7 @@ def NewCompressor(algr: str):
     return None
 
 
-def _batch(algo: int, pairs, device_mask: int, compress: bool):
+def _batch(algo: int, pairs, device_mask: int, compress: bool, with_crc: bool = False):
     """pairs: list of (dst, src).  Returns list of (n, err)."""
     lib = L.load()
     nb = len(pairs)
@@ -156,8 +161,12 @@ def _batch(algo: int, pairs, device_mask: int, compress: bool):
         keep.append((kd, ks))
         iov[i].src, iov[i].src_len, iov[i].dst, iov[i].dst_cap = s, sn, d, dn
     out = (ctypes.c_int64 * max(nb, 1))()
-    fn = lib.jfs_compress_batch if compress else lib.jfs_decompress_batch
-    rc = fn(algo, nb, iov, out, device_mask)
+    crc = (ctypes.c_uint32 * max(nb, 1))()
+    if with_crc:
+        rc = lib.jfs_compress_batch_crc(algo, nb, iov, out, crc, device_mask)
+    else:
+        fn = lib.jfs_compress_batch if compress else lib.jfs_decompress_batch
+        rc = fn(algo, nb, iov, out, device_mask)
     if rc != 0:
         raise _err(rc, 0, 0, "batch")
     res = []
@@ -168,4 +177,6 @@ def _batch(algo: int, pairs, device_mask: int, compress: bool):
             res.append((n, _err(r, iov[i].dst_cap, iov[i].src_len, "compress" if compress else "decompress")))
         else:
             res.append((r, None))
+    if with_crc:
+        return [(n, e, int(crc[i])) for i, (n, e) in enumerate(res)]
     return res

@@ -362,6 +362,24 @@ void start_janitor() {
     });
 }
 
+// crc32.Update(crc, crc32c, p[0:n]) on the host (pkg/object/checksum.go:30-45):
+// table-driven, for the few hundred header bytes of an envelope and the
+// "none" codec; block payloads are summed by crc32c.hip
+uint32_t host_crc32c(uint32_t crc, const uint8_t *p, int64_t n) {
+    static uint32_t tab[256];
+    static std::once_flag once;
+    std::call_once(once, [] {
+        for (uint32_t i = 0; i < 256; i++) {
+            uint32_t c = i;
+            for (int k = 0; k < 8; k++) c = (c >> 1) ^ ((c & 1u) ? 0x82F63B78u : 0u);
+            tab[i] = c;
+        }
+    });
+    crc = ~crc;
+    for (int64_t i = 0; i < n; i++) crc = tab[(crc ^ p[i]) & 255u] ^ (crc >> 8);
+    return ~crc;
+}
+
 enum Dir { COMPRESS = 0, DECOMPRESS = 1 };
 constexpr int COMPRESS_DIR = COMPRESS, DECOMPRESS_DIR = DECOMPRESS;
 
@@ -523,7 +541,7 @@ struct Aead {
 // batch is not cut finer than that (a decode kernel over fewer blocks than
 // CUs lasts about one block's latency whatever its size).
 int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_iov *iov, int64_t *out,
-                  const Aead *ae = nullptr) {
+                  const Aead *ae = nullptr, uint32_t *crc_out = nullptr) {
     if (nblk <= 0) return JFS_OK;
     DevGuard guard;
     (void)hipSetDevice(dev->id);
@@ -536,17 +554,24 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
         DevCtx *d;
         ~Touch() { d->last_use_ms = steady_ms(); }
     } touch{dev};
+    // Chunk kernels alternate between this lane's kernel stream and the other
+    // lane's: an encode launch lasts one block's latency (~0.5 s) whatever its
+    // size, so two chunks' kernels must run side by side (a device has only
+    // two kernel streams: see Lane).
+    Lane &other = dev->lane[(&ln - dev->lane + 1) % NLANE];
+    auto kstream = [&](int chunk) { return (chunk & 1) ? other.s_k : ln.s_k; };
     std::vector<int64_t> cap(nblk), in_off(nblk), out_off(nblk);
     struct Chunk {
         int s, e, slot;
         int64_t tin, tout;
+        hipStream_t ks;  // its kernel stream
     };
     std::vector<Chunk> ch;
     {
         const int64_t limit = chunk_limit();
         int s = 0;
         while (s < nblk) {
-            Chunk c{s, s, (int)(ch.size() % NSLOT), 0, 0};
+            Chunk c{s, s, (int)(ch.size() % NSLOT), 0, 0, kstream((int)ch.size())};
             while (c.e < nblk) {
                 const int64_t ci = ae ? iov[c.e].dst_cap : staged_cap(algo, dir, iov[c.e]);
                 const int64_t ib = align16(iov[c.e].src_len), ob = align16(ci);  // = staged_bytes()
@@ -588,10 +613,67 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
         p += align16(nb * 4);
         *kn = p;
     };
+    auto aead_bytes = [&](int64_t nb) {
+        return ae ? align16(nb * (int64_t)sizeof(jfs_aead_block)) + align16(nb * 4) + align16(nb * 64) : 0;
+    };
+    // PUT-payload checksums: descriptors, seeds, results (after the aead area)
+    auto crc_layout = [&](const Chunk &c, uint8_t *base, jfs_dev_block **cd, uint32_t **seed, uint32_t **crc) {
+        const int64_t nb = c.e - c.s;
+        uint8_t *p = base + c.tin + c.tout + align16(nb * (int64_t)sizeof(jfs_dev_block)) + align16(nb * 4) +
+                     align16(nb * zib) + aead_bytes(nb);
+        *cd = (jfs_dev_block *)p;
+        p += align16(nb * (int64_t)sizeof(jfs_dev_block));
+        *seed = (uint32_t *)p;
+        p += align16(nb * 4);
+        *crc = (uint32_t *)p;
+    };
     auto chunk_bytes = [&](const Chunk &c) {
         const int64_t nb = c.e - c.s;
         return c.tin + c.tout + align16(nb * (int64_t)sizeof(jfs_dev_block)) + align16(nb * 4) + align16(nb * zib) +
-               (ae ? align16(nb * (int64_t)sizeof(jfs_aead_block)) + align16(nb * 4) + nb * 64 : 0);
+               aead_bytes(nb) + (crc_out ? align16(nb * (int64_t)sizeof(jfs_dev_block)) + 2 * align16(nb * 4) : 0);
+    };
+    // stage the checksum descriptors (payload = the codec's output area) and
+    // queue their H2D on s_in; seeds: the envelope header's CRC for a seal
+    auto stage_crc = [&](const Chunk &c, Slot &sl, uint8_t *d_out) -> int64_t {
+        if (!crc_out) return JFS_OK;
+        const int n = c.e - c.s;
+        jfs_dev_block *h_cd, *d_cd;
+        uint32_t *h_seed, *d_seed, *h_crc, *d_crc;
+        crc_layout(c, sl.h, &h_cd, &h_seed, &h_crc);
+        crc_layout(c, sl.d, &d_cd, &d_seed, &d_crc);
+        for (int k = 0; k < n; k++) {
+            const int i = c.s + k;
+            h_cd[k] = jfs_dev_block{d_out + out_off[i], nullptr, 0, 0};
+            h_seed[k] = 0;
+            if (ae && ae->seal) {
+                const jfs_seal_param &p = ae->sp[i];
+                const uint8_t h3[3] = {(uint8_t)(p.wrapped_len >> 8), (uint8_t)(p.wrapped_len & 0xFF), 12};
+                uint32_t v = host_crc32c(0, h3, 3);
+                v = host_crc32c(v, p.wrapped, p.wrapped_len);
+                h_seed[k] = host_crc32c(v, ae->nonce[i], 12);
+            }
+        }
+        const size_t bytes = (size_t)(align16((int64_t)n * (int64_t)sizeof(jfs_dev_block)) + align16((int64_t)n * 4));
+        return hipMemcpyAsync(d_cd, h_cd, bytes, hipMemcpyHostToDevice, dev->s_in) == hipSuccess ? JFS_OK : JFS_ERR_HIP;
+    };
+    // after the kernels: the checksum launch (lengths from the device) and its D2H
+    auto run_crc = [&](const Chunk &c, Slot &sl, const int32_t *d_lens) -> int64_t {
+        if (!crc_out) return JFS_OK;
+        const int n = c.e - c.s;
+        jfs_dev_block *d_cd;
+        uint32_t *d_seed, *d_crc;
+        crc_layout(c, sl.d, &d_cd, &d_seed, &d_crc);
+        return jfs_launch_crc32c_lens(d_cd, n, d_lens, d_seed, d_crc, c.ks) == 0 ? JFS_OK : JFS_ERR_HIP;
+    };
+    auto fetch_crc = [&](const Chunk &c, Slot &sl) -> int64_t {
+        if (!crc_out) return JFS_OK;
+        jfs_dev_block *h_cd, *d_cd;
+        uint32_t *h_seed, *d_seed, *h_crc, *d_crc;
+        crc_layout(c, sl.h, &h_cd, &h_seed, &h_crc);
+        crc_layout(c, sl.d, &d_cd, &d_seed, &d_crc);
+        return hipMemcpyAsync(h_crc, d_crc, (size_t)(c.e - c.s) * 4, hipMemcpyDeviceToHost, dev->s_out) == hipSuccess
+                   ? JFS_OK
+                   : JFS_ERR_HIP;
     };
     (void)aeb;
     // compress -> seal, or open -> decompress (the staged inputs and the
@@ -630,21 +712,22 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
                 a.dst_cap = algo == JFS_ALGO_NONE ? (int32_t)cap[i] : (int32_t)iov[i].src_len;
             }
         }
-        const int64_t ab = align16((int64_t)n * (int64_t)sizeof(jfs_aead_block)) + align16((int64_t)n * 4) + n * 64;
+        const int64_t ab = aead_bytes(n);
         if (hipMemcpyAsync(d_in, h_in, (size_t)c.tin, hipMemcpyHostToDevice, dev->s_in) != hipSuccess) return JFS_ERR_HIP;
         if (hipMemcpyAsync(d_desc, h_desc, (size_t)n * sizeof(jfs_dev_block), hipMemcpyHostToDevice, dev->s_in) !=
             hipSuccess)
             return JFS_ERR_HIP;
         if (hipMemcpyAsync(d_ad, h_ad, (size_t)ab, hipMemcpyHostToDevice, dev->s_in) != hipSuccess) return JFS_ERR_HIP;
+        if (stage_crc(c, sl, d_out) != JFS_OK) return JFS_ERR_HIP;
         if (hipEventRecord(sl.ev_in, dev->s_in) != hipSuccess) return JFS_ERR_HIP;
-        if (hipStreamWaitEvent(ln.s_k, sl.ev_in, 0) != hipSuccess) return JFS_ERR_HIP;
+        if (hipStreamWaitEvent(c.ks, sl.ev_in, 0) != hipSuccess) return JFS_ERR_HIP;
         int lk = 0;
         if (ae->seal) {
-            if (algo != JFS_ALGO_NONE) lk = launch_kernel(algo, COMPRESS, d_desc, n, d_ret, ln.s_k);
+            if (algo != JFS_ALGO_NONE) lk = launch_kernel(algo, COMPRESS, d_desc, n, d_ret, c.ks);
             if (lk == 0)
-                lk = jfs_launch_aead(ae->cipher, d_ad, n, 0, d_r2, algo != JFS_ALGO_NONE ? d_ret : nullptr, ln.s_k);
+                lk = jfs_launch_aead(ae->cipher, d_ad, n, 0, d_r2, algo != JFS_ALGO_NONE ? d_ret : nullptr, c.ks);
         } else {
-            lk = jfs_launch_aead(ae->cipher, d_ad, n, 1, d_r2, nullptr, ln.s_k);
+            lk = jfs_launch_aead(ae->cipher, d_ad, n, 1, d_r2, nullptr, c.ks);
             if (lk == 0 && algo == JFS_ALGO_LZ4) {
                 if (n <= split_max()) {
                     std::vector<int32_t> lens(n), caps(n);
@@ -657,22 +740,24 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
                     }
                     if (!sl.ensure_split(jfs_lz4_split_scratch_bytes(n, lens.data(), caps.data())))
                         return JFS_ERR_NO_MEMORY;
-                    lk = jfs_launch_lz4_split(d_desc, n, d_ret, sl.sp, nseg, max_cap, ln.s_k);
+                    lk = jfs_launch_lz4_split(d_desc, n, d_ret, sl.sp, nseg, max_cap, c.ks);
                 } else {
-                    lk = jfs_launch_lz4_decode(d_desc, n, d_ret, ln.s_k);
+                    lk = jfs_launch_lz4_decode(d_desc, n, d_ret, c.ks);
                 }
             } else if (lk == 0 && algo == JFS_ALGO_ZSTD) {
                 // the host holds ciphertext only: the device API plans the scratch itself
-                lk = jfs_launch_zstd_decode(d_desc, n, d_ret, nullptr, ln.s_k);
+                lk = jfs_launch_zstd_decode(d_desc, n, d_ret, nullptr, c.ks);
             }
         }
         if (lk != 0) return JFS_ERR_HIP;
-        if (hipEventRecord(sl.ev_k, ln.s_k) != hipSuccess) return JFS_ERR_HIP;
+        if (ae->seal && run_crc(c, sl, d_r2) != JFS_OK) return JFS_ERR_HIP;
+        if (hipEventRecord(sl.ev_k, c.ks) != hipSuccess) return JFS_ERR_HIP;
         if (hipStreamWaitEvent(dev->s_out, sl.ev_k, 0) != hipSuccess) return JFS_ERR_HIP;
         if (hipMemcpyAsync(h_ret, d_ret, (size_t)n * 4, hipMemcpyDeviceToHost, dev->s_out) != hipSuccess)
             return JFS_ERR_HIP;
         if (hipMemcpyAsync(h_r2, d_r2, (size_t)n * 4, hipMemcpyDeviceToHost, dev->s_out) != hipSuccess)
             return JFS_ERR_HIP;
+        if (ae->seal && fetch_crc(c, sl) != JFS_OK) return JFS_ERR_HIP;
         if (hipMemcpyAsync(h_out, d_out, (size_t)c.tout, hipMemcpyDeviceToHost, dev->s_out) != hipSuccess)
             return JFS_ERR_HIP;
         if (hipEventRecord(sl.ev, dev->s_out) != hipSuccess) return JFS_ERR_HIP;
@@ -720,11 +805,12 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
             return JFS_ERR_HIP;
         if (zplan && hipMemcpyAsync(d_zi, h_zi, (size_t)(n * zib), hipMemcpyHostToDevice, dev->s_in) != hipSuccess)
             return JFS_ERR_HIP;
+        if (dir == COMPRESS && stage_crc(c, sl, d_out) != JFS_OK) return JFS_ERR_HIP;
         if (hipEventRecord(sl.ev_in, dev->s_in) != hipSuccess) return JFS_ERR_HIP;
-        if (hipStreamWaitEvent(ln.s_k, sl.ev_in, 0) != hipSuccess) return JFS_ERR_HIP;
+        if (hipStreamWaitEvent(c.ks, sl.ev_in, 0) != hipSuccess) return JFS_ERR_HIP;
         int lk;
         if (zplan) {
-            lk = jfs_launch_zstd_decode_planned(d_desc, n, d_ret, d_zi, sl.z_lit, sl.z_tabs, sl.z_items, ln.s_k);
+            lk = jfs_launch_zstd_decode_planned(d_desc, n, d_ret, d_zi, sl.z_lit, sl.z_tabs, sl.z_items, c.ks);
         } else if (algo == JFS_ALGO_LZ4 && dir == DECOMPRESS && n <= split_max()) {
             std::vector<int32_t> lens(n), caps(n);
             int64_t nseg = 0, max_cap = 0;
@@ -735,15 +821,17 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
                 max_cap = std::max<int64_t>(max_cap, caps[k]);
             }
             if (!sl.ensure_split(jfs_lz4_split_scratch_bytes(n, lens.data(), caps.data()))) return JFS_ERR_NO_MEMORY;
-            lk = jfs_launch_lz4_split(d_desc, n, d_ret, sl.sp, nseg, max_cap, ln.s_k);
+            lk = jfs_launch_lz4_split(d_desc, n, d_ret, sl.sp, nseg, max_cap, c.ks);
         } else {
-            lk = launch_kernel(algo, dir, d_desc, n, d_ret, ln.s_k);
+            lk = launch_kernel(algo, dir, d_desc, n, d_ret, c.ks);
         }
         if (lk != 0) return JFS_ERR_HIP;
-        if (hipEventRecord(sl.ev_k, ln.s_k) != hipSuccess) return JFS_ERR_HIP;
+        if (dir == COMPRESS && run_crc(c, sl, d_ret) != JFS_OK) return JFS_ERR_HIP;
+        if (hipEventRecord(sl.ev_k, c.ks) != hipSuccess) return JFS_ERR_HIP;
         if (hipStreamWaitEvent(dev->s_out, sl.ev_k, 0) != hipSuccess) return JFS_ERR_HIP;
         if (hipMemcpyAsync(h_ret, d_ret, (size_t)n * 4, hipMemcpyDeviceToHost, dev->s_out) != hipSuccess)
             return JFS_ERR_HIP;
+        if (dir == COMPRESS && fetch_crc(c, sl) != JFS_OK) return JFS_ERR_HIP;
         if (hipMemcpyAsync(h_out, d_out, (size_t)c.tout, hipMemcpyDeviceToHost, dev->s_out) != hipSuccess)
             return JFS_ERR_HIP;
         if (hipEventRecord(sl.ev, dev->s_out) != hipSuccess) return JFS_ERR_HIP;
@@ -803,6 +891,12 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
                 out[i] = r;
             }
         }
+        if (crc_out) {
+            jfs_dev_block *h_cd;
+            uint32_t *h_seed, *h_crc;
+            crc_layout(c, sl.h, &h_cd, &h_seed, &h_crc);
+            for (int i = c.s; i < c.e; i++) crc_out[i] = out[i] >= 0 ? h_crc[i - c.s] : 0u;
+        }
         par_copy(jobs);
         if (host_trace())
             fprintf(stderr, "[jfs host] chunk %d-%d wait %.2f ms copy-out %.1f MiB %.2f ms\n", c.s, c.e, t1 - t0,
@@ -820,6 +914,7 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
     if (rc != JFS_OK) {  // leave no copy in flight into the staging slots
         (void)hipStreamSynchronize(dev->s_in);
         (void)hipStreamSynchronize(ln.s_k);
+        (void)hipStreamSynchronize(other.s_k);
         (void)hipStreamSynchronize(dev->s_out);
     }
     return rc;
@@ -840,21 +935,21 @@ bool lane_healthy(DevCtx *dev, Lane &ln) {
 }
 
 void run_isolated(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_iov *iov, int64_t *out,
-                  const Aead *ae = nullptr) {
+                  const Aead *ae = nullptr, uint32_t *crc = nullptr) {
     if (nblk <= 0) return;
-    const int64_t rc = run_batch(dev, ln, algo, dir, nblk, iov, out, ae);
+    const int64_t rc = run_batch(dev, ln, algo, dir, nblk, iov, out, ae, crc);
     if (rc == JFS_OK) return;
     if (nblk == 1 || (rc == JFS_ERR_HIP && !lane_healthy(dev, ln))) {
         for (int i = 0; i < nblk; i++) out[i] = rc;
         return;
     }
     const int h = nblk / 2;
-    run_isolated(dev, ln, algo, dir, h, iov, out, ae);
+    run_isolated(dev, ln, algo, dir, h, iov, out, ae, crc);
     if (ae) {
         const Aead a2 = ae->at(h);
-        run_isolated(dev, ln, algo, dir, nblk - h, iov + h, out + h, &a2);
+        run_isolated(dev, ln, algo, dir, nblk - h, iov + h, out + h, &a2, crc ? crc + h : nullptr);
     } else {
-        run_isolated(dev, ln, algo, dir, nblk - h, iov + h, out + h);
+        run_isolated(dev, ln, algo, dir, nblk - h, iov + h, out + h, nullptr, crc ? crc + h : nullptr);
     }
 }
 
@@ -1016,7 +1111,7 @@ bool pre_answer(int algo, int dir, const jfs_iov &v, int64_t *res) {
 // Deal the todo blocks round-robin over the selected devices
 // and run them; ae_all (optional) is parallel to iov2.
 int64_t deal(int algo, int dir, const std::vector<int> &todo, const std::vector<jfs_iov> &iov2, int64_t *out_n,
-             uint32_t mask, const Aead *ae_all) {
+             uint32_t mask, const Aead *ae_all, uint32_t *crc = nullptr) {
     std::vector<DevCtx *> &all = devices();
     std::vector<DevCtx *> ds;
     for (DevCtx *d : all)
@@ -1028,6 +1123,7 @@ int64_t deal(int algo, int dir, const std::vector<int> &todo, const std::vector<
         std::vector<const uint8_t *> key, nonce;
         std::vector<jfs_seal_param> sp;
         std::vector<int64_t> hdr, res;
+        std::vector<uint32_t> crc;
         std::vector<int> idx;
     };
     std::vector<Part> part(G);
@@ -1046,14 +1142,16 @@ int64_t deal(int algo, int dir, const std::vector<int> &todo, const std::vector<
     auto work = [&](size_t g) {
         Part &p = part[g];
         p.res.assign(p.iov.size(), 0);
+        p.crc.assign(p.iov.size(), 0u);
+        uint32_t *pc = crc ? p.crc.data() : nullptr;
         std::unique_lock<std::mutex> lk;
         Lane &ln = ds[g]->acquire_lane(lk);
         if (ae_all) {
             Aead a{ae_all->cipher, ae_all->seal, p.orig.data(), p.key.data(), p.nonce.data(),
                    ae_all->sp ? p.sp.data() : nullptr, ae_all->hdr ? p.hdr.data() : nullptr};
-            run_isolated(ds[g], ln, algo, dir, (int)p.iov.size(), p.iov.data(), p.res.data(), &a);
+            run_isolated(ds[g], ln, algo, dir, (int)p.iov.size(), p.iov.data(), p.res.data(), &a, pc);
         } else {
-            run_isolated(ds[g], ln, algo, dir, (int)p.iov.size(), p.iov.data(), p.res.data());
+            run_isolated(ds[g], ln, algo, dir, (int)p.iov.size(), p.iov.data(), p.res.data(), nullptr, pc);
         }
     };
     if (G == 1) work(0);
@@ -1063,7 +1161,10 @@ int64_t deal(int algo, int dir, const std::vector<int> &todo, const std::vector<
         for (auto &t : th) t.join();
     }
     for (size_t g = 0; g < G; g++)
-        for (size_t k = 0; k < part[g].idx.size(); k++) out_n[part[g].idx[k]] = part[g].res[k];
+        for (size_t k = 0; k < part[g].idx.size(); k++) {
+            out_n[part[g].idx[k]] = part[g].res[k];
+            if (crc) crc[part[g].idx[k]] = part[g].crc[k];
+        }
     return JFS_OK;
 }
 
@@ -1078,17 +1179,19 @@ int64_t envelope_parse(const uint8_t *src, int64_t n, int64_t *woff, int64_t *wl
     return 3 + kl + nl;
 }
 
-int64_t batch_common(int algo, int dir, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t mask) {
+int64_t batch_common(int algo, int dir, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t mask,
+                     uint32_t *crc = nullptr) {
     if (nblk < 0 || (nblk > 0 && (!iov || !out_n))) return JFS_ERR_INVALID;
     if (algo != JFS_ALGO_NONE && algo != JFS_ALGO_LZ4 && algo != JFS_ALGO_ZSTD) return JFS_ERR_INVALID;
     std::vector<int> todo;
     for (int i = 0; i < nblk; i++) {
         if (!pre_answer(algo, dir, iov[i], &out_n[i])) todo.push_back(i);
+        else if (crc) crc[i] = out_n[i] >= 0 ? host_crc32c(0, iov[i].dst, out_n[i]) : 0u;  // "none": the payload is dst
     }
     if (todo.empty()) return JFS_OK;
     std::vector<jfs_iov> iov2(todo.size());
     for (size_t k = 0; k < todo.size(); k++) iov2[k] = iov[todo[k]];
-    return deal(algo, dir, todo, iov2, out_n, mask, nullptr);
+    return deal(algo, dir, todo, iov2, out_n, mask, nullptr, crc);
 }
 
 }  // namespace
@@ -1152,9 +1255,10 @@ int64_t jfs_decompress(int algo, uint8_t *dst, int64_t dst_cap, const uint8_t *s
     return one_call(algo, DECOMPRESS, dst, dst_cap, src, n);
 }
 
-static int64_t batch_call(int algo, int dir, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t device_mask) {
+static int64_t batch_call(int algo, int dir, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t device_mask,
+                          uint32_t *crc = nullptr) {
     const int64_t t0 = steady_ns();
-    const int64_t r = batch_common(algo, dir, nblk, iov, out_n, device_mask);
+    const int64_t r = batch_common(algo, dir, nblk, iov, out_n, device_mask, crc);
     if (OpStats *st = op_stats(algo, dir)) {
         st->calls.fetch_add(1, std::memory_order_relaxed);
         if (r == JFS_OK)
@@ -1177,7 +1281,7 @@ int64_t jfs_envelope_parse(const uint8_t *src, int64_t n, int64_t *wrapped_off, 
 }
 
 int64_t jfs_compress_seal_batch(int algo, int cipher, int nblk, const jfs_iov *iov, const jfs_seal_param *p,
-                                int64_t *out_n, uint32_t device_mask) {
+                                int64_t *out_n, uint32_t *crc, uint32_t device_mask) {
     if (nblk < 0 || (nblk > 0 && (!iov || !out_n || !p))) return JFS_ERR_INVALID;
     if (algo != JFS_ALGO_NONE && algo != JFS_ALGO_LZ4 && algo != JFS_ALGO_ZSTD) return JFS_ERR_INVALID;
     if (jfs_cipher_key_size(cipher) < 0) return JFS_ERR_INVALID;
@@ -1188,6 +1292,7 @@ int64_t jfs_compress_seal_batch(int algo, int cipher, int nblk, const jfs_iov *i
     std::vector<jfs_seal_param> sp;
     std::vector<int64_t> hdr;
     for (int i = 0; i < nblk; i++) {
+        if (crc) crc[i] = 0;
         const jfs_iov &v = iov[i];
         const jfs_seal_param &q = p[i];
         const int64_t bound = jfs_envelope_bound(algo, v.src_len, q.wrapped_len);
@@ -1216,7 +1321,7 @@ int64_t jfs_compress_seal_batch(int algo, int cipher, int nblk, const jfs_iov *i
     int64_t rc = JFS_OK;
     if (!todo.empty()) {
         Aead ae{cipher, true, orig.data(), key.data(), nonce.data(), sp.data(), hdr.data()};
-        rc = deal(algo, COMPRESS, todo, iov2, out_n, device_mask, &ae);
+        rc = deal(algo, COMPRESS, todo, iov2, out_n, device_mask, &ae, crc);
     }
     if (OpStats *st = op_stats(algo, COMPRESS)) {
         st->calls.fetch_add(1, std::memory_order_relaxed);
@@ -1295,6 +1400,12 @@ int64_t jfs_open_decompress_batch(int algo, int cipher, int nblk, const jfs_iov 
 
 int64_t jfs_compress_batch(int algo, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t device_mask) {
     return batch_call(algo, COMPRESS, nblk, iov, out_n, device_mask);
+}
+
+int64_t jfs_compress_batch_crc(int algo, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t *crc,
+                               uint32_t device_mask) {
+    if (nblk > 0 && !crc) return JFS_ERR_INVALID;
+    return batch_call(algo, COMPRESS, nblk, iov, out_n, device_mask, crc);
 }
 
 int64_t jfs_decompress_batch(int algo, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t device_mask) {

@@ -126,9 +126,13 @@ struct Smem {
     uint32_t part[LANES / 64];
 };
 
+// lens (optional): per-block lengths produced on the device by the previous
+// kernel (the codec's or the AEAD's result; <= 0 = it failed: crc 0);
+// seeds (optional): crc32.Update(seed, crc32c, data) instead of seed 0.
 __global__ __launch_bounds__(LANES) void crc32c_kernel(const jfs_dev_block *__restrict__ blocks, int nblk, int32_t rows,
                                                         int32_t emit_segments, uint32_t *__restrict__ crc_out,
-                                                        int32_t *__restrict__ ret) {
+                                                        int32_t *__restrict__ ret, const int32_t *__restrict__ lens,
+                                                        const uint32_t *__restrict__ seeds) {
     __shared__ Smem s;
     const int b = blockIdx.x;
     const int t = threadIdx.x, l = t & 63, w = t >> 6;
@@ -143,7 +147,12 @@ __global__ __launch_bounds__(LANES) void crc32c_kernel(const jfs_dev_block *__re
     const jfs_dev_block blk = ((const gc_blk *)blocks)[b];
     const gc_u8 *src = (const gc_u8 *)blk.src;
     g_u8 *out = (g_u8 *)blk.dst;
-    const int64_t n = blk.src_len;
+    const int64_t n = lens ? (int64_t)lens[b] : (int64_t)blk.src_len;
+    const uint32_t seed = seeds ? seeds[b] : 0u;
+    if (lens && n <= 0) {
+        if (t == 0 && crc_out) crc_out[b] = 0;
+        return;
+    }
     const int64_t S = (int64_t)rows * ROW;
     const int64_t words = n > 0 ? (n - 1) / S + 1 : 1;  // Go's ((len-1)/csBlock+1), 1 word for len 0
     if (n < 0 || (emit_segments && (out == nullptr || (int64_t)blk.dst_cap < 4 * words))) {
@@ -207,7 +216,7 @@ __global__ __launch_bounds__(LANES) void crc32c_kernel(const jfs_dev_block *__re
     }
     if (t == 0) {
         if (n == 0 && emit_segments) out[0] = out[1] = out[2] = out[3] = 0;
-        if (crc_out) crc_out[b] = n == 0 ? 0u : ~(total ^ mulp(0xFFFFFFFFu, xpow8(T, (uint64_t)n)));
+        if (crc_out) crc_out[b] = n == 0 ? seed : ~(total ^ mulp(~seed, xpow8(T, (uint64_t)n)));
         if (ret) ret[b] = emit_segments ? (int32_t)(4 * words) : 0;
     }
 }
@@ -222,6 +231,18 @@ extern "C" int jfs_launch_crc32c(const jfs_dev_block *d_blocks, int nblk, int32_
     const int emit = seg_bytes > 0;
     const int32_t S = emit ? seg_bytes : (32 << 10);
     if (S % ROW != 0 || S > (64 << 20)) return -1;
-    hipLaunchKernelGGL(crc32c_kernel, dim3(nblk), dim3(LANES), 0, stream, d_blocks, nblk, S / ROW, emit, d_crc, d_ret);
+    hipLaunchKernelGGL(crc32c_kernel, dim3(nblk), dim3(LANES), 0, stream, d_blocks, nblk, S / ROW, emit, d_crc, d_ret,
+                       (const int32_t *)nullptr, (const uint32_t *)nullptr);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// whole-block CRC-32C of device blocks whose length the previous kernel wrote
+// (lens), continuing from per-block seeds (the host path's PUT payloads)
+extern "C" int jfs_launch_crc32c_lens(const jfs_dev_block *d_blocks, int nblk, const int32_t *d_lens,
+                                      const uint32_t *d_seeds, uint32_t *d_crc, hipStream_t stream) {
+    using namespace jfs::crc;
+    if (nblk <= 0) return 0;
+    hipLaunchKernelGGL(crc32c_kernel, dim3(nblk), dim3(LANES), 0, stream, d_blocks, nblk, (32 << 10) / ROW, 0, d_crc,
+                       (int32_t *)nullptr, d_lens, d_seeds);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

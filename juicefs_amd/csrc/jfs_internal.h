@@ -35,6 +35,8 @@ void jfs_zstd_plan_host(const uint8_t *const *srcs, const int32_t *lens, const i
                         uint64_t *totals);
 int jfs_launch_crc32c(const jfs_dev_block *d_blocks, int nblk, int32_t seg_bytes, uint32_t *d_crc, int32_t *d_ret,
                       hipStream_t stream);
+int jfs_launch_crc32c_lens(const jfs_dev_block *d_blocks, int nblk, const int32_t *d_lens, const uint32_t *d_seeds,
+                           uint32_t *d_crc, hipStream_t stream);
 int jfs_launch_aes256gcm(const jfs_aead_block *d_blocks, int nblk, int mode, int32_t *d_ret, const int32_t *d_lens,
                          hipStream_t stream);
 int jfs_launch_aead(int cipher, const jfs_aead_block *d_blocks, int nblk, int mode, int32_t *d_ret,

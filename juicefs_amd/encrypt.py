@@ -59,8 +59,9 @@ def _err_of(code: int, dst_len: int, src_len: int, op: str) -> CompressError:
     return _err(code, dst_len, src_len, op)
 
 
-def compress_seal_batch(codec: int, algo: str, pairs, params, device_mask: int = 0):
-    """pairs: [(dst, raw block)], params: [(key, nonce, wrapped_key)] -> [(envelope bytes, err)]"""
+def compress_seal_batch(codec: int, algo: str, pairs, params, device_mask: int = 0, crcs: list | None = None):
+    """pairs: [(dst, raw block)], params: [(key, nonce, wrapped_key)] -> [(envelope bytes, err)];
+    with crcs=[], it receives each envelope's CRC-32C (generateChecksum)."""
     lib = L.load()
     nb = len(pairs)
     iov = (L.JfsIov * max(nb, 1))()
@@ -76,9 +77,12 @@ def compress_seal_batch(codec: int, algo: str, pairs, params, device_mask: int =
         iov[i].src, iov[i].src_len, iov[i].dst, iov[i].dst_cap = s, sn, d, dn
         sp[i].key, sp[i].nonce, sp[i].wrapped, sp[i].wrapped_len = kk, nn, ww, wn
     out = (ctypes.c_int64 * max(nb, 1))()
-    rc = lib.jfs_compress_seal_batch(codec, cipher_id(algo), nb, iov, sp, out, device_mask)
+    crc = (ctypes.c_uint32 * max(nb, 1))() if crcs is not None else None
+    rc = lib.jfs_compress_seal_batch(codec, cipher_id(algo), nb, iov, sp, out, crc, device_mask)
     if rc != 0:
         raise _err_of(rc, 0, 0, "seal batch")
+    if crcs is not None:
+        crcs[:] = [int(crc[i]) for i in range(nb)]
     return [(int(out[i]), None) if out[i] >= 0 else
             (0, _err_of(int(out[i]), iov[i].dst_cap, iov[i].src_len, "compress+seal")) for i in range(nb)]
 

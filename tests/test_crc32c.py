@@ -122,3 +122,16 @@ def test_crc32c_bad_descriptor(gpu):
     # dst too small for the segment sums -> ret -1, nothing written past cap
     c, r, segs = _run_gpu(gpu, [bytes(100000)], 32 << 10, extra_cap=-4)
     assert r == [-1]
+
+
+def test_none_codec_batch_checksum_on_host(oracle):
+    """jfs_compress_batch_crc with the "none" codec: the payload is the block
+    itself (noOp, compress.go:55-68), summed on the host; no GPU needed."""
+    from juicefs_amd import compress as C
+    c = C.NewCompressor("none")
+    srcs = [b"", b"a", gen_block("T", 3, 70000), gen_block("R", 4, 4097)]
+    pairs = [(bytearray(len(s)), s) for s in srcs] + [(bytearray(1), b"toolong")]
+    res = c.CompressBatchChecksum(pairs)
+    for (d, s), (n, e, crc) in zip(pairs[:-1], res[:-1]):
+        assert e is None and n == len(s) and crc == oracle.crc32c(s)
+    assert res[-1][1] is not None and res[-1][2] == 0

@@ -93,3 +93,23 @@ def test_seal_short_dst_and_bad_cipher(gpu):
     assert r[0][1].code == L.JFS_ERR_SHORT_BUFFER
     with pytest.raises(ValueError):
         E.cipher_id("rot13")
+
+
+@pytest.mark.parametrize("codec", ["lz4", "zstd"])
+def test_put_payload_checksums(gpu, oracle, codec):
+    """generateChecksum (pkg/object/checksum.go:30-45) of what is PUT: the
+    compressed block (jfs_compress_batch_crc) or the whole envelope
+    (jfs_compress_seal_batch), computed on the GPU; CRC-32C oracle pinned by
+    RFC 3720."""
+    raws = _blocks()
+    c = C.NewCompressor(codec)
+    pairs = [(bytearray(c.CompressBound(len(r))), r) for r in raws]
+    res = c.CompressBatchChecksum(pairs)
+    for (d, _), (n, e, crc) in zip(pairs, res):
+        assert e is None and crc == oracle.crc32c(bytes(d[:n]))
+    params = [(bytes(range(32)), bytes(range(12)), b"k" * (100 + i)) for i in range(len(raws))]
+    spairs = [(bytearray(E.envelope_bound(CODECS[codec], len(r), 100 + i)), r) for i, r in enumerate(raws)]
+    crcs = []
+    sres = E.compress_seal_batch(CODECS[codec], E.CHACHA20_RSA, spairs, params, crcs=crcs)
+    for (d, _), (n, e), crc in zip(spairs, sres, crcs):
+        assert e is None and crc == oracle.crc32c(bytes(d[:n]))
