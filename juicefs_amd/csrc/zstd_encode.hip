@@ -11,7 +11,7 @@
 // literal-header format).
 //
 // Per 128 KiB block:
-//   1. greedy LZ77 parse (4-byte hash of the position, table of 4096 positions
+//   1. greedy LZ77 parse (4-byte hash of the position, table of 8192 positions
 //      in LDS, acceleration skip on misses like LZ4's, forward extension 64
 //      bytes per step across the wave, backward catch-up); literals go
 //      straight to the output, sequences to a per-input scratch list;
@@ -40,7 +40,10 @@ constexpr int64_t LSTREAM = 36 << 10;       // one Huffman stream (<= 32 KiB of 
 constexpr int64_t SCR_PER = SEQ_CAP * 8 + 4 * LSTREAM;  // scratch bytes per input
 constexpr int HUF_MAXB = 11;                // code length limit (HUF_TABLELOG_DEFAULT)
 constexpr int HUF_MINL = 64;                // fewer literals stay raw
-constexpr int32_t HBITS = 12;               // hash table: 4096 positions
+#ifndef JFS_ZE_HBITS
+#define JFS_ZE_HBITS 13  // libzstd level 1 for inputs > 256 KiB: hashLog 13
+#endif
+constexpr int32_t HBITS = JFS_ZE_HBITS;     // hash table: 2^HBITS positions in LDS
 
 // RFC 8878 3.1.1.3.2.1 code tables and 3.1.1.3.2.2 predefined distributions
 __constant__ uint32_t LL_BASE[36] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,   10,  11,  12,   13,   14,   15,    16,    18,

@@ -148,4 +148,4 @@ def test_zstd_encode_ratio_floor(gpu):
     r, frames = encode_device(srcs, gpu)
     ratio = sum(len(s) for s in srcs) / sum(r)
     print("zstd GPU ratio", ratio)
-    assert ratio >= 2.7, ratio
+    assert ratio >= 3.0, ratio
