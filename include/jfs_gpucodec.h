@@ -187,6 +187,22 @@ int jfs_lz4_split_counts(uint64_t *out, int reset);
 /* ret[i] = LZ4_compress_default(src, dst, src_len, dst_cap): compressed size,
  * or 0 when it does not fit dst_cap. */
 int64_t jfs_lz4_compress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream);
+/* The same bytes as jfs_lz4_compress_device for few blocks (one-call
+ * Compress under cachedStore.upload, pkg/chunk/cached_store.go:372): every
+ * block is cut into segments that are parsed at once and re-parsed, each from
+ * the state the segment before it stopped in, until nothing changes (then the
+ * result is the serial parse, byte for byte); blocks that do not settle take
+ * the serial kernel.  src_len = HOST copies of the descriptors' src_len.
+ * Asynchronous on `stream`; per-device scratch of about 4 bytes per input
+ * byte, reused across calls.  jfs_compress / small jfs_compress_batch calls use
+ * it below JFS_LZ4E_SEG_MAX blocks (default 256). */
+int64_t jfs_lz4_compress_device_small(const jfs_dev_block *d_blocks, const int32_t *src_len, int nblk, int32_t *d_ret,
+                                      void *stream);
+/* Diagnostics of the segment encoder: out[r] (r = 1..16) = blocks whose
+ * segments settled after r rounds, out[0] = blocks handed to the serial kernel
+ * (not settled within JFS_LZ4E_SEG_ROUNDS, default 8, or a segment with too
+ * many sequences); on the current device since the last reset.  Synchronous. */
+int jfs_lz4_eseg_counts(uint64_t *out, int reset);
 /* ret[i]: decoded bytes, -1 malformed frame (ZSTD error), -2 output larger
  * than dst_cap ("Destination buffer is too small"), -3 src size incorrect
  * (truncated / trailing bytes). */

@@ -498,6 +498,17 @@ double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// LZ4 encode batches of at most this many blocks take the segment-parallel
+// parse (lz4_encode.hip, lz4_eseg): latency of a few segment parses instead of
+// one whole-block parse per wave
+int eseg_max() {
+    static int v = [] {
+        const char *e = getenv("JFS_LZ4E_SEG_MAX");
+        return e ? atoi(e) : 256;
+    }();
+    return v;
+}
+
 int launch_kernel(int algo, int dir, const jfs_dev_block *d_desc, int nblk, int32_t *d_ret, hipStream_t st) {
     if (algo == JFS_ALGO_LZ4 && dir == DECOMPRESS) return jfs_launch_lz4_decode(d_desc, nblk, d_ret, st);
     if (algo == JFS_ALGO_LZ4 && dir == COMPRESS) return jfs_launch_lz4_encode(d_desc, nblk, d_ret, st);
@@ -677,6 +688,16 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
     };
     (void)aeb;
     // compress -> seal, or open -> decompress (the staged inputs and the
+    // LZ4 encode of a staged chunk: segment-parallel for small batches
+    auto lz4_encode = [&](Slot &sl, const jfs_dev_block *h_desc, const jfs_dev_block *d_desc, int n, int32_t *d_ret,
+                          hipStream_t ks) -> int64_t {
+        if (n > eseg_max()) return jfs_launch_lz4_encode(d_desc, n, d_ret, ks) == 0 ? JFS_OK : JFS_ERR_HIP;
+        std::vector<int32_t> lens(n);
+        for (int k = 0; k < n; k++) lens[k] = h_desc[k].src_len;
+        if (!sl.ensure_split(jfs_lz4_eseg_scratch_bytes(n, lens.data()))) return JFS_ERR_NO_MEMORY;
+        return jfs_launch_lz4_encode_seg(d_desc, n, lens.data(), d_ret, sl.sp, sl.sp_cap, ks) == 0 ? JFS_OK
+                                                                                                   : JFS_ERR_HIP;
+    };
     // codec descriptors are already in place; run on the lane's kernel stream)
     auto launch_aead = [&](const Chunk &c, Slot &sl, uint8_t *h_in, uint8_t *h_out, jfs_dev_block *h_desc,
                            int32_t *h_ret, uint8_t *d_in, uint8_t *d_out, jfs_dev_block *d_desc,
@@ -723,7 +744,13 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
         if (hipStreamWaitEvent(c.ks, sl.ev_in, 0) != hipSuccess) return JFS_ERR_HIP;
         int lk = 0;
         if (ae->seal) {
-            if (algo != JFS_ALGO_NONE) lk = launch_kernel(algo, COMPRESS, d_desc, n, d_ret, c.ks);
+            if (algo == JFS_ALGO_LZ4) {
+                const int64_t r = lz4_encode(sl, h_desc, d_desc, n, d_ret, c.ks);
+                if (r == JFS_ERR_NO_MEMORY) return r;
+                lk = r == JFS_OK ? 0 : -1;
+            } else if (algo != JFS_ALGO_NONE) {
+                lk = launch_kernel(algo, COMPRESS, d_desc, n, d_ret, c.ks);
+            }
             if (lk == 0)
                 lk = jfs_launch_aead(ae->cipher, d_ad, n, 0, d_r2, algo != JFS_ALGO_NONE ? d_ret : nullptr, c.ks);
         } else {
@@ -822,6 +849,10 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
             }
             if (!sl.ensure_split(jfs_lz4_split_scratch_bytes(n, lens.data(), caps.data()))) return JFS_ERR_NO_MEMORY;
             lk = jfs_launch_lz4_split(d_desc, n, d_ret, sl.sp, nseg, max_cap, c.ks);
+        } else if (algo == JFS_ALGO_LZ4 && dir == COMPRESS) {
+            const int64_t r = lz4_encode(sl, h_desc, d_desc, n, d_ret, c.ks);
+            if (r == JFS_ERR_NO_MEMORY) return r;
+            lk = r == JFS_OK ? 0 : -1;
         } else {
             lk = launch_kernel(algo, dir, d_desc, n, d_ret, c.ks);
         }
@@ -1469,6 +1500,36 @@ int64_t jfs_lz4_decompress_device_small(const jfs_dev_block *d_blocks, const int
     hipStream_t st = (hipStream_t)stream;
     if (hipStreamWaitEvent(st, z.ev_done, 0) != hipSuccess) return JFS_ERR_HIP;
     if (jfs_launch_lz4_split(d_blocks, nblk, d_ret, z.p, nseg, max_cap, st) != 0) return JFS_ERR_HIP;
+    return hipEventRecord(z.ev_done, st) == hipSuccess ? JFS_OK : JFS_ERR_HIP;
+}
+
+SplitScratch g_eseg_scr[64];
+
+int64_t jfs_lz4_compress_device_small(const jfs_dev_block *d_blocks, const int32_t *src_len, int nblk, int32_t *d_ret,
+                                      void *stream) {
+    if (!current_device_ok()) return JFS_ERR_NO_DEVICE;
+    if (nblk < 0 || (nblk > 0 && !src_len)) return JFS_ERR_INVALID;
+    if (nblk == 0) return JFS_OK;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return JFS_ERR_HIP;
+    stat_launch(JFS_ALGO_LZ4, COMPRESS, nblk);
+    const int64_t need = jfs_lz4_eseg_scratch_bytes(nblk, src_len);
+    SplitScratch &z = g_eseg_scr[dev];
+    std::lock_guard<std::mutex> lk(z.mu);
+    if (!z.ev_done && hipEventCreateWithFlags(&z.ev_done, hipEventDisableTiming) != hipSuccess) return JFS_ERR_HIP;
+    if (need > z.cap) {
+        if (hipEventSynchronize(z.ev_done) != hipSuccess) return JFS_ERR_HIP;
+        if (z.p) (void)hipFree(z.p);
+        z.p = nullptr;
+        z.cap = 0;
+        int64_t want = 64ll << 20;
+        while (want < need) want <<= 1;
+        if (hipMalloc((void **)&z.p, (size_t)want) != hipSuccess) return JFS_ERR_NO_MEMORY;
+        z.cap = want;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    if (hipStreamWaitEvent(st, z.ev_done, 0) != hipSuccess) return JFS_ERR_HIP;
+    if (jfs_launch_lz4_encode_seg(d_blocks, nblk, src_len, d_ret, z.p, z.cap, st) != 0) return JFS_ERR_HIP;
     return hipEventRecord(z.ev_done, st) == hipSuccess ? JFS_OK : JFS_ERR_HIP;
 }
 

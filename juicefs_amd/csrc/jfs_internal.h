@@ -25,6 +25,11 @@ typedef JFS_GLOBAL const jfs_dev_block gc_blk;
 extern "C" {
 int jfs_launch_lz4_decode(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, hipStream_t stream);
 int jfs_launch_lz4_encode(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, hipStream_t stream);
+// segment-parallel LZ4 encode (same bytes as jfs_launch_lz4_encode); lens = the
+// blocks' src_len on the host; scratch of jfs_lz4_eseg_scratch_bytes
+int64_t jfs_lz4_eseg_scratch_bytes(int nblk, const int32_t *lens);
+int jfs_launch_lz4_encode_seg(const jfs_dev_block *d_blocks, int nblk, const int32_t *lens, int32_t *d_ret,
+                              void *scratch, int64_t scratch_cap, hipStream_t stream);
 int jfs_launch_zstd_encode(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, hipStream_t stream);
 int jfs_launch_zstd_decode(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, uint8_t *d_scratch,
                            hipStream_t stream);

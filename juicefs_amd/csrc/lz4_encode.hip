@@ -48,6 +48,7 @@ __device__ unsigned long long g_eprof[12];
 #define JFS_LZ4E_PSEARCH 1  // lane-parallel search over the skip schedule (serial loop on shared hashes)
 #endif
 constexpr int64_t kMaxInput = 0x7E000000;
+constexpr int64_t kSegMinInput = 65536 + 12 - 1;  // byU32 table (smaller blocks: byU16, serial kernel only)
 constexpr int OB = 2048;  // output staging ring (the put_* paths assume OB >= 2 * OFLUSH + slack)
 constexpr int OBMASK = OB - 1;
 constexpr int OFLUSH = 1024;
@@ -244,12 +245,140 @@ __device__ __forceinline__ void put_token(Smem &s, Enc &e, int64_t tp, uint32_t 
     }
 }
 
+// Extend a match from xend (all bytes before it equal) by up to 4 KiB:
+// lane l compares the 16-byte pieces at xend + 16 l + 1024 u (u < 4) with the
+// bytes `off` earlier (source bytes: overlap is irrelevant), bytes at or past
+// matchlimit count as different.  Advances xend to the first difference (or by
+// 4 KiB); returns whether all 4 KiB were equal.
+__device__ __forceinline__ bool extend_wide(const Enc &e, int64_t &xend, uint32_t off, int64_t matchlimit) {
+    const int l = lane_id();
+    uint32_t fd[4];
+    uint32_t xw[4][4], yw[4][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int64_t a = xend + 1024 * u + 16 * l;
+        if (a + 16 <= matchlimit) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                xw[u][i] = ld32u(e.src + a + 4 * i);
+                yw[u][i] = ld32u(e.src + a - (int64_t)off + 4 * i);
+            }
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int64_t a = xend + 1024 * u + 16 * l;
+        fd[u] = 16;
+        if (a + 16 <= matchlimit) {
+#pragma unroll
+            for (int i = 3; i >= 0; --i) {
+                const uint32_t d = xw[u][i] ^ yw[u][i];
+                if (d) fd[u] = 4 * i + (__builtin_ctz(d) >> 3);
+            }
+        } else {
+            fd[u] = 0;
+            while (a + fd[u] < matchlimit && e.src[a + fd[u]] == e.src[a + fd[u] - (int64_t)off]) ++fd[u];
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const uint64_t ne = __ballot(fd[u] < 16);
+        if (ne) {
+            const int k = (int)__builtin_ctzll(ne);
+            xend += 1024 * u + 16 * k + (int64_t)readlane(fd[u], k);
+            return false;
+        }
+    }
+    xend += 4096;
+    return true;
+}
+
+// ---- segment mode (lz4_eseg) ----------------------------------------------
+// A search state of the parse: the next search position P, the start of the
+// pending literal run, the skip-schedule index of P (0 right after a match).
+struct SegState {
+    int64_t P, anchor;
+    int32_t k0, end;  // end: the parse finished (last literals) before or in this segment
+    int64_t pad;
+};
+// one sequence of the segment's output: literal count, match length - 4 (or
+// kLastSeq: the block's last literals), offset
+struct Seq {
+    uint32_t lit, ml, off;
+};
+constexpr uint32_t kLastSeq = 0xFFFFFFFFu;
+constexpr int kSegRoundsMax = 16;
+// settled-round histogram of segment-mode blocks (index 0: unsettled -> serial kernel)
+__device__ unsigned long long g_eseg[kSegRoundsMax + 1];
+struct SegCtl {
+    int round, nseg, nblk, cap;
+    int64_t warm;  // round 1: segment k > 0 starts its parse this many bytes before its nominal start
+    int32_t *seg_blk, *seg_k, *seq_n, *first, *nsegb, *fail, *todo, *diff;
+    int64_t *seg_lo, *seg_hi, *anchor0, *seg_bytes, *map_off, *mlen;
+    void *st;  // SegState [2][nseg]: round r writes half r & 1
+    Seq *seq;  // [nseg][cap]
+    uint8_t *map;  // per block two halves of mlen bytes: round r marks its insertions with r in half r & 1
+};
+// the round at which block b's segments reached their fixed point (0: not yet)
+__device__ __forceinline__ int seg_conv(const SegCtl &c, int b, int upto) {
+    if (c.fail[b]) return 0;
+    if (c.nsegb[b] == 1) return 1;  // one segment starts at the true start: exact at once
+    for (int r = 2; r <= upto; ++r)
+        if (c.diff[r * c.nblk + b] == 0) return r;
+    return 0;
+}
+// The hash table at search position P: for every hash, the latest position
+// before P that the parse inserted (map byte == rv); only the last 65,535
+// positions matter (older entries fail the distance check, like position 0).
+__device__ void seg_table(Smem &s, const Enc &e, const uint8_t *mapr, uint8_t rv, int64_t P) {
+    const int l = lane_id();
+    for (int k = l; k < 4096; k += 64) s.table[k] = 0;
+    __builtin_amdgcn_wave_barrier();
+    const int64_t w0 = P > 65535 ? P - 65535 : 0;
+    for (int64_t q = (w0 & ~(int64_t)15) + 16 * l; q < P; q += 1024) {
+        const uint4 m = *(const gc_u4 *)(mapr + q);
+        const uint32_t mw[4] = {m.x, m.y, m.z, m.w};
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int64_t p = q + i;
+            if (((mw[i >> 2] >> (8 * (i & 3))) & 255u) == rv && p >= w0 && p < P) {
+                const uint64_t v = (uint64_t)ld32u(e.src + p) | ((uint64_t)ld32u(e.src + p + 4) << 32);
+                atomicMax(&s.table[hash_of(v, false)], (uint32_t)p);
+            }
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (int k = l; k < 4096; k += 64) {
+        const uint32_t pos = s.table[k];
+        s.table[k] = pos | check_of(e, ld32u(e.src + pos));
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+
 // Residency: 20 KiB of LDS per block -> 8 blocks (waves) per CU.
-__global__ __launch_bounds__(64) void lz4_encode_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
-                                                       int32_t *__restrict__ ret) {
+//
+// SEG = false: one workgroup per block, the whole parse, output bytes.
+// SEG = true: one workgroup per segment of a block (lz4_eseg below): the parse
+// from the segment's start state up to the first search position at or past
+// the segment's end, recording the positions it inserts (map) and its
+// sequences instead of output bytes.
+template <bool SEG>
+__global__ __launch_bounds__(64) void lz4_encode_kernel_t(const jfs_dev_block *__restrict__ blocks, int nblk,
+                                                         int32_t *__restrict__ ret, const int32_t *__restrict__ todo,
+                                                         SegCtl c) {
+    static_assert(!SEG || JFS_LZ4E_PSEARCH, "segment mode needs the lane-parallel search");
     __shared__ Smem s;
-    const int b = blockIdx.x;
-    if (b >= nblk) return;
+    int b, j = 0;
+    if constexpr (SEG) {
+        j = blockIdx.x;
+        if (j >= c.nseg) return;
+        b = c.seg_blk[j];
+        if (c.nsegb[b] == 0 || c.fail[b] || (c.round >= 2 && seg_conv(c, b, c.round - 1))) return;
+    } else {
+        b = blockIdx.x;
+        if (b >= nblk) return;
+        if (todo && !todo[b]) return;
+    }
     const int l = lane_id();
     const jfs_dev_block d = ((const gc_blk *)blocks)[b];
     EP_DECL
@@ -286,14 +415,69 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(const jfs_dev_block *__r
         sw_fill(s, e, 0);
         // empty table: every entry is position 0 (LZ4's zeroed table), with its check bits
         const uint32_t init = u16 ? 0u : (n >= 4 ? check_of(e, sw_rd32(s, e, 0)) : 0u);
-        for (int k = l; k < 4096; k += 64) s.table[k] = init;
-        __builtin_amdgcn_wave_barrier();
         const int64_t mflimitP1 = n - 12 + 1, matchlimit = n - 5;
         int64_t ip = 0, anchor = 0;
+        // segment mode: start state, insertion map, sequence list
+        int32_t seg_k = 0, k0s = 0, ns = 0;
+        int64_t seg_hi = INT64_MAX, hand_P = -1, hand_k0 = 0, anchor0 = 0;
+        int64_t rec_lo = 0;  // positions below are warm-up: parsed, not marked
+        bool from0 = true;   // the parse starts at the block start
+        bool rec_seq = true; // sequences are kept (round 1 is a guess for segments k > 0)
+        bool ovf = false;
+        uint8_t *mapw = nullptr;
+        Seq *sq = nullptr;
+        const uint8_t rv = (uint8_t)c.round;
+        if constexpr (SEG) {
+            seg_k = c.seg_k[j];
+            seg_hi = c.seg_hi[j];
+            uint8_t *mb = c.map + c.map_off[b];
+            mapw = mb + ((c.round & 1) ? c.mlen[b] : 0);
+            sq = c.seq + (int64_t)j * c.cap;
+            if (seg_k == 0) {
+                ip = 1;
+            } else if (c.round == 1) {
+                // a guess: a fresh parse from `warm` bytes before the nominal
+                // start (or from the block start), whose table and state at
+                // the nominal start are then close to the serial parse's
+                rec_lo = c.seg_lo[j];
+                if (rec_lo - c.warm > 0) {
+                    ip = anchor = rec_lo - c.warm;
+                    from0 = false;
+                }
+            } else {
+                from0 = false;
+                const SegState st = ((const SegState *)c.st)[(int64_t)((c.round - 1) & 1) * c.nseg + j - 1];
+                if (st.end) {
+                    if (l == 0) {
+                        SegState o = {0, 0, 0, 1, 0};
+                        ((SegState *)c.st)[(int64_t)(c.round & 1) * c.nseg + j] = o;
+                        c.seq_n[j] = 0;
+                        c.anchor0[j] = 0;
+                    }
+                    return;
+                }
+                ip = st.P;
+                anchor = st.anchor;
+                k0s = st.k0;
+            }
+            anchor0 = anchor;
+            rec_seq = c.round >= 2 || seg_k == 0;
+            if (!from0 && c.round >= 2) {
+                seg_table(s, e, mb + (((c.round - 1) & 1) ? c.mlen[b] : 0), (uint8_t)(c.round - 1), ip);
+            } else {
+                for (int k = l; k < 4096; k += 64) s.table[k] = init;
+            }
+        } else {
+            for (int k = l; k < 4096; k += 64) s.table[k] = init;
+        }
+        __builtin_amdgcn_wave_barrier();
         if (n >= 13) {
-            uint64_t v0 = src64(s, e, 0);
-            tput(s, e, hash_of(v0, u16), 0, (uint32_t)v0, u16);
-            ip = 1;
+            if (from0) {
+                uint64_t v0 = src64(s, e, 0);
+                tput(s, e, hash_of(v0, u16), 0, (uint32_t)v0, u16);
+                if (SEG && l == 0 && rec_lo == 0) mapw[0] = rv;
+                ip = 1;
+            }
             uint64_t fv = src64(s, e, ip);  // 8 bytes at the next search position
             uint32_t fh = hash_of(fv, u16);
             for (;;) {
@@ -315,9 +499,15 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(const jfs_dev_block *__r
                 // write + read-back).  The first lane whose candidate matches
                 // ends the search; positions up to it are inserted, the others'
                 // entries are restored.
-                int32_t k0 = 0;  // schedule index of lane 0
+                int32_t k0 = k0s;  // schedule index of lane 0
+                k0s = 0;
                 int64_t pk = ip;
                 for (;;) {
+                    if (SEG && pk >= seg_hi) {  // hand the search over to the next segment
+                        hand_P = pk;
+                        hand_k0 = k0;
+                        break;
+                    }
                     const int32_t k = k0 + l;
                     const int32_t sk = k == 0 ? 1 : (63 + k) >> 6;
                     const uint32_t inc = dpp_scan_add((uint32_t)sk);
@@ -326,7 +516,13 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(const jfs_dev_block *__r
                     const uint64_t endm = __ballot(span && Pn > mflimitP1), spm = __ballot(span);
                     const int jend = endm ? (int)__builtin_ctzll(endm) : 64;
                     const int jspan = ~spm ? (int)__builtin_ctzll(~spm) : 64;
-                    const int nl = jend < jspan ? jend : jspan;  // lanes [0, nl) are looked up
+                    int nl = jend < jspan ? jend : jspan;  // lanes [0, nl) are looked up
+                    int jstop = 64;
+                    if constexpr (SEG) {  // positions at or past the segment end belong to the next segment
+                        const uint64_t stm = __ballot(P >= seg_hi);
+                        jstop = stm ? (int)__builtin_ctzll(stm) : 64;
+                        if (jstop < nl) nl = jstop;
+                    }
                     const bool on = l < nl;
                     if (nl > 0) sw_need(s, e, pk + (int64_t)readlane(inc - (uint32_t)sk, nl - 1), 8);
                     uint32_t cv = 0, h = 0, E = 0;
@@ -378,7 +574,10 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(const jfs_dev_block *__r
                     const uint64_t hm = __ballot(pass);
                     const int jm = hm ? (int)__builtin_ctzll(hm) : 64;
                     if (l < nb) {
-                        if (l <= jm) tput(s, e, h, (uint32_t)P, cv, u16);
+                        if (l <= jm) {
+                            tput(s, e, h, (uint32_t)P, cv, u16);
+                            if (SEG && P >= rec_lo) mapw[P] = rv;
+                        }
                         else if (u16) ((uint16_t *)s.table)[h] = (uint16_t)E;
                         else s.table[h] = E;
                     }
@@ -389,7 +588,7 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(const jfs_dev_block *__r
                         pre_ok = ip == pre_ip && match == pre_m;
                         break;
                     }
-                    if (nb == nl && endm && jend <= jspan) { last = true; break; }  // the schedule passed mflimit
+                    if (nb == nl && endm && jend <= jspan && jend <= jstop) { last = true; break; }  // the schedule passed mflimit
                     pk += (int64_t)readlane(inc, nb - 1);
                     k0 += nb;
                 }
@@ -423,6 +622,7 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(const jfs_dev_block *__r
                 }
                 EP(0);
                 if (last) break;
+                if (SEG && hand_P >= 0) break;
                 EPC(8);
                 // One HBM round trip for the first 64 bytes of the three
                 // byte-parallel phases: catch-up (before ip / match), literals
@@ -466,8 +666,9 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(const jfs_dev_block *__r
                 EP(2);
                 // ---- literals
                 int64_t tp = e.op;
-                uint32_t token;
-                {
+                uint32_t token = 0;
+                uint32_t seq_lit = (uint32_t)(ip - anchor);
+                if constexpr (!SEG) {
                     int64_t lit = ip - anchor;
                     e.op++;  // token slot
                     if (lit >= 15) { token = 15u << 4; put_len(s, e, (uint32_t)(lit - 15)); }
@@ -477,29 +678,35 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(const jfs_dev_block *__r
                 EP(3);
                 for (;;) {  // next_match
                     uint32_t off = (uint32_t)(ip - match);
-                    put1(s, e, off & 255);
-                    put1(s, e, off >> 8);
+                    if constexpr (!SEG) {
+                        put1(s, e, off & 255);
+                        put1(s, e, off >> 8);
+                    }
                     // match length: equal bytes from ip+4 / match+4 up to matchlimit
                     // (the first 64 were compared when the match was found)
-                    while (xmore) {
-                        const int64_t a = xend + l;
-                        const bool eq = a < matchlimit && src[a] == src[a - (int64_t)off];
-                        const uint64_t ne = ~__ballot(eq);
-                        const int run = ne ? (int)__builtin_ctzll(ne) : 64;
-                        xend += run;
-                        xmore = run == 64;
-                    }
+                    // beyond the first 64 bytes (long matches: runs, zero pages):
+                    // 4 KiB per step, 16-byte pieces per lane, loads issued together
+                    while (xmore) xmore = extend_wide(e, xend, off, matchlimit);
                     const int64_t mc = xend - (ip + 4);
                     ip = xend;
-                    if (mc >= 15) {
-                        token += 15;
-                        put_len(s, e, (uint32_t)(mc - 15));
+                    if constexpr (SEG) {
+                        if (rec_seq) {
+                            if (ns >= c.cap) { ovf = true; break; }
+                            if (l == 0) { Seq q = {seq_lit, (uint32_t)mc, off}; sq[ns] = q; }
+                        }
+                        ++ns;
+                        seq_lit = 0;
                     } else {
-                        token += (uint32_t)mc;
+                        if (mc >= 15) {
+                            token += 15;
+                            put_len(s, e, (uint32_t)(mc - 15));
+                        } else {
+                            token += (uint32_t)mc;
+                        }
+                        EP(4);
+                        put_token(s, e, tp, token);
+                        maybe_flush(s, e, INT64_MAX);
                     }
-                    EP(4);
-                    put_token(s, e, tp, token);
-                    maybe_flush(s, e, INT64_MAX);
                     EP(5);
                     anchor = ip;
                     if (ip >= mflimitP1) break;
@@ -518,6 +725,10 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(const jfs_dev_block *__r
                     const uint32_t ent = tget(s, h, u16);
                     const uint32_t mi = u16 ? ent : (ent & e.pmask);
                     tput(s, e, h, (uint32_t)ip, (uint32_t)vi, u16);
+                    if (SEG && l == 0) {
+                        if (ip - 2 >= rec_lo) mapw[ip - 2] = rv;
+                        if (ip >= rec_lo) mapw[ip] = rv;
+                    }
                     bool rm = (u16 || (int64_t)mi + 65535 >= ip) && may_match(e, ent, (uint32_t)vi, u16);
                     if (rm) {  // the 4-byte check and the first 64 extension bytes in one round trip
                         const int64_t ax = ip + 4 + l, dlt = ip - (int64_t)mi;
@@ -533,19 +744,45 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(const jfs_dev_block *__r
                     if (rm) {
                         EPC(10);
                         match = mi;
-                        tp = e.op;
-                        e.op++;
+                        if constexpr (!SEG) {
+                            tp = e.op;
+                            e.op++;
+                        }
                         token = 0;
                         continue;
                     }
                     break;
                 }
+                if (SEG && ovf) break;
                 if (anchor >= mflimitP1) break;
                 ++ip;
                 fv = src64(s, e, ip);
                 fh = hash_of(fv, u16);
                 EP(0);
             }
+        }
+        if constexpr (SEG) {
+            bool end = false;
+            if (!ovf && hand_P < 0) {  // the parse reached the end: last literals
+                if (rec_seq && ns >= c.cap) ovf = true;
+                else {
+                    if (l == 0 && rec_seq) { Seq q = {(uint32_t)(n - anchor), kLastSeq, 0}; sq[ns] = q; }
+                    ++ns;
+                    end = true;
+                }
+            }
+            // no match in the whole first segment (incompressible data): the
+            // skip schedule's state then runs through every segment and only
+            // settles one segment per round -- the serial kernel is faster
+            if (c.round == 1 && seg_k == 0 && ns == 0 && hand_P >= 0) ovf = true;
+            if (l == 0) {
+                if (ovf) c.fail[b] = 1;
+                SegState o = {hand_P, anchor, (int32_t)hand_k0, (ovf || end) ? 1 : 0, 0};
+                ((SegState *)c.st)[(int64_t)(c.round & 1) * c.nseg + j] = o;
+                c.seq_n[j] = ns;
+                c.anchor0[j] = anchor0;
+            }
+            return;
         }
         // ---- last literals
         {
@@ -569,13 +806,360 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel(const jfs_dev_block *__r
     EP_FLUSH();
 }
 
+// ---- segment mode: plan, fixed-point check, output ---------------------------
+//
+// A lone block is one serial parse (~0.5 s for 4 MiB of text on one wave).
+// Segment mode cuts each block at nominal boundaries k*L and parses all
+// segments at once, in rounds.  Round 1 starts segment k > 0 with a fresh
+// search at k*L and an empty table (a guess).  Round r starts segment k from
+// the search state at which segment k-1 stopped in round r-1 (the first
+// search position at or past k*L) and rebuilds the table from the positions
+// round r-1 inserted in the 64 KiB before it.  When a round's stop states and
+// insertion maps equal the previous round's, each segment's inputs are what
+// the segment before produced, and by induction from segment 0 (always exact)
+// every segment is the serial parse: the output is LZ4_compress_default's,
+// byte for byte.  Blocks that do not settle within the round limit (or
+// overflow a sequence list) are encoded by the serial kernel.
+
+constexpr int kPlanThreads = 1024;
+__global__ __launch_bounds__(kPlanThreads) void eseg_plan_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
+                                                                 int64_t L, SegCtl c) {
+    __shared__ int64_t sa[kPlanThreads], sb[kPlanThreads];
+    const int t = threadIdx.x;
+    int64_t carry_s = 0, carry_m = 0;
+    for (int base = 0; base < nblk; base += kPlanThreads) {
+        const int b = base + t;
+        const int64_t n = b < nblk ? (int64_t)((const gc_blk *)blocks)[b].src_len : 0;
+        const int64_t ns = (b < nblk && n >= kSegMinInput && n <= kMaxInput) ? (n / L > 0 ? n / L : 1) : 0;
+        const int64_t ml = ns ? ((n + 63) & ~(int64_t)63) : 0;
+        sa[t] = ns;
+        sb[t] = 2 * ml;
+        __syncthreads();
+        for (int d = 1; d < kPlanThreads; d <<= 1) {
+            const int64_t xa = t >= d ? sa[t - d] : 0, xb = t >= d ? sb[t - d] : 0;
+            __syncthreads();
+            sa[t] += xa;
+            sb[t] += xb;
+            __syncthreads();
+        }
+        const int64_t first = carry_s + sa[t] - ns, moff = carry_m + sb[t] - 2 * ml;
+        if (b < nblk) {
+            c.first[b] = (int32_t)first;
+            c.nsegb[b] = (int32_t)ns;
+            c.map_off[b] = moff;
+            c.mlen[b] = ml;
+            c.todo[b] = ns == 0;
+            for (int64_t k = 0; k < ns; ++k) {
+                const int64_t jj = first + k;
+                c.seg_blk[jj] = b;
+                c.seg_k[jj] = (int32_t)k;
+                c.seg_lo[jj] = k * L;
+                c.seg_hi[jj] = k == ns - 1 ? n : (k + 1) * L;
+            }
+        }
+        carry_s += sa[kPlanThreads - 1];
+        carry_m += sb[kPlanThreads - 1];
+        __syncthreads();
+    }
+}
+
+// after round r: did any stop state or map byte of block b change?
+constexpr int64_t kCmpChunk = 1 << 20;
+__global__ __launch_bounds__(256) void eseg_cmp_kernel(SegCtl c) {
+    const int b = blockIdx.y;
+    if (c.nsegb[b] <= 1 || c.fail[b] || seg_conv(c, b, c.round - 1)) return;
+    const int r = c.round;
+    const uint8_t *mb = c.map + c.map_off[b];
+    const uint8_t *A = mb + ((r & 1) ? c.mlen[b] : 0), *B = mb + (((r - 1) & 1) ? c.mlen[b] : 0);
+    const uint32_t ra = (uint32_t)r * 0x01010101u, rb = (uint32_t)(r - 1) * 0x01010101u;
+    bool d = false;
+    const int64_t lo = (int64_t)blockIdx.x * kCmpChunk, hi = lo + kCmpChunk < c.mlen[b] ? lo + kCmpChunk : c.mlen[b];
+    for (int64_t q = lo + 16 * threadIdx.x; q < hi; q += 16 * 256) {
+        const uint4 x = *(const gc_u4 *)(A + q), y = *(const gc_u4 *)(B + q);
+        const uint32_t xs[4] = {x.x, x.y, x.z, x.w}, ys[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t ex = xs[i] ^ ra, ey = ys[i] ^ rb;  // zero bytes: marked in that round
+#pragma unroll
+            for (int k = 0; k < 4; ++k) d |= (((ex >> (8 * k)) & 255u) == 0) != (((ey >> (8 * k)) & 255u) == 0);
+        }
+    }
+    if (blockIdx.x == 0) {
+        const SegState *sa = (const SegState *)c.st + (int64_t)(r & 1) * c.nseg;
+        const SegState *sb = (const SegState *)c.st + (int64_t)((r - 1) & 1) * c.nseg;
+        for (int k = threadIdx.x; k < c.nsegb[b]; k += 256) {
+            const SegState x = sa[c.first[b] + k], y = sb[c.first[b] + k];
+            d |= x.end != y.end || (!x.end && (x.P != y.P || x.anchor != y.anchor || x.k0 != y.k0));
+        }
+    }
+    if (__syncthreads_or(d) && threadIdx.x == 0) atomicOr(&c.diff[r * c.nblk + b], 1);
+}
+
+__device__ __forceinline__ uint32_t len_bytes(uint32_t v) { return v >= 15 ? (v - 15) / 255 + 1 : 0; }
+__device__ __forceinline__ uint32_t seq_bytes(const Seq &q) {
+    uint32_t n = 1 + len_bytes(q.lit) + q.lit;
+    if (q.ml != kLastSeq) n += 2 + len_bytes(q.ml);
+    return n;
+}
+
+// output bytes of each settled segment; unsettled blocks go to the serial kernel
+__global__ __launch_bounds__(64) void eseg_size_kernel(SegCtl c, int rounds) {
+    const int j = blockIdx.x, l = lane_id();
+    if (j >= c.nseg) return;
+    const int b = c.seg_blk[j];
+    if (c.nsegb[b] == 0) return;
+    const int rc = seg_conv(c, b, rounds);
+    if (rc == 0) {
+        if (c.seg_k[j] == 0 && l == 0) {
+            c.todo[b] = 1;
+            atomicAdd(&g_eseg[0], 1ull);
+        }
+        return;
+    }
+    if (c.seg_k[j] == 0 && l == 0) atomicAdd(&g_eseg[rc], 1ull);
+    const Seq *sq = c.seq + (int64_t)j * c.cap;
+    uint32_t tot = 0;  // a block's output is below 2^31 (bound of n <= kMaxInput)
+    for (int i = l; i < c.seq_n[j]; i += 64) tot += seq_bytes(sq[i]);
+    tot = dwave_sum(tot);
+    if (l == 0) c.seg_bytes[j] = (int64_t)tot;
+}
+
+// write each settled segment's sequences at its offset in the block's output
+__global__ __launch_bounds__(64) void eseg_emit_kernel(const jfs_dev_block *__restrict__ blocks, int32_t *__restrict__ ret,
+                                                       SegCtl c, int rounds) {
+    __shared__ uint32_t lo_s[64], ls_s[64];
+    __shared__ int64_t so_s[64], do_s[64];
+    const int j = blockIdx.x, l = lane_id();
+    if (j >= c.nseg) return;
+    const int b = c.seg_blk[j];
+    if (c.nsegb[b] == 0 || seg_conv(c, b, rounds) == 0) return;
+    const jfs_dev_block d = ((const gc_blk *)blocks)[b];
+    const int k = c.seg_k[j], f = c.first[b], nsb = c.nsegb[b];
+    uint32_t before = 0, total = 0;
+    for (int i = l; i < nsb; i += 64) {
+        const uint32_t v = (uint32_t)c.seg_bytes[f + i];
+        total += v;
+        if (i < k) before += v;
+    }
+    before = dwave_sum(before);
+    total = dwave_sum(total);
+    if (total > (uint64_t)d.dst_cap) {
+        if (k == 0 && l == 0) ret[b] = 0;
+        return;
+    }
+    if (k == 0 && l == 0) ret[b] = (int32_t)total;
+    const gc_u8 *src = (const gc_u8 *)d.src;
+    g_u8 *dst = (g_u8 *)d.dst;
+    const Seq *sq = c.seq + (int64_t)j * c.cap;
+    const int nsq = c.seq_n[j];
+    int64_t op = (int64_t)before, sp = c.anchor0[j];
+    for (int g = 0; g < nsq; g += 64) {
+        const int i = g + l;
+        Seq q = {0, kLastSeq, 0};
+        if (i < nsq) q = sq[i];
+        const uint32_t ob = i < nsq ? seq_bytes(q) : 0;
+        const uint32_t sb_ = i < nsq ? q.lit + (q.ml == kLastSeq ? 0 : q.ml + 4) : 0;
+        const uint32_t oinc = dpp_scan_add(ob), sinc = dpp_scan_add(sb_);
+        const int64_t o = op + (int64_t)(oinc - ob), sx = sp + (int64_t)(sinc - sb_);
+        // token and literal-length bytes
+        const uint32_t lb = len_bytes(q.lit);
+        const int64_t lo_out = o + 1 + lb;  // first literal byte
+        if (i < nsq) {
+            const uint32_t mlc = q.ml == kLastSeq ? 0 : (q.ml >= 15 ? 15 : q.ml);
+            dst[o] = (uint8_t)(((q.lit >= 15 ? 15 : q.lit) << 4) | mlc);
+            if (lb) {
+                for (uint32_t t = 0; t + 1 < lb; ++t) dst[o + 1 + t] = 255;
+                dst[o + lb] = (uint8_t)((q.lit - 15) % 255);
+            }
+            if (q.ml != kLastSeq) {
+                const int64_t mo = lo_out + q.lit;
+                dst[mo] = (uint8_t)(q.off & 255);
+                dst[mo + 1] = (uint8_t)(q.off >> 8);
+                const uint32_t mb = len_bytes(q.ml);
+                if (mb) {
+                    for (uint32_t t = 0; t + 1 < mb; ++t) dst[mo + 2 + t] = 255;
+                    dst[mo + 1 + mb] = (uint8_t)((q.ml - 15) % 255);
+                }
+            }
+        }
+        // literals of the group: the wave copies them together, byte t of
+        // the group's literal bytes found by a binary search over the prefix
+        const uint32_t lit = i < nsq ? q.lit : 0;
+        const uint32_t linc = dpp_scan_add(lit);
+        lo_s[l] = linc - lit;
+        ls_s[l] = lit;
+        so_s[l] = sx;
+        do_s[l] = lo_out;
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t T = (uint32_t)readlane(linc, 63);
+        for (uint32_t t0 = 0; t0 < T; t0 += 256) {
+            uint8_t v[4];
+            int64_t to[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t t = t0 + (uint32_t)(u * 64 + l);
+                to[u] = -1;
+                if (t < T) {
+                    int lo = 0, hi = 63;  // last lane whose literal run starts at or before t
+                    while (lo < hi) {
+                        const int mid = (lo + hi + 1) >> 1;
+                        if (lo_s[mid] <= t) lo = mid;
+                        else hi = mid - 1;
+                    }
+                    const uint32_t r = t - lo_s[lo];
+                    v[u] = src[so_s[lo] + r];
+                    to[u] = do_s[lo] + r;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (to[u] >= 0) dst[to[u]] = v[u];
+        }
+        __builtin_amdgcn_wave_barrier();
+        op += (int64_t)readlane(oinc, 63);
+        sp += (int64_t)readlane(sinc, 63);
+    }
+}
+
 }  // namespace lz4e
 }  // namespace jfs
 
+using jfs::lz4e::SegCtl;
+
 extern "C" int jfs_launch_lz4_encode(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, hipStream_t stream) {
     if (nblk <= 0) return 0;
-    hipLaunchKernelGGL(jfs::lz4e::lz4_encode_kernel, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, d_ret);
+    hipLaunchKernelGGL(jfs::lz4e::lz4_encode_kernel_t<false>, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, d_ret,
+                       (const int32_t *)nullptr, SegCtl{});
     return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+namespace {
+int eseg_rounds() {
+    static int v = [] {
+        const char *e = getenv("JFS_LZ4E_SEG_ROUNDS");
+        const int r = e ? atoi(e) : jfs::lz4e::kSegRoundsMax;
+        return r < 2 ? 2 : (r > jfs::lz4e::kSegRoundsMax ? jfs::lz4e::kSegRoundsMax : r);
+    }();
+    return v;
+}
+int64_t eseg_warm() {
+    static int64_t v = [] {
+        const char *e = getenv("JFS_LZ4E_SEG_WARM_KB");
+        return (int64_t)(e ? atoi(e) : 64) << 10;
+    }();
+    return v;
+}
+// Segment length: about 2,048 segments over the batch (8 waves per CU), at
+// least 64 KiB (JFS_LZ4E_SEG_MIN_KB).  A difference between two rounds travels
+// about one segment per round, and some persist for tens of KiB of input
+// (hash-table entries live until overwritten), so shorter segments need more
+// rounds: on 4 MiB text blocks 16 KiB did not settle in 8 rounds, 32 KiB took
+// 7, 64 KiB 4-6 (scripts/eseg_timing.py).
+int64_t eseg_len(int nblk, const int32_t *lens) {
+    static int64_t lmin = [] {
+        const char *e = getenv("JFS_LZ4E_SEG_MIN_KB");
+        return (int64_t)(e ? atoi(e) : 64) << 10;
+    }();
+    int64_t tot = 0;
+    for (int b = 0; b < nblk; ++b) tot += lens[b] > 0 ? lens[b] : 0;
+    int64_t L = lmin;
+    while (L * 2048 < tot) L <<= 1;
+    return L;
+}
+struct EsegLayout {
+    int64_t nseg, L, cap, o_int, o_i64, o_st, o_seq, o_map, total;
+};
+int64_t a16(int64_t x) { return (x + 15) & ~(int64_t)15; }
+EsegLayout eseg_layout(int nblk, const int32_t *lens) {
+    using namespace jfs::lz4e;
+    EsegLayout y;
+    y.L = eseg_len(nblk, lens);
+    y.cap = y.L / 8 + 1024;  // sequences per segment (more: the block takes the serial kernel)
+    y.nseg = 0;
+    int64_t maps = 0;
+    for (int b = 0; b < nblk; ++b) {
+        const int64_t n = lens[b];
+        if (n >= kSegMinInput && n <= kMaxInput) {
+            y.nseg += n / y.L > 0 ? n / y.L : 1;
+            maps += 2 * ((n + 63) & ~(int64_t)63);
+        }
+    }
+    const int64_t S = y.nseg, B = nblk;
+    y.o_int = 0;  // seg_blk, seg_k, seq_n [S]; first, nsegb, fail, todo [B]; diff [(R+1) B]
+    y.o_i64 = a16(y.o_int + 4 * (3 * S + 4 * B + (kSegRoundsMax + 1) * B));
+    y.o_st = a16(y.o_i64 + 8 * (4 * S + 2 * B));  // seg_lo, seg_hi, anchor0, seg_bytes [S]; map_off, mlen [B]
+    y.o_seq = a16(y.o_st + (int64_t)sizeof(SegState) * 2 * S);
+    y.o_map = (y.o_seq + (int64_t)sizeof(Seq) * y.cap * S + 63) & ~(int64_t)63;
+    y.total = y.o_map + maps;
+    return y;
+}
+}  // namespace
+
+extern "C" int64_t jfs_lz4_eseg_scratch_bytes(int nblk, const int32_t *lens) {
+    return nblk > 0 ? eseg_layout(nblk, lens).total : 0;
+}
+
+extern "C" int jfs_launch_lz4_encode_seg(const jfs_dev_block *d_blocks, int nblk, const int32_t *lens, int32_t *d_ret,
+                                         void *scratch, int64_t scratch_cap, hipStream_t st) {
+    using namespace jfs::lz4e;
+    if (nblk <= 0) return 0;
+    const EsegLayout y = eseg_layout(nblk, lens);
+    if (y.total > scratch_cap) return -1;
+    uint8_t *base = (uint8_t *)scratch;
+    const int64_t S = y.nseg, B = nblk;
+    SegCtl c{};
+    c.nseg = (int)S;
+    c.nblk = nblk;
+    c.cap = (int)y.cap;
+    c.warm = eseg_warm();
+    int32_t *pi = (int32_t *)(base + y.o_int);
+    c.seg_blk = pi;
+    c.seg_k = pi + S;
+    c.seq_n = pi + 2 * S;
+    c.first = pi + 3 * S;
+    c.nsegb = c.first + B;
+    c.fail = c.nsegb + B;
+    c.todo = c.fail + B;
+    c.diff = c.todo + B;
+    int64_t *pl = (int64_t *)(base + y.o_i64);
+    c.seg_lo = pl;
+    c.seg_hi = pl + S;
+    c.anchor0 = pl + 2 * S;
+    c.seg_bytes = pl + 3 * S;
+    c.map_off = pl + 4 * S;
+    c.mlen = c.map_off + B;
+    c.st = base + y.o_st;
+    c.seq = (Seq *)(base + y.o_seq);
+    c.map = base + y.o_map;
+    // counters, flags and stop states zeroed; the maps zeroed (no stale round marks)
+    if (hipMemsetAsync(base, 0, (size_t)y.o_seq, st) != hipSuccess) return -1;
+    if (y.total > y.o_map && hipMemsetAsync(base + y.o_map, 0, (size_t)(y.total - y.o_map), st) != hipSuccess) return -1;
+    hipLaunchKernelGGL(eseg_plan_kernel, dim3(1), dim3(kPlanThreads), 0, st, d_blocks, nblk, y.L, c);
+    const int R = eseg_rounds();
+    int64_t maxml = 0;
+    for (int b = 0; b < nblk; ++b) maxml = lens[b] > maxml ? lens[b] : maxml;
+    const unsigned nchunk = (unsigned)((maxml + 63 + kCmpChunk - 1) / kCmpChunk);
+    if (S > 0) {
+        for (int r = 1; r <= R; ++r) {
+            c.round = r;
+            hipLaunchKernelGGL(lz4_encode_kernel_t<true>, dim3((unsigned)S), dim3(64), 0, st, d_blocks, nblk, d_ret,
+                               (const int32_t *)nullptr, c);
+            if (r >= 2) hipLaunchKernelGGL(eseg_cmp_kernel, dim3(nchunk, (unsigned)B), dim3(256), 0, st, c);
+        }
+        hipLaunchKernelGGL(eseg_size_kernel, dim3((unsigned)S), dim3(64), 0, st, c, R);
+        hipLaunchKernelGGL(eseg_emit_kernel, dim3((unsigned)S), dim3(64), 0, st, d_blocks, d_ret, c, R);
+    }
+    // blocks below the segment size, unsettled or overflowed: the serial parse
+    hipLaunchKernelGGL(lz4_encode_kernel_t<false>, dim3(nblk), dim3(64), 0, st, d_blocks, nblk, d_ret,
+                       (const int32_t *)c.todo, SegCtl{});
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int jfs_lz4_eseg_counts(uint64_t *out, int reset) {
+    unsigned long long z[jfs::lz4e::kSegRoundsMax + 1] = {0};
+    if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(jfs::lz4e::g_eseg), sizeof(z)) != hipSuccess) return -1;
+    if (reset && hipMemcpyToSymbol(HIP_SYMBOL(jfs::lz4e::g_eseg), z, sizeof(z)) != hipSuccess) return -1;
+    return 0;
 }
 
 #ifdef JFS_PROF

@@ -72,6 +72,23 @@ def lz4_split_counts(reset: bool = False):
     return tuple(int(x) for x in out)
 
 
+def lz4_compress_small(desc: torch.Tensor, ret: torch.Tensor, src_lens, stream=None):
+    """jfs_lz4_compress_device_small: few blocks, each parsed as segments
+    across the GPU (same bytes as lz4_compress); src_lens = host copies."""
+    n = desc.numel() // DESC_DTYPE.itemsize
+    sl = (ctypes.c_int32 * max(n, 1))(*[int(x) for x in src_lens])
+    _check(L.load().jfs_lz4_compress_device_small(desc.data_ptr(), sl, n, ret.data_ptr(), _stream_ptr(stream)),
+           "jfs_lz4_compress_device_small")
+
+
+def lz4_eseg_counts(reset: bool = False):
+    """Segment encoder: {rounds: blocks settled after that many rounds}, with
+    0 = blocks handed to the serial kernel."""
+    out = (ctypes.c_uint64 * 17)()
+    _check(L.load().jfs_lz4_eseg_counts(out, 1 if reset else 0), "jfs_lz4_eseg_counts")
+    return {i: int(x) for i, x in enumerate(out) if x}
+
+
 def zstd_decompress(desc: torch.Tensor, ret: torch.Tensor, stream=None):
     n = desc.numel() // DESC_DTYPE.itemsize
     _check(L.load().jfs_zstd_decompress_device(desc.data_ptr(), n, ret.data_ptr(), _stream_ptr(stream)),

@@ -1,0 +1,115 @@
+"""GPU: the segment-parallel LZ4 encoder (lz4_encode.hip, segment mode) must
+write exactly LZ4_compress_default's bytes -- the serial parse of
+pkg/compress/compress.go:115-117 -- on every input: it cuts a block into
+segments, re-parses each from the state the segment before it stopped in, and
+uses the result only once a round changes nothing; blocks that do not settle
+(or overflow a segment's sequence list) are encoded by the serial kernel.
+Checked against the CPU oracle (oracle/lz4_oracle.c, pinned by liblz4 1.9.3
+golden vectors) and against the serial GPU kernel, on text, zero, random and
+mixed blocks whose content changes at the segment boundaries."""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from juicefs_amd import compress as C
+from juicefs_amd import device as D
+from juicefs_amd.blockgen import gen_block
+
+pytestmark = pytest.mark.gpu
+
+
+def _encode_both(srcs, caps=None):
+    """(segment-mode results, serial-kernel results) as lists of bytes / 0."""
+    dev = torch.device("cuda:0")
+    n = len(srcs)
+    caps = caps or [D.lz4_bound(len(s)) for s in srcs]
+    soff = np.cumsum([0] + [(len(s) + 255) // 256 * 256 for s in srcs])
+    doff = np.cumsum([0] + [(c + 255) // 256 * 256 for c in caps])
+    raw = torch.zeros(int(soff[-1]) + 256, dtype=torch.uint8)
+    for i, s in enumerate(srcs):
+        if s:
+            raw[int(soff[i]):int(soff[i]) + len(s)] = torch.frombuffer(bytearray(s), dtype=torch.uint8)
+    raw = raw.to(dev)
+    outs = []
+    for small in (True, False):
+        comp = torch.zeros(int(doff[-1]) + 256, dtype=torch.uint8, device=dev)
+        desc = D.make_desc(raw, soff[:-1], [len(s) for s in srcs], comp, doff[:-1], caps)
+        ret = torch.zeros(n, dtype=torch.int32, device=dev)
+        if small:
+            D.lz4_compress_small(desc, ret, [len(s) for s in srcs])
+        else:
+            D.lz4_compress(desc, ret)
+        torch.cuda.synchronize()
+        r = ret.cpu().numpy()
+        host = comp.cpu().numpy()
+        outs.append([bytes(host[int(doff[i]):int(doff[i]) + int(r[i])]) if r[i] > 0 else int(r[i]) for i in range(n)])
+    return outs
+
+
+def _mixed(seed, n, pieces):
+    """Text with zero runs and random runs placed across 64 KiB boundaries."""
+    rng = random.Random(seed)
+    b = bytearray(gen_block("T", seed, n))
+    for _ in range(pieces):
+        at = (rng.randrange(1, max(2, n >> 16)) << 16) + rng.randrange(-3000, 3000)
+        ln = rng.choice([40, 300, 5000, 70000])
+        at = max(0, min(at, n - ln))
+        fill = bytes(ln) if rng.random() < 0.5 else gen_block("R", seed + at, ln)
+        b[at:at + ln] = fill
+    return bytes(b)
+
+
+def test_eseg_matches_oracle_and_serial(gpu, oracle):
+    D.lz4_eseg_counts(reset=True)
+    srcs = [gen_block("T", 11, 4 << 20), gen_block("T", 12, (4 << 20) - 7), gen_block("T", 13, 1 << 20),
+            gen_block("T", 14, 65547), gen_block("T", 15, 65546), gen_block("T", 16, 200001),
+            gen_block("Z", 17, 4 << 20), gen_block("R", 18, 1 << 20), b"", gen_block("T", 19, 5),
+            _mixed(20, 4 << 20, 12), _mixed(21, 3 << 20, 30), _mixed(22, 1 << 20, 6)]
+    seg, ser = _encode_both(srcs)
+    for i, s in enumerate(srcs):
+        want = oracle.lz4_compress(s)[1]
+        assert seg[i] == want, (i, len(s))
+        assert ser[i] == want, (i, len(s))
+    cnt = D.lz4_eseg_counts()
+    # every text block of >= 65547 bytes settles (the random block is handed to
+    # the serial kernel after its first segment finds no match)
+    assert sum(v for k, v in cnt.items() if k > 0) >= 8, cnt
+
+
+def test_eseg_limited_output(gpu, oracle):
+    """dst_cap below the bound: the whole output or 0, like LZ4_compress_default."""
+    src = gen_block("T", 31, 1 << 20)
+    full = oracle.lz4_compress(src)[1]
+    caps = [len(full), len(full) - 1, len(full) + 1, 1000, D.lz4_bound(len(src))]
+    seg, ser = _encode_both([src] * len(caps), caps)
+    for c, a, b in zip(caps, seg, ser):
+        want = full if c >= len(full) else 0
+        assert a == want and b == want, c
+
+
+def test_eseg_dense_sequences_overflow_to_serial(gpu, oracle):
+    """4-byte words from a small vocabulary: a sequence every ~5 bytes, more
+    than a segment's sequence list holds -> the serial kernel takes the block,
+    same bytes."""
+    rng = random.Random(5)
+    words = [bytes(rng.randrange(256) for _ in range(4)) for _ in range(64)]
+    src = b"".join(rng.choice(words) for _ in range((2 << 20) // 4))
+    D.lz4_eseg_counts(reset=True)
+    seg, ser = _encode_both([src])
+    want = oracle.lz4_compress(src)[1]
+    assert seg[0] == want and ser[0] == want
+    assert D.lz4_eseg_counts().get(0, 0) == 1
+
+
+def test_eseg_many_blocks_and_batch_api(gpu, oracle):
+    """A 64-block batch through the host batch ABI (segment path below
+    JFS_LZ4E_SEG_MAX blocks), ragged sizes."""
+    rng = random.Random(9)
+    srcs = [gen_block("TTTZ"[i % 4], 400 + i, rng.randrange(60000, 1 << 20)) for i in range(64)]
+    c = C.LZ4()
+    pairs = [(bytearray(c.CompressBound(len(s))), s) for s in srcs]
+    res = c.CompressBatch(pairs)
+    for (d, s), (n, err) in zip(pairs, res):
+        assert err is None and bytes(d[:n]) == oracle.lz4_compress(s)[1]
