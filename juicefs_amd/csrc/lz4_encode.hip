@@ -218,10 +218,57 @@ __device__ __forceinline__ void put_len(Smem &s, Enc &e, uint32_t len) {
     put1(s, e, len % 255);
 }
 
+// Copy source bytes [spos, spos + len) to output positions [dpos, ...) in HBM
+// directly (nothing at or beyond cap): aligned 16-byte stores, the source
+// read as dwords + v_alignbyte, four pieces per lane in flight (4 KiB per
+// step).  For long literal runs (incompressible data), which through the LDS
+// ring cost one dependent byte load per 64 bytes.
+__device__ void copy_direct(Enc &e, int64_t dpos, int64_t spos, int64_t len) {
+    const int l = lane_id();
+    int64_t end = dpos + len;
+    if (end > e.cap) end = e.cap;
+    if (end <= dpos) return;
+    const int64_t delta = spos - dpos;
+    int64_t a = dpos + (int64_t)((16u - ((e.dmis + (uint32_t)dpos) & 15u)) & 15u);
+    if (a > end) a = end;
+    if (l < a - dpos) e.dst[dpos + l] = e.src[dpos + l + delta];
+    int64_t lim = end;
+    if (lim > e.n - 4 - delta) lim = e.n - 4 - delta;  // the dword reads stay inside the source
+    const int64_t b = lim > a ? a + ((lim - a) & ~(int64_t)15) : a;
+    for (int64_t x0 = a + 16 * l; x0 < b; x0 += 4096) {
+        uint4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t x = x0 + 1024 * u;
+            if (x < b) {
+                const uintptr_t p = (uintptr_t)(e.src + x + delta);
+                const gc_u32 *w = (const gc_u32 *)(p & ~(uintptr_t)3);
+                const uint32_t sh = (uint32_t)(p & 3);
+                const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
+                v[u] = make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                                  __builtin_amdgcn_alignbyte(w3, w2, sh), __builtin_amdgcn_alignbyte(w4, w3, sh));
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t x = x0 + 1024 * u;
+            if (x < b) *(g_u4 *)(e.dst + x) = v[u];
+        }
+    }
+    for (int64_t x = b + l; x < end; x += 64) e.dst[x] = e.src[x + delta];
+}
+
 // copy literals src[from, from+len) into the output
 __device__ __forceinline__ void put_lits(Smem &s, Enc &e, int64_t from, int64_t len, int64_t keep_from,
                                          int32_t pre = -1) {
     const int l = lane_id();
+    if (len >= 2048) {  // long run: flush the ring (token and length bytes), copy HBM -> HBM
+        oflush2(s, e, e.op);
+        copy_direct(e, e.op, from, len);
+        e.op += len;
+        e.F = e.op < e.cap ? e.op : e.cap;
+        return;
+    }
     for (int64_t k = 0; k < len; k += 64) {
         maybe_flush(s, e, keep_from);
         if (e.op + 64 + 16 - e.F > OB) {
