@@ -483,6 +483,62 @@ def mixed_host_path(raw_src, nblk=4096, seed=11):
                     "GPU encoders and decoders, every block verified"}
 
 
+def ranked_host_path(S, world, rank, local, dev, nblk, U):
+    """BASELINE configs[0] on every rank (N > 1): each process compresses and
+    decompresses its own nblk host blocks through jfs_{de,}compress_batch
+    with device_mask = its GPU only (the batch ABI's device selection,
+    SURVEY.md 8e), timed between barriers, max over ranks; value = all ranks'
+    uncompressed bytes / that time.  The library's per-device counters show
+    which GPU each rank's blocks ran on."""
+    import torch
+    from juicefs_amd import _lib as L
+    from juicefs_amd import compress as C
+    from juicefs_amd import device as D
+    mask = 1 << local
+    raw = np.empty(nblk * U, dtype=np.uint8)
+    dbuf = torch.empty(nblk * U, dtype=torch.uint8, device=dev)
+    D.gen_blocks(dbuf, nblk, U, "T", S.seed_base(rank, nblk) + 70001)
+    raw[:] = dbuf.cpu().numpy()
+    del dbuf
+    c = C.LZ4()
+    bound = c.CompressBound(U)
+    comp = np.zeros(nblk * bound, dtype=np.uint8)
+    pairs = [(comp[i * bound:(i + 1) * bound], raw[i * U:(i + 1) * U]) for i in range(nblk)]
+    res = c.CompressBatch(pairs, device_mask=mask)  # warm: staging pinned, scratch sized
+    lib = L.load()
+    lib.jfs_stats_reset()
+    holder = {}
+
+    def comp_step():
+        holder["c"] = c.CompressBatch(pairs, device_mask=mask)
+    tc = S.max_over_ranks(S.timed_steps(comp_step, 1, 0, lambda: None, world), world, dev)
+    res = holder["c"]
+    sizes = [n for n, e in res]
+    ok = all(e is None and n > 0 for n, e in res)
+    out = np.zeros(nblk * U, dtype=np.uint8)
+    dpairs = [(out[i * U:(i + 1) * U], comp[i * bound:i * bound + sizes[i]]) for i in range(nblk)]
+    c.DecompressBatch(dpairs, device_mask=mask)  # warm
+
+    def dec_step():
+        holder["d"] = c.DecompressBatch(dpairs, device_mask=mask)
+    td = S.max_over_ranks(S.timed_steps(dec_step, 1, 0, lambda: None, world), world, dev)
+    ok = ok and all(e is None and n == U for n, e in holder["d"]) and np.array_equal(out, raw)
+    if not S.all_ranks_ok(ok, world, dev):
+        raise RuntimeError("ranked host path: round trip mismatch on some rank")
+    ds = (L.JfsDeviceStat * 64)()
+    nd = lib.jfs_device_stats(ds, 64)
+    mine = {int(ds[i].device): int(ds[i].blocks) for i in range(nd) if ds[i].blocks}
+    # every rank's blocks ran on its own GPU only
+    only_mine = S.all_ranks_ok(set(mine) == {local}, world, dev)
+    total = world * nblk * U
+    return {"decompress": {"value": total / td / 2**30, "unit": "GiB/s", "s": td},
+            "compress": {"value": total / tc / 2**30, "unit": "GiB/s", "s": tc},
+            "blocks_per_gpu": nblk, "n_gpus": world, "scaling": "weak",
+            "rank0_device_blocks": mine, "each_rank_used_only_its_gpu": bool(only_mine),
+            "path": "configs[0] per rank: jfs_compress_batch / jfs_decompress_batch with device_mask = 1 << "
+                    "local_rank, host buffers, barrier-bracketed, max over ranks; every block verified"}
+
+
 # ---------------------------------------------------------------------------
 # device-resident sub-records (every rank)
 # ---------------------------------------------------------------------------
@@ -739,6 +795,11 @@ def main():
             out["lz4_other_classes"] = other_classes(a, S, world, rank, dev)
         except Exception as e:
             out["lz4_other_classes"] = {"error": repr(e)}
+    if extras and a.codec == "lz4" and world > 1 and not a.no_host_path:
+        try:
+            out["host_path_ranked"] = ranked_host_path(S, world, rank, local, dev, a.c0_blocks // 4, U)
+        except Exception as e:
+            out["host_path_ranked"] = {"error": repr(e)}
     if rank == 0 and world == 1:
         # bounded sample for the CPU legs: 32 distinct blocks of the headline batch
         ns = min(32, nblk)
