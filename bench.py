@@ -267,7 +267,7 @@ def cpu_codec_legs(raw_blocks, comp_blocks, zstd_frames, U, seconds):
 # ---------------------------------------------------------------------------
 # host-buffer legs (C ABI batch entry points: what the cgo drop-in calls)
 # ---------------------------------------------------------------------------
-def host_path_rate(comp_blocks, raw_blocks, U, nblk, reps=2):
+def host_path_rate(comp_blocks, raw_blocks, U, nblk, reps=2, device_mask=0):
     """PCIe-inclusive: Go-heap-like host buffers -> pinned -> HBM -> kernel ->
     pinned -> host buffers, via the C ABI batch entry points, chunked and
     pipelined over two streams (capi.hip run_batch).  Host clock around the
@@ -277,11 +277,11 @@ def host_path_rate(comp_blocks, raw_blocks, U, nblk, reps=2):
     k = max(1, nblk // len(comp_blocks))
     srcs = (comp_blocks * k)[:nblk]
     pairs = [(bytearray(U), cb) for cb in srcs]
-    c.DecompressBatch(pairs[:4])
+    c.DecompressBatch(pairs[:4], device_mask=device_mask)
     res_d = 0.0
     for _ in range(reps):
         t0 = time.perf_counter()
-        res = c.DecompressBatch(pairs)
+        res = c.DecompressBatch(pairs, device_mask=device_mask)
         dt = time.perf_counter() - t0
         assert all(n == U and e is None for n, e in res)
         res_d = max(res_d, len(pairs) * U / dt / 2**30)
@@ -291,7 +291,7 @@ def host_path_rate(comp_blocks, raw_blocks, U, nblk, reps=2):
     raws = (raw_blocks * (ncb // len(raw_blocks) + 1))[:ncb]
     cpairs = [(bytearray(bound), rb) for rb in raws]
     t0 = time.perf_counter()
-    res = c.CompressBatch(cpairs)
+    res = c.CompressBatch(cpairs, device_mask=device_mask)
     dt = time.perf_counter() - t0
     assert all(n > 0 and e is None for n, e in res)
     return {"lz4_decompress": {"value": res_d, "unit": "GiB/s"},
@@ -441,7 +441,7 @@ def configs0_roundtrip(dev, nblk, U, seed_base=90001):
                     "value = uncompressed bytes / (compress s + decompress s)"}
 
 
-def mixed_host_path(raw_src, nblk=4096, seed=11):
+def mixed_host_path(raw_src, nblk=4096, seed=11, device_mask=0):
     """BASELINE configs[4] on one GPU: mixed LZ4/Zstd blocks of 64 KiB-4 MiB
     (log-uniform sizes, codec alternating), host buffers in and out through the
     C ABI batch entry points.  Every block is checked against its source."""
@@ -457,7 +457,7 @@ def mixed_host_path(raw_src, nblk=4096, seed=11):
     t0 = time.perf_counter()
     for name, cd in codecs.items():
         pairs = [(bytearray(cd.CompressBound(len(raws[i]))), raws[i]) for i in idx[name]]
-        res = cd.CompressBatch(pairs)
+        res = cd.CompressBatch(pairs, device_mask=device_mask)
         for (buf, _), (n, e), i in zip(pairs, res, idx[name]):
             if e is not None or n <= 0:
                 raise RuntimeError(f"mixed compress failed: {name} block {i}: {e}")
@@ -467,7 +467,7 @@ def mixed_host_path(raw_src, nblk=4096, seed=11):
     for _ in range(2):
         outs = {name: [(bytearray(len(raws[i])), comp[i]) for i in idx[name]] for name in codecs}
         t0 = time.perf_counter()
-        res = {name: codecs[name].DecompressBatch(outs[name]) for name in codecs}
+        res = {name: codecs[name].DecompressBatch(outs[name], device_mask=device_mask) for name in codecs}
         td = time.perf_counter() - t0
         for name in codecs:
             for (buf, _), (n, e), i in zip(outs[name], res[name], idx[name]):
@@ -481,6 +481,28 @@ def mixed_host_path(raw_src, nblk=4096, seed=11):
             "sizes": "log-uniform 64 KiB-4 MiB, LZ4 and Zstd alternating",
             "path": "BASELINE configs[4] on 1 GPU: jfs_{de,}compress_batch per codec, host buffers in and out, "
                     "GPU encoders and decoders, every block verified"}
+
+
+def dealer_legs(batch, U, a):
+    """Rank 0 with device_mask = all GPUs: host_path (LZ4 decompress and
+    compress of host buffers) and configs[4] (mixed LZ4/Zstd, 64 KiB-4 MiB),
+    the batch ABI dealing blocks round-robin over every visible device; the
+    per-device block counters show the spread."""
+    from juicefs_amd import _lib as L
+    ns = min(32, batch.nblk)
+    comp = [batch.comp[i * batch.slot:i * batch.slot + int(batch.csize[i])].cpu().numpy().tobytes() for i in range(ns)]
+    raws = [batch.raw[i * U:(i + 1) * U].cpu().numpy().tobytes() for i in range(ns)]
+    lib = L.load()
+    lib.jfs_stats_reset()
+    out = {"host_path": host_path_rate(comp, raws, U, a.host_blocks, device_mask=0)}
+    if not a.no_mixed:
+        out["mixed_host_path"] = mixed_host_path(raws, a.mixed_blocks, device_mask=0)
+    ds = (L.JfsDeviceStat * 64)()
+    nd = lib.jfs_device_stats(ds, 64)
+    out["device_blocks"] = {int(ds[i].device): int(ds[i].blocks) for i in range(nd)}
+    out["path"] = ("rank 0 alone, jfs_{de,}compress_batch with device_mask 0 (every visible GPU), blocks dealt "
+                   "round-robin, one host thread per device; host buffers in and out")
+    return out
 
 
 def ranked_host_path(S, world, rank, local, dev, nblk, U):
@@ -800,6 +822,15 @@ def main():
             out["host_path_ranked"] = ranked_host_path(S, world, rank, local, dev, a.c0_blocks // 4, U)
         except Exception as e:
             out["host_path_ranked"] = {"error": repr(e)}
+        # the single-process dealer (north_star's form of configs[4]): rank 0
+        # alone drives every visible GPU through the batch ABI (device_mask 0
+        # = all), round-robin per block; the other ranks wait at the barrier
+        if rank == 0:
+            try:
+                out["dealer_all_gpus"] = dealer_legs(batch, U, a)
+            except Exception as e:
+                out["dealer_all_gpus"] = {"error": repr(e)}
+        S._barrier(world)
     if rank == 0 and world == 1:
         # bounded sample for the CPU legs: 32 distinct blocks of the headline batch
         ns = min(32, nblk)

@@ -203,3 +203,32 @@ def test_device_mask_round_robin(gpu):
     # a mask naming no visible device
     with pytest.raises(C.CompressError):
         lz.CompressBatch(a, device_mask=1 << 31)
+
+
+def test_blocks_dealt_to_distinct_devices(gpu, oracle):
+    """with two or more GPUs a batch's blocks are dealt
+    round-robin over the devices in device_mask -- every selected device runs
+    some of them (jfs_device_stats) and every output is the oracle's.  With
+    one GPU the deal degenerates to that device, which is checked instead."""
+    import torch
+    ndev = torch.cuda.device_count()
+    lib = L.load()
+    lz = C.LZ4()
+    srcs = [gen_block("TZR"[i % 3], 700 + i, 30000 + 4099 * i) for i in range(24)]
+    comps = [oracle.lz4_compress(s)[1] for s in srcs]
+    lib.jfs_stats_reset()
+    cp = [(bytearray(lz.CompressBound(len(s))), s) for s in srcs]
+    res = lz.CompressBatch(cp)
+    assert all(e is None and bytes(d[:n]) == c for (d, _), (n, e), c in zip(cp, res, comps))
+    dp = [(bytearray(len(s)), c) for s, c in zip(srcs, comps)]
+    res = lz.DecompressBatch(dp)
+    assert all(e is None and bytes(d) == s for (d, _), (n, e), s in zip(dp, res, srcs))
+    ds = (L.JfsDeviceStat * 64)()
+    nd = lib.jfs_device_stats(ds, 64)
+    used = {int(ds[i].device): int(ds[i].blocks) for i in range(nd) if ds[i].blocks}
+    assert sum(used.values()) == 2 * len(srcs)
+    if ndev >= 2 and nd >= 2:
+        assert len(used) == min(nd, len(srcs)), used  # every device got blocks
+        assert max(used.values()) - min(used.values()) <= 2 * 1 + 2, used  # round-robin: balanced
+    else:
+        assert len(used) == 1, used
