@@ -375,8 +375,14 @@ def oneshot_concurrency(comp_blocks, raw_blocks, U, n_dec=200, n_enc=20, rounds=
     for t in range(n_enc):
         for r in range(kmax if t == 0 else rounds):
             edst[(t, r)] = bytearray(b"\x01") * bound
-    # warm the coalescer and its staging (pinned once, then reused): bursts
-    # of the timed size, so every lane's slots have grown before timing
+    # warm the coalescer and its staging (pinned once, then reused; growing a
+    # slot pins new memory at ~0.1 s per GiB): one full-size batch per lane at
+    # once (both lanes' first slots), then bursts of the timed size
+    wpairs = [[(bytearray(U), comp_blocks[i % nc]) for i in range(n_dec)] for _ in range(2)]
+    wth = [threading.Thread(target=c.DecompressBatch, args=(wp,)) for wp in wpairs]
+    [x.start() for x in wth]
+    [x.join() for x in wth]
+    del wpairs
     warm = [run(n_dec, rounds, dec, dchk)["device_batches"] for _ in range(2)]
     warm += [run(n_enc, rounds, enc, echk)["device_batches"]]
     out = {"decompress_lone": run(1, 5, dec, dchk), "compress_lone": run(1, 3, enc, echk),

@@ -14,6 +14,7 @@
 // staging and streams per worker).  Batches go host -> pinned staging -> HBM
 // -> kernel -> HBM -> pinned -> host, pipelined in chunks (run_batch).
 #include <hip/hip_runtime.h>
+#include <sched.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -466,27 +467,100 @@ struct CopyJob {
     const uint8_t *src;
     int64_t n;
 };
+// One process-wide pool of copy threads shared by every lane of every device:
+// concurrent batches (two lanes per GPU, up to eight GPUs) interleave their
+// pieces instead of each spawning its own 16 threads, which oversubscribed the
+// CPU quota (a 38 MiB stage-in took 65 ms next to another lane's copy-out).
+// Size: JFS_COPY_THREADS, default min(16, CPUs this process may run on).
+class CopyPool {
+   public:
+    static CopyPool &get() {
+        static CopyPool *p = new CopyPool();  // never destroyed: workers outlive static dtors
+        return *p;
+    }
+    int threads() const { return nthr_; }
+    void run(std::vector<CopyJob> &pc) {
+        Task t;
+        t.pc = pc.data();
+        t.n = pc.size();
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            q_.push_back(&t);
+        }
+        cv_.notify_all();
+        work(t);  // the caller copies too
+        std::unique_lock<std::mutex> lk(mu_);
+        q_.erase(std::find(q_.begin(), q_.end(), &t));  // no worker picks it up any more
+        done_cv_.wait(lk, [&] { return t.done.load() == t.n && t.active == 0; });
+    }
+
+   private:
+    struct Task {
+        CopyJob *pc = nullptr;
+        size_t n = 0;
+        std::atomic<size_t> next{0}, done{0};
+        int active = 0;  // workers inside work(*this) (guarded by mu_)
+    };
+    std::mutex mu_;
+    std::condition_variable cv_, done_cv_;
+    std::deque<Task *> q_;
+    int nthr_ = 1;
+
+    static int cpu_share() {
+        cpu_set_t set;
+        CPU_ZERO(&set);
+        if (sched_getaffinity(0, sizeof(set), &set) == 0) return std::max(1, CPU_COUNT(&set));
+        return (int)std::max(1u, std::thread::hardware_concurrency());
+    }
+    CopyPool() {
+        const char *e = getenv("JFS_COPY_THREADS");
+        nthr_ = e ? std::max(1, atoi(e)) : std::min(16, cpu_share());
+        for (int i = 1; i < nthr_; i++) std::thread([this] { loop(); }).detach();
+    }
+    static void work(Task &t) {
+        for (size_t i; (i = t.next.fetch_add(1)) < t.n;) {
+            memcpy(t.pc[i].dst, t.pc[i].src, (size_t)t.pc[i].n);
+            t.done.fetch_add(1);
+        }
+    }
+    void loop() {
+        for (;;) {
+            Task *t = nullptr;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] {
+                    for (Task *x : q_)
+                        if (x->next.load() < x->n) return true;
+                    return false;
+                });
+                for (Task *x : q_)  // the oldest task with pieces left
+                    if (x->next.load() < x->n) { t = x; break; }
+                if (t) t->active++;
+            }
+            if (!t) continue;
+            work(*t);
+            {
+                std::lock_guard<std::mutex> lk(mu_);
+                if (--t->active == 0) done_cv_.notify_all();
+            }
+        }
+    }
+};
+
 void par_copy(std::vector<CopyJob> &jobs) {
     int64_t total = 0;
     for (const CopyJob &j : jobs) total += j.n;
-    int T = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
-    if (total < (16ll << 20) || T == 1) {
+    CopyPool &pool = CopyPool::get();
+    if (total < (16ll << 20) || pool.threads() == 1) {
         for (const CopyJob &j : jobs) memcpy(j.dst, j.src, (size_t)j.n);
         return;
     }
-    // cut into <= 8 MiB pieces, deal them out in byte-balanced stripes
-    constexpr int64_t PIECE = 8ll << 20;
+    // cut into <= 4 MiB pieces, handed out one at a time
+    constexpr int64_t PIECE = 4ll << 20;
     std::vector<CopyJob> pc;
     for (const CopyJob &j : jobs)
         for (int64_t o = 0; o < j.n; o += PIECE) pc.push_back({j.dst + o, j.src + o, std::min(PIECE, j.n - o)});
-    std::atomic<size_t> next{0};
-    auto work = [&] {
-        for (size_t i; (i = next.fetch_add(1)) < pc.size();) memcpy(pc[i].dst, pc[i].src, (size_t)pc[i].n);
-    };
-    std::vector<std::thread> th;
-    for (int t = 1; t < T; t++) th.emplace_back(work);
-    work();
-    for (auto &t : th) t.join();
+    pool.run(pc);
 }
 
 // JFS_HOST_TRACE=1: per-chunk host timings on stderr (diagnostics)

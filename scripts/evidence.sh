@@ -22,4 +22,9 @@ find $O/kt_lz4 -name '*kernel_stats.csv' -exec cp {} $O/lz4_kernel_stats.csv \;
 timeout -k 10 300 python scripts/prof_run.py 4096 0 T zstd > /dev/null 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt_zstd -o kt --output-format csv -- python scripts/prof_run.py 4096 3 T zstd > $O/kt_zstd.log 2>&1
 find $O/kt_zstd -name '*kernel_stats.csv' -exec cp {} $O/zstd_kernel_stats.csv \;
+# HBM traffic of the Zstd decode kernels (one launch each pass, frames from the cache)
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/zpf -o zpf --output-format csv -- python scripts/prof_run.py 4096 1 T zstd > $O/zpf.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $O/zpw -o zpw --output-format csv -- python scripts/prof_run.py 4096 1 T zstd > $O/zpw.log 2>&1
+find $O/zpf -name '*counter_collection.csv' -exec cp {} $O/zstd_fetch.csv \;
+find $O/zpw -name '*counter_collection.csv' -exec cp {} $O/zstd_write.csv \;
 echo evidence-done
