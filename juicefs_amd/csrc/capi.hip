@@ -25,6 +25,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <deque>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -625,8 +626,12 @@ struct Aead {
 // chunk_limit() staging bytes; the lane's kernels run in chunk order, so a
 // batch is not cut finer than that (a decode kernel over fewer blocks than
 // CUs lasts about one block's latency whatever its size).
+// max_chunk_blocks (> 0) also caps a chunk's block count; on_chunk (optional)
+// is called with [s, e) as soon as those blocks' results and outputs are final
+// (the coalescer releases their callers there, before later chunks finish).
 int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_iov *iov, int64_t *out,
-                  const Aead *ae = nullptr, uint32_t *crc_out = nullptr) {
+                  const Aead *ae = nullptr, uint32_t *crc_out = nullptr, int max_chunk_blocks = 0,
+                  const std::function<void(int, int)> *on_chunk = nullptr) {
     if (nblk <= 0) return JFS_OK;
     DevGuard guard;
     (void)hipSetDevice(dev->id);
@@ -660,7 +665,8 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
             while (c.e < nblk) {
                 const int64_t ci = ae ? iov[c.e].dst_cap : staged_cap(algo, dir, iov[c.e]);
                 const int64_t ib = align16(iov[c.e].src_len), ob = align16(ci);  // = staged_bytes()
-                if (c.e > s && c.tin + c.tout + ib + ob > limit) break;
+                if (c.e > s && (c.tin + c.tout + ib + ob > limit || (max_chunk_blocks > 0 && c.e - s >= max_chunk_blocks)))
+                    break;
                 cap[c.e] = ci;
                 in_off[c.e] = c.tin;
                 out_off[c.e] = c.tout;
@@ -884,7 +890,8 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
         const double t0 = host_trace() ? now_ms() : 0.0;
         par_copy(jobs);
         if (host_trace())
-            fprintf(stderr, "[jfs host] chunk %d-%d stage-in %.1f MiB %.2f ms\n", c.s, c.e, c.tin / 1048576.0, now_ms() - t0);
+            fprintf(stderr, "[jfs host] t=%.2f chunk %d-%d stage-in %.1f MiB %.2f ms\n", now_ms(), c.s, c.e,
+                    c.tin / 1048576.0, now_ms() - t0);
         const int n = c.e - c.s;
         if (ae) return launch_aead(c, sl, h_in, h_out, h_desc, h_ret, d_in, d_out, d_desc, d_ret);
         if (algo != JFS_ALGO_LZ4 && algo != JFS_ALGO_ZSTD) return JFS_ERR_UNSUPPORTED;
@@ -1004,18 +1011,24 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
         }
         par_copy(jobs);
         if (host_trace())
-            fprintf(stderr, "[jfs host] chunk %d-%d wait %.2f ms copy-out %.1f MiB %.2f ms\n", c.s, c.e, t1 - t0,
+            fprintf(stderr, "[jfs host] t=%.2f chunk %d-%d wait %.2f ms copy-out %.1f MiB %.2f ms\n", now_ms(), c.s, c.e, t1 - t0,
                     c.tout / 1048576.0, now_ms() - t1);
         return JFS_OK;
     };
     const int nch = (int)ch.size();
     int64_t rc = JFS_OK;
     int done = 0;  // chunks [0, done) finished
+    auto finish_next = [&]() -> int64_t {
+        const Chunk &c = ch[done++];
+        const int64_t r = finish(c);
+        if (r == JFS_OK && on_chunk) (*on_chunk)(c.s, c.e);
+        return r;
+    };
     for (int k = 0; k < nch && rc == JFS_OK; k++) {
-        if (k >= NSLOT) rc = finish(ch[done++]);
+        if (k >= NSLOT) rc = finish_next();
         if (rc == JFS_OK) rc = launch(ch[k]);
     }
-    while (done < nch && rc == JFS_OK) rc = finish(ch[done++]);
+    while (done < nch && rc == JFS_OK) rc = finish_next();
     if (rc != JFS_OK) {  // leave no copy in flight into the staging slots
         (void)hipStreamSynchronize(dev->s_in);
         (void)hipStreamSynchronize(ln.s_k);
@@ -1077,6 +1090,17 @@ struct Pending {
 struct Gather {
     int64_t gap_us, max_us;
 };
+// Decode batches of the coalescer run in chunks of at most this many blocks
+// (JFS_COALESCE_CHUNK, 0 = by staging bytes only): the first chunk's callers
+// return while later chunks run, and chunk copies / kernels pipeline.
+int coalesce_chunk_blocks() {
+    static int v = [] {
+        const char *e = getenv("JFS_COALESCE_CHUNK");
+        return e ? std::max(0, atoi(e)) : 16;
+    }();
+    return v;
+}
+
 Gather gather_window(int dir) {
     static int64_t g[2] = {-1, -1};
     static std::once_flag once;
@@ -1141,6 +1165,7 @@ class Coalescer {
         std::vector<Pending *> batch;
         std::vector<jfs_iov> iov;
         std::vector<int64_t> out;
+        std::vector<char> released;
         double t_gather = 0.0;
         for (;;) {
             {
@@ -1173,19 +1198,46 @@ class Coalescer {
             cv_work_.notify_all();  // the next worker may start gathering
             iov.resize(batch.size());
             out.assign(batch.size(), 0);
+            released.assign(batch.size(), 0);
             for (size_t i = 0; i < batch.size(); i++) iov[i] = batch[i]->iov;
             {
                 const double t0 = host_trace() ? now_ms() : 0.0;
                 std::lock_guard<std::mutex> llk(ln.mu);
-                run_isolated(dev, ln, batch[0]->algo, batch[0]->dir, (int)batch.size(), iov.data(), out.data());
+                const int algo = batch[0]->algo, dir = batch[0]->dir, n = (int)batch.size();
+                // chunks of a decode batch release their callers as they finish:
+                // those callers' next calls gather while the rest of the batch runs
+                const std::function<void(int, int)> release = [&](int s, int e) {
+                    {
+                        std::lock_guard<std::mutex> lk(mu_);
+                        for (int i = s; i < e; i++) {
+                            batch[i]->res = out[i];
+                            batch[i]->done = true;
+                            released[i] = 1;
+                        }
+                    }
+                    cv_done_.notify_all();
+                };
+                const int cb = dir == DECOMPRESS ? coalesce_chunk_blocks() : 0;
+                if (run_batch(dev, ln, algo, dir, n, iov.data(), out.data(), nullptr, nullptr, cb, &release) != JFS_OK) {
+                    // what was not released yet goes through the error-isolating path
+                    std::vector<int> idx;
+                    for (int i = 0; i < n; i++)
+                        if (!released[i]) idx.push_back(i);
+                    std::vector<jfs_iov> iv2(idx.size());
+                    std::vector<int64_t> o2(idx.size(), 0);
+                    for (size_t k = 0; k < idx.size(); k++) iv2[k] = iov[idx[k]];
+                    run_isolated(dev, ln, algo, dir, (int)idx.size(), iv2.data(), o2.data());
+                    for (size_t k = 0; k < idx.size(); k++) out[idx[k]] = o2[k];
+                }
                 if (host_trace())
-                    fprintf(stderr, "[jfs coalescer] dev %d lane %d algo %d dir %d: %zu calls, gathered %.2f ms, ran %.2f ms\n",
-                            dev->id, (int)(&ln - dev->lane), batch[0]->algo, batch[0]->dir, batch.size(), t0 - t_gather,
-                            now_ms() - t0);
+                    fprintf(stderr, "[jfs coalescer] t=%.2f dev %d lane %d algo %d dir %d: %zu calls, gathered %.2f ms, ran %.2f ms\n",
+                            now_ms(), dev->id, (int)(&ln - dev->lane), batch[0]->algo, batch[0]->dir, batch.size(),
+                            t0 - t_gather, now_ms() - t0);
             }
             {
                 std::lock_guard<std::mutex> lk(mu_);
                 for (size_t i = 0; i < batch.size(); i++) {
+                    if (released[i]) continue;
                     batch[i]->res = out[i];
                     batch[i]->done = true;
                 }
