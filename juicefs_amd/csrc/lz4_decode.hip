@@ -52,6 +52,10 @@ constexpr int RMASK = R - 1;
 #ifndef JFS_LZ4_DP
 #define JFS_LZ4_DP 1  // exit-table parser for windows away from the input end
 #endif
+#ifndef JFS_LZ4_SEG
+#define JFS_LZ4_SEG 128  // segment-walk parser (bytes per lane); 0 = per-window exit-table parser
+#endif
+constexpr int SEG = JFS_LZ4_SEG;
 #ifndef JFS_LZ4_SUBST
 #define JFS_LZ4_SUBST 1  // source-substitution hops per batch (with the whole-wave near fallback: 1 = 2 > 3)
 #endif
@@ -1210,6 +1214,223 @@ __device__ __forceinline__ void table_chain(Smem &s, Ctx &c, int32_t wbase, int3
 }
 #endif
 
+#if JFS_LZ4_SEG
+// ---------------------------------------------------------------------------
+// segment-walk parser (round 3): the token chain of a span of SW = 64 * SEG
+// compressed bytes at once, one SEG-byte segment per lane, read straight from
+// HBM (no staging).  Each lane walks its segment speculatively from SPRE bytes
+// before it (lane 0 from the exact entry), fix-up rounds take each segment's
+// true entry (the previous segment's exit) until nothing changes.  The chain
+// positions stay in the lanes' registers (SEG bits each) while the windows of
+// the span are staged and tabled.  A long segment amortizes the pre-roll and
+// the fix-up over ~SEG/5.6 tokens per lane; the window exit-table parser spent
+// ~29 VALU per byte offset.
+// ---------------------------------------------------------------------------
+static_assert(SEG == 128, "segment bit sets are two u64 per lane");
+constexpr int SW = 64 * SEG;
+#ifndef JFS_LZ4_SPRE
+#define JFS_LZ4_SPRE 32
+#endif
+constexpr int SPRE = JFS_LZ4_SPRE;
+#ifndef JFS_LZ4_SEG_BUDGET
+#define JFS_LZ4_SEG_BUDGET 12  // walk steps of the next span per window
+#endif
+constexpr int SEG_BUDGET = JFS_LZ4_SEG_BUDGET;
+
+// Next token position after p (or STOP | p): the exact chain rule of
+// parse_tok, bytes from HBM.
+__device__ __noinline__ uint32_t g_next_exact(const Ctx &c, int32_t p) {
+    const int32_t n = c.n;
+    if (p > n - 18) return STOP | (uint32_t)p;
+    const uint32_t tb = c.src[p];
+    int32_t q = p + 1;
+    int32_t ll = (int32_t)(tb >> 4);
+    if (ll == 15) {
+        int k = 0;
+        uint32_t sv;
+        do {
+            sv = c.src[q];
+            q++;
+            ll += (int32_t)sv;
+            if (q >= n - 15 || ++k > KEXT) return STOP | (uint32_t)p;
+        } while (sv == 255);
+        if (q + ll > n - 32) return STOP | (uint32_t)p;
+    }
+    q += ll + 2;
+    if ((tb & 15u) == 15u) {
+        int k = 0;
+        uint32_t sv;
+        do {
+            sv = c.src[q];
+            q++;
+            if (q >= n - 4 || ++k > KEXT) return STOP | (uint32_t)p;
+        } while (sv == 255);
+    }
+    return (uint32_t)q;
+}
+
+// Lean step from HBM: the token byte and the byte after it, then the first
+// match-length byte (two dependent load rounds).  A literal length with one
+// extension byte is taken here; tokens with a 255 extension byte (runs of
+// >= 270 literals or >= 274-byte matches) take g_next_exact.
+__device__ __forceinline__ uint32_t g_step(const Ctx &c, int32_t p, bool act) {
+    const int32_t n = c.n;
+    const bool edge = p > n - 18;
+    const int32_t pa = edge ? 0 : p;
+    const uint32_t tb = c.src[pa], e1 = c.src[edge ? 0 : p + 1];
+    const uint32_t llx = (tb >> 4) == 15u ? 1u : 0u;
+    const uint32_t L = llx ? 15u + e1 : (tb >> 4);
+    // parse_tok's end-of-input rules for the literal-length extension
+    const bool lstop = llx && (p + 2 >= n - 15 || p + 2 + (int32_t)L > n - 32);
+    const int32_t q = p + 3 + (int32_t)llx + (int32_t)L;  // first match-length extension byte
+    const uint32_t e2 = c.src[edge || lstop ? 0 : q];
+    const uint32_t mlx = (tb & 15u) == 15u ? 1u : 0u;
+    uint32_t x = (uint32_t)q + mlx;
+    const bool slow = act && !edge && !lstop && ((llx & (e1 == 255u)) | (mlx & (e2 == 255u)));
+    if (edge || lstop || (mlx && (int32_t)x >= n - 4)) x = STOP | (uint32_t)p;
+    if (__ballot(slow)) {
+        if (slow) x = g_next_exact(c, p);
+    }
+    return x;
+}
+
+// 128-bit sets as two u64 (bit d = position plo + d)
+__device__ __forceinline__ bool tbit2(uint64_t a0, uint64_t a1, uint32_t d) {
+    return (((d < 64u ? a0 : a1) >> (d & 63u)) & 1ull) != 0;
+}
+__device__ __forceinline__ void sbit2(uint64_t &a0, uint64_t &a1, uint32_t d) {
+    const uint64_t m = 1ull << (d & 63u);
+    a0 |= d < 64u ? m : 0ull;
+    a1 |= d < 64u ? 0ull : m;
+}
+__device__ __forceinline__ uint64_t from_lo(uint32_t d) { return d < 64u ? (~0ull << (d & 63u)) : 0ull; }
+__device__ __forceinline__ uint64_t from_hi(uint32_t d) { return d < 64u ? ~0ull : (~0ull << (d & 63u)); }
+
+// Chain of the span [base, base + SW), resumable: advance() runs at most
+// `budget` walk steps (one HBM load round each) and returns true once the
+// chain is final, so the parser wave can walk the next span a few steps per
+// window while the copier works (the walk is bound by load latency).
+// Result: vt0/vt1 = true chain positions of this lane's segment, ex = its
+// true exit (first position >= its end, or STOP | p).
+struct SegWalk {
+    int32_t base, plo, phi;
+    int32_t q;            // walk position of a moving lane
+    uint32_t cur;         // entry the current result assumes
+    uint32_t sx, ex;      // speculative / true exit
+    uint64_t vs0, vs1;    // speculative chain positions
+    uint64_t vt0, vt1;    // true chain positions
+    uint64_t vp0, vp1;    // positions of a fix-up walk
+    bool mv;              // this lane is walking
+    int phase;            // 0 speculative walk, 1 fix-up rounds, 2 final
+    bool round;           // a fix-up round is to be started
+    int steps, rounds;
+
+    __device__ __forceinline__ void start(int32_t b) {
+        const int l = lane_id();
+        base = b;
+        plo = b + l * SEG;
+        phi = plo + SEG;
+        cur = l == 0 ? (uint32_t)b : (uint32_t)(plo - SPRE);
+        q = (int32_t)cur;
+        vs0 = vs1 = vt0 = vt1 = vp0 = vp1 = 0;
+        sx = ex = 0;
+        mv = true;
+        phase = 0;
+        round = false;
+        steps = rounds = 0;
+    }
+
+    __device__ __forceinline__ bool advance(Ctx &c, int budget PROF_ARG) {
+        // speculative walks (one load round trip per step for every lane)
+        if (phase == 0) {
+            for (; budget > 0 && __ballot(mv); --budget) {
+                PCOUNT(11, 1);
+                if (mv) {
+                    const uint32_t x = g_step(c, q, true);
+                    const bool stop = (x & STOP) != 0;
+                    if (!stop && q >= plo) sbit2(vs0, vs1, (uint32_t)(q - plo));
+                    const bool out = stop || (int32_t)x >= phi;
+                    sx = out ? x : sx;
+                    mv = !out;
+                    q = (int32_t)x;
+                }
+                if (++steps > SEG + SPRE) { c.bug = 6; phase = 2; return true; }
+            }
+            if (budget == 0) return false;
+            vt0 = vs0;
+            vt1 = vs1;
+            ex = sx;
+            phase = 1;
+            round = true;
+        }
+        // fix-up rounds: true entry = exit of the previous segment; an entry
+        // off the speculative chain walks until it joins it (or leaves)
+        while (phase == 1 && budget > 0) {
+            if (round) {
+                const uint32_t In = dpp_shift_up(ex, (uint32_t)base);
+                const bool ch = In != cur;
+                if (!__ballot(ch)) { phase = 2; break; }
+                if (++rounds > 64) { c.bug = 3; phase = 2; break; }
+                PCOUNT(12, 1);
+                mv = false;
+                if (ch) {
+                    cur = In;
+                    const uint32_t d = In - (uint32_t)plo;
+                    if ((In & STOP) || (int32_t)In >= phi) {
+                        vt0 = vt1 = 0;
+                        ex = In;
+                    } else if (tbit2(vs0, vs1, d)) {
+                        vt0 = vs0 & from_lo(d);
+                        vt1 = vs1 & from_hi(d);
+                        ex = sx;
+                    } else {
+                        mv = true;
+                    }
+                }
+                q = (int32_t)In;
+                vp0 = vp1 = 0;
+                steps = 0;
+                round = false;
+            }
+            for (; budget > 0 && __ballot(mv); --budget) {
+                PCOUNT(13, 1);
+                if (mv) {
+                    const uint32_t d = (uint32_t)(q - plo);
+                    const bool join = tbit2(vs0, vs1, d);
+                    const uint32_t x = g_step(c, q, !join);
+                    const bool stop = !join && (x & STOP) != 0;
+                    if (!join && !stop) sbit2(vp0, vp1, d);
+                    const bool out = join || stop || (int32_t)x >= phi;
+                    if (out) {
+                        vt0 = vp0 | (join ? vs0 & from_lo(d) : 0ull);
+                        vt1 = vp1 | (join ? vs1 & from_hi(d) : 0ull);
+                        ex = join ? sx : x;
+                    }
+                    mv = !out;
+                    q = (int32_t)x;
+                }
+                if (++steps > SEG + 1) { c.bug = 7; phase = 2; return true; }
+            }
+            if (!__ballot(mv)) round = true;
+        }
+        return phase == 2;
+    }
+};
+
+// Dword k (0..4*64-1) of the span's bit set; lane k/4 holds it as dword k%4 of
+// (vt0, vt1).  Out-of-span dwords read as 0.
+__device__ __forceinline__ uint32_t span_dword(uint64_t vt0, uint64_t vt1, int32_t k) {
+    const int src = (k >> 2) & 63;
+    const uint32_t d0 = (uint32_t)__shfl((int)(uint32_t)vt0, src, 64);
+    const uint32_t d1 = (uint32_t)__shfl((int)(uint32_t)(vt0 >> 32), src, 64);
+    const uint32_t d2 = (uint32_t)__shfl((int)(uint32_t)vt1, src, 64);
+    const uint32_t d3 = (uint32_t)__shfl((int)(uint32_t)(vt1 >> 32), src, 64);
+    const uint32_t j = (uint32_t)k & 3u;
+    const uint32_t v = j == 0 ? d0 : j == 1 ? d1 : j == 2 ? d2 : d3;
+    return (k >= 0 && k < 4 * 64) ? v : 0u;
+}
+#endif
+
 // ---------------------------------------------------------------------------
 // parser wave: stage one window, find its true token chain, write the table
 // ---------------------------------------------------------------------------
@@ -1260,6 +1481,80 @@ __device__ __forceinline__ void parse_window(Smem &s, Ctx &c, int32_t wbase, uin
     PSTAMP(2);
 }
 
+#if JFS_LZ4_SEG
+// The chain of one span (seg_chain), kept by the parser wave across windows.
+struct Span {
+    uint64_t v0, v1;  // this lane's segment bits
+    int32_t base;     // span start (a true chain position)
+    uint32_t exit;    // first chain position >= base + SW, or STOP | p
+};
+
+// Stage the window at wbase and table its tokens from the span's chain: the
+// window ends at cbase + CW or at the span's end, whichever comes first.
+__device__ __forceinline__ void parse_window_seg(Smem &s, Ctx &c, int32_t wbase, const Span &sp, uint32_t *T_out,
+                                                 uint32_t *efin_out PROF_ARG) {
+    static_assert(P == 32, "a window lane covers one dword of the span bit set");
+    const int l = lane_id();
+    stage_window(s, c, wbase);
+    const int32_t cbase = c.cbase;
+    PCOUNT(10, 1);
+    __builtin_amdgcn_wave_barrier();
+    PSTAMP(0);
+    const int32_t send = sp.base + SW;
+    const int32_t wend = cbase + CW < send ? cbase + CW : send;
+    // lane l: positions [cbase + 32 l, + 32) = span bits [o, o + 32)
+    const int32_t o = cbase - sp.base + 32 * l;  // >= -15
+    const int32_t K = o >> 5;
+    const uint32_t lo = span_dword(sp.v0, sp.v1, K), hi = span_dword(sp.v0, sp.v1, K + 1);
+    uint32_t field = __builtin_amdgcn_alignbit(hi, lo, (uint32_t)o & 31u);
+    const int32_t plo = cbase + 32 * l;
+    const int32_t a = wbase - plo, b = wend - plo;  // keep bits [a, b)
+    const uint32_t ma = a <= 0 ? 0xFFFFFFFFu : a >= 32 ? 0u : (0xFFFFFFFFu << a);
+    const uint32_t mb = b >= 32 ? 0xFFFFFFFFu : b <= 0 ? 0u : ((1u << b) - 1u);
+    field &= ma & mb;
+    PSTAMP(1);
+    // token table: positions (relative to cbase) in stream order
+    const uint32_t cnt = (uint32_t)__builtin_popcount(field);
+    const uint32_t cinc = dpp_scan_add(cnt);
+    const uint32_t tall = readlane(cinc, 63);
+    *T_out = tall < (uint32_t)TCAP ? tall : (uint32_t)TCAP;
+    uint32_t ex = 0;
+    {
+        uint32_t idx = cinc - cnt;
+        uint32_t v = field;
+        while (__ballot(v != 0)) {
+            if (v) {
+                const uint32_t bb = (uint32_t)__builtin_ctz(v);
+                if (idx < (uint32_t)TCAP) c.tab[idx] = (uint16_t)((uint32_t)l * P + bb);
+                else if (idx == (uint32_t)TCAP) ex = (uint32_t)plo + bb;  // first token left to the next window
+                idx++;
+                v &= v - 1;
+            }
+        }
+    }
+    if (tall > (uint32_t)TCAP) {  // the window ends at token TCAP
+        const uint64_t hit = __ballot(cinc - cnt <= (uint32_t)TCAP && (uint32_t)TCAP < cinc);
+        *efin_out = readlane(ex, (int)__builtin_ctzll(hit));
+    } else if (wend >= send) {
+        *efin_out = sp.exit;
+    } else {
+        // first chain position >= wend inside the span, else the span's exit
+        const int32_t d = wend - sp.base - l * SEG;
+        const uint32_t dd = d < 0 ? 0u : (uint32_t)d;
+        const uint64_t m0 = d >= SEG ? 0ull : sp.v0 & from_lo(dd), m1 = d >= SEG ? 0ull : sp.v1 & from_hi(dd);
+        const uint64_t any = __ballot((m0 | m1) != 0ull);
+        if (any) {
+            const int f = (int)__builtin_ctzll(any);
+            const uint32_t bit = m0 ? (uint32_t)__builtin_ctzll(m0) : 64u + (uint32_t)__builtin_ctzll(m1 | (1ull << 63));
+            *efin_out = (uint32_t)sp.base + (uint32_t)(f * SEG) + readlane(bit, f);
+        } else {
+            *efin_out = sp.exit;
+        }
+    }
+    PSTAMP(2);
+}
+#endif
+
 // LDS-only workgroup barrier between the parser and copier waves
 __device__ __forceinline__ void wg_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
@@ -1278,6 +1573,16 @@ __device__ __forceinline__ void use_buffer(Smem &s, Ctx &c, int buf) {
 __device__ __forceinline__ void parser_wave(Smem &s, Ctx &c PROF_ARG) {
     int32_t pip = 0;
     bool pstop = false;
+#if JFS_LZ4_SEG
+    Span sp;
+    sp.v0 = sp.v1 = 0;
+    sp.base = 0;
+    sp.exit = 0;
+    bool spv = false;  // sp describes the chain from sp.base
+    bool nxt = false;  // wk walks the span that follows sp
+    SegWalk wk;
+    wk.start(0);
+#endif
     for (uint32_t k = 0;; ++k) {
         const int buf = (int)(k & 1u);
         Meta m;
@@ -1290,7 +1595,26 @@ __device__ __forceinline__ void parser_wave(Smem &s, Ctx &c PROF_ARG) {
             if (pip < c.n - 64) {
                 use_buffer(s, c, buf);
                 uint32_t T, efin;
+#if JFS_LZ4_SEG
+                if (!spv || pip >= sp.base + SW) {
+                    // the span at pip: the walk started ahead of time, or a fresh one
+                    if (!(spv && nxt && wk.base == pip)) wk.start(pip);
+                    wk.advance(c, 1 << 20 PROF_PASS);
+                    PSTAMP(1);
+                    sp.v0 = wk.vt0;
+                    sp.v1 = wk.vt1;
+                    sp.base = pip;
+                    sp.exit = readlane(wk.ex, 63);
+                    spv = true;
+                    nxt = !(sp.exit & STOP) && !c.bug;
+                    if (nxt) wk.start((int32_t)sp.exit);  // walk the next span during this one's windows
+                }
+                parse_window_seg(s, c, pip, sp, &T, &efin PROF_PASS);
+                if (nxt) wk.advance(c, SEG_BUDGET PROF_PASS);
+                PSTAMP(1);
+#else
                 parse_window(s, c, pip, &T, &efin PROF_PASS);
+#endif
                 m.kind = c.bug ? W_BUG : W_WIN;
                 m.cbase = c.cbase;
                 m.T = T;
@@ -1312,6 +1636,10 @@ __device__ __forceinline__ void parser_wave(Smem &s, Ctx &c PROF_ARG) {
         if (restart) {
             pip = rip;
             pstop = false;
+#if JFS_LZ4_SEG
+            spv = false;
+            nxt = false;
+#endif
         }
     }
 }
