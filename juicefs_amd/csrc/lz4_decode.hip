@@ -1233,7 +1233,7 @@ constexpr int SW = 64 * SEG;
 #endif
 constexpr int SPRE = JFS_LZ4_SPRE;
 #ifndef JFS_LZ4_SEG_BUDGET
-#define JFS_LZ4_SEG_BUDGET 12  // walk steps of the next span per window
+#define JFS_LZ4_SEG_BUDGET 16  // walk steps of the next span per window
 #endif
 constexpr int SEG_BUDGET = JFS_LZ4_SEG_BUDGET;
 
@@ -1274,20 +1274,22 @@ __device__ __noinline__ uint32_t g_next_exact(const Ctx &c, int32_t p) {
 // extension byte is taken here; tokens with a 255 extension byte (runs of
 // >= 270 literals or >= 274-byte matches) take g_next_exact.
 __device__ __forceinline__ uint32_t g_step(const Ctx &c, int32_t p, bool act) {
+    // unsigned 32-bit offsets from the uniform base: saddr loads, no 64-bit
+    // address arithmetic; bitwise 0/1 logic: no exec-mask branches
     const int32_t n = c.n;
-    const bool edge = p > n - 18;
-    const int32_t pa = edge ? 0 : p;
-    const uint32_t tb = c.src[pa], e1 = c.src[edge ? 0 : p + 1];
-    const uint32_t llx = (tb >> 4) == 15u ? 1u : 0u;
-    const uint32_t L = llx ? 15u + e1 : (tb >> 4);
-    // parse_tok's end-of-input rules for the literal-length extension
-    const bool lstop = llx && (p + 2 >= n - 15 || p + 2 + (int32_t)L > n - 32);
-    const int32_t q = p + 3 + (int32_t)llx + (int32_t)L;  // first match-length extension byte
-    const uint32_t e2 = c.src[edge || lstop ? 0 : q];
-    const uint32_t mlx = (tb & 15u) == 15u ? 1u : 0u;
-    uint32_t x = (uint32_t)q + mlx;
-    const bool slow = act && !edge && !lstop && ((llx & (e1 == 255u)) | (mlx & (e2 == 255u)));
-    if (edge || lstop || (mlx && (int32_t)x >= n - 4)) x = STOP | (uint32_t)p;
+    const uint32_t edge = (uint32_t)(p > n - 18);
+    const uint32_t up = (uint32_t)p;
+    const uint32_t tb = c.src[edge ? 0u : up], e1 = c.src[edge ? 0u : up + 1u];
+    const uint32_t hi = tb >> 4;
+    const uint32_t llx = (uint32_t)(hi == 15u);
+    const uint32_t L = llx ? 15u + e1 : hi;
+    const uint32_t lstop = llx & ((uint32_t)(p + 2 >= n - 15) | (uint32_t)(p + 2 + (int32_t)L > n - 32));
+    const uint32_t q = up + 3u + llx + L;  // first match-length extension byte
+    const uint32_t e2 = c.src[(edge | lstop) ? 0u : q];
+    const uint32_t mlx = (uint32_t)((tb & 15u) == 15u);
+    uint32_t x = q + mlx;
+    const uint32_t slow = (uint32_t)act & (edge ^ 1u) & (lstop ^ 1u) & ((llx & (uint32_t)(e1 == 255u)) | (mlx & (uint32_t)(e2 == 255u)));
+    x = (edge | lstop | (mlx & (uint32_t)((int32_t)x >= n - 4))) ? (STOP | up) : x;
     if (__ballot(slow)) {
         if (slow) x = g_next_exact(c, p);
     }
