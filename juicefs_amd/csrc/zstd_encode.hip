@@ -63,17 +63,37 @@ __constant__ int16_t ML_DEF[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 
 __constant__ int16_t OF_DEF[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1,
                                    1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
 
-// FSE compression table (FSE_buildCTable semantics) of one code type
-struct CTab {
-    uint16_t st[512];  // state table: tableSize + spread position, by cumulative symbol rank
+// FSE compression table (FSE_buildCTable semantics) of one code type; N =
+// state-table capacity (512 for a block's own tables, 64 for the predefined
+// and Huffman-weight tables, table log <= 6)
+template <int N>
+struct CTabN {
+    uint16_t st[N];    // state table: tableSize + spread position, by cumulative symbol rank
     int32_t dnb[53];   // deltaNbBits
-    int32_t dfs[53];   // deltaFindState
+    int16_t dfs[53];   // deltaFindState (|.| <= 512)
 };
+typedef CTabN<512> CTab;
+typedef CTabN<64> CTab64;
+// read view of either size
+struct CView {
+    const uint16_t *st;
+    const int32_t *dnb;
+    const int16_t *dfs;
+};
+template <int N>
+__device__ __forceinline__ CView cview(const CTabN<N> &t) { return CView{t.st, t.dnb, t.dfs}; }
 
 // Huffman literal coding state of the current block (lane 0 builds, lanes 0-3 encode)
 struct HufSmem {
     uint32_t cnt[256];
-    uint32_t w[512];    // tree node weights (leaves 0..n-1, sorted by count)
+    union {
+        uint32_t w[512];  // tree node weights (leaves 0..n-1, sorted by count; huf_build)
+        struct {          // the tree description's FSE table (huf_describe)
+            CTab64 wct;   // Huffman weights (log 6)
+            uint8_t tsym[512];
+            int32_t cumul[64];
+        } d;
+    };
     uint16_t par[512];
     uint8_t dep[512];
     uint16_t sym[256];  // leaf -> symbol
@@ -86,20 +106,28 @@ struct HufSmem {
     int32_t ssz[4];     // stream sizes
 };
 
-struct Smem {
-    uint32_t table[1 << HBITS];
-    CTab ct[3];  // 0 LL (log 6), 1 ML (log 6), 2 OF (log 5)
-    CTab wct;    // Huffman weights (log 6)
-    CTab act[3]; // FSE_Compressed tables of the current block (LL, ML, OF)
-    uint8_t lut_ll[64], lut_ml[128];
-    uint8_t tsym[512];
-    int32_t cumul[64];
-    uint32_t scnt[3][64];  // code histograms of the current block's sequences
+// Sequence-table state of the current block (after its literals are written)
+struct SeqSmem {
+    CTab act[3];           // FSE_Compressed tables (LL, ML, OF)
+    uint32_t scnt[3][64];  // code histograms of the block's sequences
     int16_t snorm[3][64];
     uint8_t shdr[3][96];   // their normalized-count headers
-    int32_t shsz[3], smode[3], slog[3];
-    HufSmem h;
+    uint8_t tsym[512];     // build_ctab scratch
+    int32_t cumul[64];
 };
+
+// <= 40 KiB: four inputs (waves) per CU
+struct Smem {
+    uint32_t table[1 << HBITS];
+    CTab64 ct[3];  // 0 LL (log 6), 1 ML (log 6), 2 OF (log 5)
+    uint8_t lut_ll[64], lut_ml[128];
+    int32_t shsz[3], smode[3], slog[3];
+    union {  // a block's literal coding, then its sequence tables
+        HufSmem h;
+        SeqSmem q;
+    };
+};
+static_assert(sizeof(Smem) <= 40960, "four encoder waves per CU");
 
 __device__ __forceinline__ uint32_t highbit(uint32_t v) { return 31u - (uint32_t)__builtin_clz(v); }
 
@@ -107,29 +135,30 @@ __device__ __forceinline__ uint32_t highbit(uint32_t v) { return 31u - (uint32_t
 // Spread and state numbering are the decoder's (FSE_buildDTable): -1
 // ("less than 1") symbols at the top, the others spread with step
 // (size>>1)+(size>>3)+3 skipping the top; state table in symbol order.
-__device__ void build_ctab(Smem &s, CTab &t, const int16_t *norm, int maxsv, int tlog) {
+template <int N>
+__device__ void build_ctab(uint8_t *tsym, int32_t *cumul, CTabN<N> &t, const int16_t *norm, int maxsv, int tlog) {
     if (lane_id() == 0) {
         const int size = 1 << tlog, mask = size - 1, step = (size >> 1) + (size >> 3) + 3;
         int high = size - 1;
-        s.cumul[0] = 0;
+        cumul[0] = 0;
         for (int u = 1; u <= maxsv + 1; u++) {
             if (norm[u - 1] == -1) {
-                s.cumul[u] = s.cumul[u - 1] + 1;
-                s.tsym[high--] = (uint8_t)(u - 1);
+                cumul[u] = cumul[u - 1] + 1;
+                tsym[high--] = (uint8_t)(u - 1);
             } else {
-                s.cumul[u] = s.cumul[u - 1] + norm[u - 1];
+                cumul[u] = cumul[u - 1] + norm[u - 1];
             }
         }
         int pos = 0;
         for (int sym = 0; sym <= maxsv; sym++) {
             for (int k = 0; k < norm[sym]; k++) {
-                s.tsym[pos] = (uint8_t)sym;
+                tsym[pos] = (uint8_t)sym;
                 do { pos = (pos + step) & mask; } while (pos > high);
             }
         }
         for (int u = 0; u < size; u++) {
-            const int sym = s.tsym[u];
-            t.st[s.cumul[sym]++] = (uint16_t)(size + u);
+            const int sym = tsym[u];
+            t.st[cumul[sym]++] = (uint16_t)(size + u);
         }
         int total = 0;
         for (int sym = 0; sym <= maxsv; sym++) {
@@ -214,13 +243,13 @@ __device__ __forceinline__ void bw_flush(BitW &w) {
     w.bp &= 7;
 }
 
-__device__ __forceinline__ uint32_t fse_init(const CTab &t, uint32_t sym) {
+__device__ __forceinline__ uint32_t fse_init(const CView &t, uint32_t sym) {
     const int32_t dnb = t.dnb[sym];
     const uint32_t nbo = (uint32_t)((dnb + (1 << 15)) >> 16);
     const uint32_t v = (nbo << 16) - (uint32_t)dnb;
     return t.st[(v >> nbo) + (uint32_t)t.dfs[sym]];
 }
-__device__ __forceinline__ void fse_enc(BitW &w, const CTab &t, uint32_t &st, uint32_t sym) {
+__device__ __forceinline__ void fse_enc(BitW &w, const CView &t, uint32_t &st, uint32_t sym) {
     const uint32_t nbo = (uint32_t)(((int32_t)st + t.dnb[sym]) >> 16);
     bw_add(w, st, (int)nbo);
     st = t.st[(st >> nbo) + (uint32_t)t.dfs[sym]];
@@ -247,9 +276,9 @@ __device__ __forceinline__ void seq_fields(const uint64_t *seq, int64_t i, uint3
 // order: last sequence first, states OF/ML/LL, extra bits LL/ML/OF).
 __device__ void encode_sequences(const Smem &s, BitW &w, const uint64_t *seq, int64_t ns) {
     // per table: the block's FSE_Compressed table (mode 2) or the predefined one
-    const CTab &TL = s.smode[0] == 2 ? s.act[0] : s.ct[0];
-    const CTab &TM = s.smode[1] == 2 ? s.act[1] : s.ct[1];
-    const CTab &TO = s.smode[2] == 2 ? s.act[2] : s.ct[2];
+    const CView TL = s.smode[0] == 2 ? cview(s.q.act[0]) : cview(s.ct[0]);
+    const CView TM = s.smode[1] == 2 ? cview(s.q.act[1]) : cview(s.ct[1]);
+    const CView TO = s.smode[2] == 2 ? cview(s.q.act[2]) : cview(s.ct[2]);
     uint32_t ll, ml, off;
     seq_fields(seq, ns - 1, ll, ml, off);
     uint32_t lc = ll_code(s, ll), mc = ml_code(s, ml - 3), ofv = off, oc = highbit(ofv);
@@ -378,7 +407,7 @@ __device__ __forceinline__ void lb_flush(LBits &b) {
         b.bp -= 8;
     }
 }
-__device__ __forceinline__ void lb_enc(LBits &b, const CTab &t, uint32_t &st, uint32_t sym) {
+__device__ __forceinline__ void lb_enc(LBits &b, const CView &t, uint32_t &st, uint32_t sym) {
     const uint32_t nbo = (uint32_t)(((int32_t)st + t.dnb[sym]) >> 16);
     lb_add(b, st, (int)nbo);
     st = t.st[(st >> nbo) + (uint32_t)t.dfs[sym]];
@@ -471,7 +500,7 @@ __device__ int huf_build(HufSmem &h) {
 
 // Tree description into h.hdr: FSE-compressed weights (2 states, table log
 // 6) when that is smaller, else direct 4-bit weights (<= 128 transmitted).
-// Returns its size, or -1 when neither applies.  Lane 0 (uses s.tsym/cumul).
+// Returns its size, or -1 when neither applies.  Lane 0 (h.d: table + scratch).
 __device__ int huf_describe(Smem &s) {
     HufSmem &h = s.h;
     const int nw = h.maxsym;  // weights of symbols 0..maxsym-1 (the last one is implied)
@@ -493,7 +522,7 @@ __device__ int huf_describe(Smem &s) {
         h.norm[big] = (int16_t)(h.norm[big] + (tsize - sum));
         if (h.norm[big] >= 1) {
             int o = 1 + write_ncount(h.hdr + 1, h.norm, maxsv, tlog);
-            build_ctab(s, s.wct, h.norm, maxsv, tlog);
+            build_ctab(h.d.tsym, h.d.cumul, h.d.wct, h.norm, maxsv, tlog);
             LBits b;
             b.out = h.hdr;
             b.o = o;
@@ -504,24 +533,24 @@ __device__ int huf_describe(Smem &s) {
             int ip = nw;
             uint32_t s1, s2;
             if (nw & 1) {
-                s1 = fse_init(s.wct, h.wt[--ip]);
-                s2 = fse_init(s.wct, h.wt[--ip]);
-                lb_enc(b, s.wct, s1, h.wt[--ip]);
+                s1 = fse_init(cview(h.d.wct), h.wt[--ip]);
+                s2 = fse_init(cview(h.d.wct), h.wt[--ip]);
+                lb_enc(b, cview(h.d.wct), s1, h.wt[--ip]);
                 lb_flush(b);
             } else {
-                s2 = fse_init(s.wct, h.wt[--ip]);
-                s1 = fse_init(s.wct, h.wt[--ip]);
+                s2 = fse_init(cview(h.d.wct), h.wt[--ip]);
+                s1 = fse_init(cview(h.d.wct), h.wt[--ip]);
             }
             if ((nw - 2) & 2) {
-                lb_enc(b, s.wct, s2, h.wt[--ip]);
-                lb_enc(b, s.wct, s1, h.wt[--ip]);
+                lb_enc(b, cview(h.d.wct), s2, h.wt[--ip]);
+                lb_enc(b, cview(h.d.wct), s1, h.wt[--ip]);
                 lb_flush(b);
             }
             while (ip > 0) {
-                lb_enc(b, s.wct, s2, h.wt[--ip]);
-                lb_enc(b, s.wct, s1, h.wt[--ip]);
-                lb_enc(b, s.wct, s2, h.wt[--ip]);
-                lb_enc(b, s.wct, s1, h.wt[--ip]);
+                lb_enc(b, cview(h.d.wct), s2, h.wt[--ip]);
+                lb_enc(b, cview(h.d.wct), s1, h.wt[--ip]);
+                lb_enc(b, cview(h.d.wct), s2, h.wt[--ip]);
+                lb_enc(b, cview(h.d.wct), s1, h.wt[--ip]);
                 lb_flush(b);
             }
             lb_add(b, s2, tlog);
@@ -593,14 +622,14 @@ __device__ int64_t huf_streams(Smem &s, const gc_u8 *lit, int64_t L, g_u8 *scr) 
 // builds the tables.  Sets s.smode / s.slog / s.shdr / s.shsz.
 __device__ void choose_seq_tables(Smem &s, const uint64_t *seq, int64_t ns) {
     const int l = lane_id();
-    for (int k = l; k < 3 * 64; k += 64) (&s.scnt[0][0])[k] = 0;
+    for (int k = l; k < 3 * 64; k += 64) (&s.q.scnt[0][0])[k] = 0;
     __syncthreads();
     for (int64_t i = l; i < ns; i += 64) {
         uint32_t ll, ml, off;
         seq_fields(seq, i, ll, ml, off);
-        atomicAdd(&s.scnt[0][ll_code(s, ll)], 1u);
-        atomicAdd(&s.scnt[1][ml_code(s, ml - 3)], 1u);
-        atomicAdd(&s.scnt[2][highbit(off)], 1u);
+        atomicAdd(&s.q.scnt[0][ll_code(s, ll)], 1u);
+        atomicAdd(&s.q.scnt[1][ml_code(s, ml - 3)], 1u);
+        atomicAdd(&s.q.scnt[2][highbit(off)], 1u);
     }
     __syncthreads();
     if (l == 0) {
@@ -610,7 +639,7 @@ __device__ void choose_seq_tables(Smem &s, const uint64_t *seq, int64_t ns) {
             s.smode[t] = 0;
             s.slog[t] = prelog[t];
             s.shsz[t] = 0;
-            const uint32_t *cnt = s.scnt[t];
+            const uint32_t *cnt = s.q.scnt[t];
             int maxsv = 0, distinct = 0;
             for (int v = 0; v < nsym[t]; v++)
                 if (cnt[v]) { maxsv = v; distinct++; }
@@ -628,7 +657,7 @@ __device__ void choose_seq_tables(Smem &s, const uint64_t *seq, int64_t ns) {
             tlog = tlog < 5 ? 5 : tlog > maxlog[t] ? maxlog[t] : tlog;
             while ((1 << tlog) < 2 * distinct && tlog < maxlog[t]) tlog++;
             const int tsize = 1 << tlog;
-            int16_t *norm = s.snorm[t];
+            int16_t *norm = s.q.snorm[t];
             int sum = 0, big = 0;
             for (int v = 0; v <= maxsv; v++) {
                 int nv = 0;
@@ -645,10 +674,10 @@ __device__ void choose_seq_tables(Smem &s, const uint64_t *seq, int64_t ns) {
             float cc = 0.f;
             for (int v = 0; v <= maxsv; v++)
                 if (cnt[v]) cc += (float)cnt[v] * ((float)tlog - __log2f((float)norm[v]));
-            const int hs = write_ncount(s.shdr[t], norm, maxsv, tlog);
+            const int hs = write_ncount(s.q.shdr[t], norm, maxsv, tlog);
             cc += 8.f * (float)hs;
             if (pre_ok && pc <= cc) continue;
-            build_ctab(s, s.act[t], norm, maxsv, tlog);
+            build_ctab(s.q.tsym, s.q.cumul, s.q.act[t], norm, maxsv, tlog);
             s.smode[t] = 2;
             s.slog[t] = tlog;
             s.shsz[t] = hs;
@@ -702,11 +731,11 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(const jfs_dev_block *__
         s.slog[t] = t == 2 ? 5 : 6;
         s.shsz[t] = 0;
     }
-    build_ctab(s, s.ct[0], LL_DEF, 35, 6);
+    build_ctab(s.q.tsym, s.q.cumul, s.ct[0], LL_DEF, 35, 6);
     __builtin_amdgcn_wave_barrier();
-    build_ctab(s, s.ct[1], ML_DEF, 52, 6);
+    build_ctab(s.q.tsym, s.q.cumul, s.ct[1], ML_DEF, 52, 6);
     __builtin_amdgcn_wave_barrier();
-    build_ctab(s, s.ct[2], OF_DEF, 28, 5);
+    build_ctab(s.q.tsym, s.q.cumul, s.ct[2], OF_DEF, 28, 5);
     __syncthreads();
 
     // ---- frame header: magic, FHD, [Window_Descriptor], Frame_Content_Size
@@ -1010,7 +1039,7 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(const jfs_dev_block *__
                 if (l == 0) dst[end] = (uint8_t)((s.smode[0] << 6) | (s.smode[2] << 4) | (s.smode[1] << 2));
                 end += 1;
                 for (int t : {0, 2, 1}) {
-                    for (int k = l; k < s.shsz[t]; k += 64) dst[end + k] = s.shdr[t][k];
+                    for (int k = l; k < s.shsz[t]; k += 64) dst[end + k] = s.q.shdr[t][k];
                     end += s.shsz[t];
                 }
                 __threadfence_block();
