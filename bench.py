@@ -19,7 +19,7 @@ output is checked against the original on the device after timing.
 
 Sub-records of the same JSON line (each names its BASELINE config):
   configs_3        Zstd level-3 decode, 4096 x 4 MiB frames in HBM, every rank
-  configs_2        LZ4 compress + decompress, 512 blocks per GPU, block i on
+  configs_2        LZ4 compress + decompress, 2048 blocks per GPU, block i on
                    rank i % N (round robin), every block verified, every rank
   configs_0        LZ4 round trip of 1024 x 4 MiB host blocks through the C ABI
                    batch entry points (rank 0, N = 1)
@@ -82,7 +82,7 @@ def parse():
     p.add_argument("--no-mixed", action="store_true", help="skip configs[4] (mixed LZ4/Zstd 64 KiB-4 MiB, host path)")
     p.add_argument("--mixed-blocks", type=int, default=4096)
     p.add_argument("--c0-blocks", type=int, default=1024, help="configs[0] blocks (host round trip)")
-    p.add_argument("--c2-blocks", type=int, default=512, help="configs[2] blocks per GPU")
+    p.add_argument("--c2-blocks", type=int, default=2048, help="configs[2] blocks per GPU (one full LZ4 encoder round: 8 blocks per CU)")
     p.add_argument("--zstd-steps", type=int, default=3, help="timed launches of the configs[3] sub-record")
     p.add_argument("--extra-blocks", type=int, default=1024, help="blocks in the Zstd compress sample")
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="wall budget per CPU baseline leg")

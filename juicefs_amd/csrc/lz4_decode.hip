@@ -52,6 +52,9 @@ constexpr int RMASK = R - 1;
 #ifndef JFS_LZ4_DP
 #define JFS_LZ4_DP 1  // exit-table parser for windows away from the input end
 #endif
+#ifndef JFS_LZ4_LITSRC
+#define JFS_LZ4_LITSRC 1  // near matches whose source lies in one literal run of the batch join the parallel round
+#endif
 #ifndef JFS_LZ4_SEG
 #define JFS_LZ4_SEG 128  // segment-walk parser (bytes per lane); 0 = per-window exit-table parser
 #endif
@@ -775,6 +778,7 @@ __device__ __forceinline__ void batch(Smem &s, Ctx &c, bool act, int32_t o, uint
     const uint64_t am = __ballot(act);
     const int first = am ? (int)__builtin_ctzll(am) : 0;
     const uint32_t key = act ? (uint32_t)ms : (lane_id() < first ? 0u : 0xFFFFFFFFu);  // non-decreasing
+    bool litsrc = false;  // the source lies wholly inside one literal run of this batch (written above)
     {
         const uint32_t mek = pend ? (uint32_t)(ms + (int32_t)ml) : 0u;
         bool cand = pend && off >= ml;
@@ -795,6 +799,15 @@ __device__ __forceinline__ void batch(Smem &s, Ctx &c, bool act, int32_t o, uint
             const int32_t voff = __shfl((int)off, lo, 64);
             const bool ok = want && vms <= (uint32_t)src && (uint32_t)(src + (int32_t)ml) <= vme && voff > 0 &&
                             src - voff >= hz;
+#if JFS_LZ4_LITSRC
+            // past the end of lane lo's match and before the next lane's match
+            // start: inside the next token's literal run, already in the ring
+            if (it == 0) {
+                const uint32_t nms = (uint32_t)__shfl((int)key, lo + 1 < 64 ? lo + 1 : 63, 64);
+                litsrc = want && vms <= (uint32_t)src && (uint32_t)src >= vme && lo < 63 &&
+                         (uint32_t)(src + (int32_t)ml) <= nms;
+            }
+#endif
             src = ok ? src - voff : src;
             cand = ok;
         }
@@ -822,7 +835,7 @@ __device__ __forceinline__ void batch(Smem &s, Ctx &c, bool act, int32_t o, uint
     {
         PCOUNT(18, 1);
 #if JFS_LZ4_NEARPM == 2
-        const bool go = pend && send <= O0;  // source wholly before the batch
+        const bool go = pend && (send <= O0 || litsrc);  // source wholly before the batch, or in its literals
 #elif JFS_LZ4_NEARPM
         const uint32_t pm = dpp_scan_max(pend ? (uint32_t)(ms + (int32_t)ml) : 0u);
         const uint32_t pmj = (uint32_t)__shfl((int)pm, jl, 64);
