@@ -132,6 +132,7 @@ struct Meta {
 // Published by the copier wave after each pipeline step.
 struct Ctl {
     int32_t done, restart, rip;
+    int32_t step;  // the copier's pipeline step, written as it reaches the step's first barrier
 };
 
 struct Smem {
@@ -1246,8 +1247,12 @@ constexpr int SW = 64 * SEG;
 #endif
 constexpr int SPRE = JFS_LZ4_SPRE;
 #ifndef JFS_LZ4_SEG_BUDGET
-#define JFS_LZ4_SEG_BUDGET 16  // walk steps of the next span per window
+#define JFS_LZ4_SEG_BUDGET 64  // at most this many walk steps of the next span per window
 #endif
+#ifndef JFS_LZ4_SEG_MIN
+#define JFS_LZ4_SEG_MIN 4  // at least this many (more while the copier is busy)
+#endif
+constexpr int SEG_MIN = JFS_LZ4_SEG_MIN;
 constexpr int SEG_BUDGET = JFS_LZ4_SEG_BUDGET;
 
 // Next token position after p (or STOP | p): the exact chain rule of
@@ -1625,7 +1630,16 @@ __device__ __forceinline__ void parser_wave(Smem &s, Ctx &c PROF_ARG) {
                     if (nxt) wk.start((int32_t)sp.exit);  // walk the next span during this one's windows
                 }
                 parse_window_seg(s, c, pip, sp, &T, &efin PROF_PASS);
-                if (nxt) wk.advance(c, SEG_BUDGET PROF_PASS);
+                if (nxt) {
+                    // walk the next span while the copier is still busy with its
+                    // window (at least SEG_MIN steps per window)
+                    bool fin = wk.advance(c, SEG_MIN PROF_PASS);
+                    for (int g = SEG_MIN; !fin && g < SEG_BUDGET; g += 2) {
+                        if (__hip_atomic_load(&s.ctl.step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= (int32_t)k)
+                            break;
+                        fin = wk.advance(c, 2 PROF_PASS);
+                    }
+                }
                 PSTAMP(1);
 #else
                 parse_window(s, c, pip, &T, &efin PROF_PASS);
@@ -1668,6 +1682,7 @@ __device__ __forceinline__ void copier_wave(Smem &s, Ctx &c, int32_t *retp PROF_
     bool skip = false;
     int32_t result = INT32_MIN;
     int64_t nser = 0;
+    if (lane_id() == 0) __hip_atomic_store(&s.ctl.step, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     for (uint32_t k = 0;; ++k) {
         int32_t done = 0, restart = 0, rip = 0;
         if (k > 0 && !skip) {
@@ -1715,7 +1730,7 @@ __device__ __forceinline__ void copier_wave(Smem &s, Ctx &c, int32_t *retp PROF_
                         break;
                     }
                 }
-                PSTAMP(8);
+                PSTAMP(7);
             }
             if (c.bug) {
                 done = 1;
@@ -1731,10 +1746,11 @@ __device__ __forceinline__ void copier_wave(Smem &s, Ctx &c, int32_t *retp PROF_
             s.ctl.done = done;
             s.ctl.restart = restart;
             s.ctl.rip = rip;
+            __hip_atomic_store(&s.ctl.step, (int32_t)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         wg_sync();
         wg_sync();
-        PSTAMP(9);
+        PSTAMP(8);
         if (done) break;
         skip = restart != 0;
     }

@@ -45,6 +45,23 @@ constexpr int HUF_MINL = 64;                // fewer literals stay raw
 #endif
 constexpr int32_t HBITS = JFS_ZE_HBITS;     // hash table: 2^HBITS positions in LDS
 
+#ifdef JFS_PROF
+// diagnostic build only: per-phase s_memtime sums of the encoder waves
+// (0 parse, 1 literal histogram + Huffman build, 2 Huffman streams, 3 literal
+// section writes, 4 sequence tables, 5 sequence bitstream, 6 block header /
+// raw fallback; 8 blocks, 9 sequences)
+__device__ unsigned long long g_zeprof[12];
+#define ZE_DECL uint64_t ze_t = __builtin_amdgcn_s_memtime(), ze_acc[12] = {0};
+#define ZE(k) do { const uint64_t x_ = __builtin_amdgcn_s_memtime(); ze_acc[k] += x_ - ze_t; ze_t = x_; } while (0)
+#define ZEC(k, n) (ze_acc[k] += (n))
+#define ZE_FLUSH() do { if (lane_id() == 0) for (int i_ = 0; i_ < 12; ++i_) atomicAdd(&g_zeprof[i_], (unsigned long long)ze_acc[i_]); } while (0)
+#else
+#define ZE_DECL
+#define ZE(k) do { } while (0)
+#define ZEC(k, n) do { } while (0)
+#define ZE_FLUSH() do { } while (0)
+#endif
+
 // RFC 8878 3.1.1.3.2.1 code tables and 3.1.1.3.2.2 predefined distributions
 __constant__ uint32_t LL_BASE[36] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,   10,  11,  12,   13,   14,   15,    16,    18,
                                      20, 22, 24, 28, 32, 40, 48, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536};
@@ -274,35 +291,64 @@ __device__ __forceinline__ void seq_fields(const uint64_t *seq, int64_t i, uint3
 // Encode sequences [0, ns) (scratch records: ll | ml << 17 | Offset_Value << 35 as
 // u64) as the predefined-mode FSE bitstream at w.wp (ZSTD_encodeSequences
 // order: last sequence first, states OF/ML/LL, extra bits LL/ML/OF).
+// Per 64 sequences the lanes load the records and look up, in parallel,
+// everything that does not depend on the FSE states (codes, extra-bit fields,
+// each symbol's deltaNbBits / deltaFindState); the serial loop then only
+// steps the three states (one LDS round trip per sequence) and packs bits.
 __device__ void encode_sequences(const Smem &s, BitW &w, const uint64_t *seq, int64_t ns) {
     // per table: the block's FSE_Compressed table (mode 2) or the predefined one
     const CView TL = s.smode[0] == 2 ? cview(s.q.act[0]) : cview(s.ct[0]);
     const CView TM = s.smode[1] == 2 ? cview(s.q.act[1]) : cview(s.ct[1]);
     const CView TO = s.smode[2] == 2 ? cview(s.q.act[2]) : cview(s.ct[2]);
-    uint32_t ll, ml, off;
-    seq_fields(seq, ns - 1, ll, ml, off);
-    uint32_t lc = ll_code(s, ll), mc = ml_code(s, ml - 3), ofv = off, oc = highbit(ofv);
-    uint32_t sML = fse_init(TM, mc), sOF = fse_init(TO, oc), sLL = fse_init(TL, lc);
-    bw_add(w, ll - LL_BASE[lc], LL_BITS[lc]);
-    bw_add(w, ml - ML_BASE[mc], ML_BITS[mc]);
-    bw_flush(w);
-    bw_add(w, ofv - (1u << oc), (int)oc);
-    bw_flush(w);
-    for (int64_t i = ns - 2; i >= 0; --i) {
-        seq_fields(seq, i, ll, ml, off);
-        lc = ll_code(s, ll);
-        mc = ml_code(s, ml - 3);
-        ofv = off;
-        oc = highbit(ofv);
-        fse_enc(w, TO, sOF, oc);
-        fse_enc(w, TM, sML, mc);
-        fse_enc(w, TL, sLL, lc);
-        bw_flush(w);
-        bw_add(w, ll - LL_BASE[lc], LL_BITS[lc]);
-        bw_add(w, ml - ML_BASE[mc], ML_BITS[mc]);
-        bw_flush(w);
-        bw_add(w, ofv - (1u << oc), (int)oc);
-        bw_flush(w);
+    const int l = lane_id();
+    uint32_t sML = 0, sOF = 0, sLL = 0;
+    for (int64_t c0 = ns - 1; c0 >= 0; c0 -= 64) {
+        const int64_t i = c0 - l;
+        uint32_t ll = 0, ml = 3, ofv = 1;
+        if (i >= 0) seq_fields(seq, i, ll, ml, ofv);
+        const uint32_t lc = ll_code(s, ll), mc = ml_code(s, ml - 3), oc = highbit(ofv);
+        const int32_t dO = TO.dnb[oc], dM = TM.dnb[mc], dL = TL.dnb[lc];
+        const uint32_t fOM = ((uint32_t)(uint16_t)TO.dfs[oc]) | ((uint32_t)(uint16_t)TM.dfs[mc] << 16);
+        const int32_t fL = TL.dfs[lc];
+        const uint32_t eLL = ll - LL_BASE[lc], eML = ml - ML_BASE[mc], eOF = ofv - (1u << oc);
+        const uint32_t nb = (uint32_t)LL_BITS[lc] | ((uint32_t)ML_BITS[mc] << 8) | (oc << 16);
+        const int nj = c0 + 1 < 64 ? (int)(c0 + 1) : 64;
+        for (int j = 0; j < nj; ++j) {
+            const int32_t jdO = (int32_t)readlane((uint32_t)dO, j), jdM = (int32_t)readlane((uint32_t)dM, j),
+                          jdL = (int32_t)readlane((uint32_t)dL, j);
+            const uint32_t jf = readlane(fOM, j);
+            const int32_t jfO = (int16_t)(jf & 0xFFFFu), jfM = (int16_t)(jf >> 16), jfL = (int32_t)readlane((uint32_t)fL, j);
+            const uint32_t jnb = readlane(nb, j);
+            const uint32_t jeLL = readlane(eLL, j), jeML = readlane(eML, j), jeOF = readlane(eOF, j);
+            if (c0 == ns - 1 && j == 0) {
+                // FSE_initCState2: the last sequence only sets the states
+                const uint32_t nM = (uint32_t)((jdM + (1 << 15)) >> 16), nO = (uint32_t)((jdO + (1 << 15)) >> 16),
+                               nL = (uint32_t)((jdL + (1 << 15)) >> 16);
+                const uint32_t vM = ((nM << 16) - (uint32_t)jdM) >> nM, vO = ((nO << 16) - (uint32_t)jdO) >> nO,
+                               vL = ((nL << 16) - (uint32_t)jdL) >> nL;
+                sML = TM.st[vM + (uint32_t)jfM];
+                sOF = TO.st[vO + (uint32_t)jfO];
+                sLL = TL.st[vL + (uint32_t)jfL];
+            } else {
+                const uint32_t nO = (uint32_t)(((int32_t)sOF + jdO) >> 16), nM = (uint32_t)(((int32_t)sML + jdM) >> 16),
+                               nL = (uint32_t)(((int32_t)sLL + jdL) >> 16);
+                bw_add(w, sOF, (int)nO);
+                bw_add(w, sML, (int)nM);
+                bw_add(w, sLL, (int)nL);
+                // the three table reads are independent: one LDS round trip
+                const uint32_t tO = TO.st[(sOF >> nO) + (uint32_t)jfO], tM = TM.st[(sML >> nM) + (uint32_t)jfM],
+                               tL = TL.st[(sLL >> nL) + (uint32_t)jfL];
+                sOF = tO;
+                sML = tM;
+                sLL = tL;
+                bw_flush(w);
+            }
+            bw_add(w, jeLL, (int)(jnb & 0xFFu));
+            bw_add(w, jeML, (int)((jnb >> 8) & 0xFFu));
+            bw_flush(w);
+            bw_add(w, jeOF, (int)(jnb >> 16));
+            bw_flush(w);
+        }
     }
     fse_fin(w, sML, s.slog[1]);
     fse_fin(w, sOF, s.slog[2]);
@@ -764,6 +810,7 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(const jfs_dev_block *__
         op = hn;
     }
 
+    ZE_DECL
     // ---- blocks (the repeat offsets carry across the frame's blocks, RFC 8878 3.1.1.5)
     uint32_t rep0 = 1;  // Repeated_Offset1 (only it is reused: Offset_Value 1 with LL > 0)
     int64_t bs = 0;
@@ -941,6 +988,9 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(const jfs_dev_block *__
             }
         }
         __threadfence_block();
+        ZE(0);
+        ZEC(8, 1);
+        ZEC(9, ns);
         // 2./3. headers and the sequences bitstream
         int64_t end = lit0 + L;
         if (ok) {
@@ -960,6 +1010,7 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(const jfs_dev_block *__
                     s.h.hsize = s.h.maxbits > 0 ? huf_describe(s) : -1;
                 }
                 __syncthreads();
+                ZE(1);
                 if (s.h.nsym == 1) {
                     kind = 1;
                 } else if (s.h.maxbits > 0 && s.h.hsize > 0) {
@@ -971,6 +1022,7 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(const jfs_dev_block *__
                 }
                 wait_vm();
                 __syncthreads();
+                ZE(2);
             }
             if (kind == 2) {
                 const uint64_t sf = hlh == 3 ? 1 : hlh == 4 ? 2 : 3;
@@ -1032,8 +1084,10 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(const jfs_dev_block *__
                 if (l == 2) dst[end + 2] = (uint8_t)(r >> 8);
                 end += 3;
             }
+            ZE(3);
             if (ns > 0) {
                 choose_seq_tables(s, seq, ns);
+                ZE(4);
                 // Symbol_Compression_Modes: LL bits 7-6, OF 5-4, ML 3-2; then the
                 // table descriptions in the order LL, OF, ML
                 if (l == 0) dst[end] = (uint8_t)((s.smode[0] << 6) | (s.smode[2] << 4) | (s.smode[1] << 2));
@@ -1053,6 +1107,7 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(const jfs_dev_block *__
                 encode_sequences(s, w, seq, ns);
                 end = w.wp;
                 if (w.ovf) ok = false;
+                ZE(5);
             }
         }
         const int64_t csize = end - (op + 3);
@@ -1066,8 +1121,10 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(const jfs_dev_block *__
             op += 3 + raw;
         }
         __threadfence_block();
+        ZE(6);
         bs = be;
     } while (bs < n);
+    ZE_FLUSH();
     if (l == 0) ret[b] = op <= cap ? (int32_t)op : -2;
 }
 
@@ -1082,6 +1139,16 @@ struct ZEScratch {
 };
 ZEScratch g_zes[16];
 }  // namespace
+
+#ifdef JFS_PROF
+extern "C" int jfs_zeprof_read(unsigned long long *out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(jfs::zstde::g_zeprof), sizeof(unsigned long long) * 12) == hipSuccess ? 0 : -1;
+}
+extern "C" int jfs_zeprof_reset() {
+    unsigned long long z[12] = {0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(jfs::zstde::g_zeprof), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" int jfs_launch_zstd_encode(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, hipStream_t stream) {
     using namespace jfs::zstde;

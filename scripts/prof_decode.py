@@ -17,7 +17,7 @@ t0 = time.perf_counter(); b.decompress(); torch.cuda.synchronize(); dt = time.pe
 assert b.verify()
 buf = (ctypes.c_uint64 * 20)()
 lib.jfs_prof_read(buf)
-names = ["stage", "walk+fixup", "table+tokparse", "batching", "lits+pref", "far", "near", "long", "serial", "tail"]
+names = ["stage", "walk+fixup", "table+tokparse", "batching", "lits+pref", "far", "near", "long+serial", "copier wait", "parser wait"]
 tot = sum(buf[:10])
 print(f"blocks={nblk} cls={cls} wall={dt*1e3:.1f} ms  GiB/s={nblk*4/1024/dt:.1f}")
 for n, v in zip(names, buf[:10]):
