@@ -319,10 +319,10 @@ def oneshot_concurrency(comp_blocks, raw_blocks, U, n_dec=200, n_enc=20, rounds=
 
     from juicefs_amd import _lib as L
 
-    def batches():  # device batches the coalescer ran so far (LZ4, both directions)
+    def batches():  # device batches the coalescer ran so far (LZ4 and Zstd, both directions)
         arr = (L.JfsOpStats * L.STATS_N)()
         L.load().jfs_stats(arr, L.STATS_N)
-        return int(arr[L.ALGO_LZ4 * 2].batches + arr[L.ALGO_LZ4 * 2 + 1].batches)
+        return int(sum(arr[a * 2 + d].batches for a in (L.ALGO_LZ4, L.ALGO_ZSTD) for d in (0, 1)))
 
     def run(n, k, fn, check):
         """n threads x k calls of fn(t, r) -> result; every result is checked
@@ -391,6 +391,28 @@ def oneshot_concurrency(comp_blocks, raw_blocks, U, n_dec=200, n_enc=20, rounds=
            "warmup_device_batches": warm,
            "path": "LZ4 one-call API (jfs_compress / jfs_decompress) from concurrent host threads, host buffers, "
                    "1 GPU; value = uncompressed GiB/s over the wall time of all calls"}
+    # the same calls with --compress zstd (ZStandard.Compress / Decompress)
+    z = C.ZStandard()
+    zb = z.CompressBound(U)
+    zdst = {(t, r): bytearray(b"\x01") * zb for t in range(n_enc) for r in range(kmax if t == 0 else rounds)}
+    zframes = []
+    for i in range(min(nc, 8)):
+        d = bytearray(zb)
+        m = z.Compress(d, raw_blocks[i])[0]
+        zframes.append(bytes(d[:m]))
+
+    def zenc(t, r):
+        return z.Compress(zdst[(t, r)], raw_blocks[(t + r) % nc])[0]
+    zechk = lambda t, r, n: n > 0 and z.Decompress(bytearray(U), bytes(zdst[(t, r)][:n]))[0] == U
+    zout = {(t, r): bytearray(b"\x01") * U for t in range(n_enc) for r in range(kmax if t == 0 else rounds)}
+
+    def zdec(t, r):
+        return z.Decompress(zout[(t, r)], zframes[(t + r) % len(zframes)])[0]
+    zdchk = lambda t, r, n: n == U and zout[(t, r)] == raw_blocks[(t + r) % len(zframes)]
+    out["zstd"] = {"compress_lone": run(1, 3, zenc, zechk), "decompress_lone": run(1, 5, zdec, zdchk),
+                   f"compress_{n_enc}_concurrent": run(n_enc, rounds, zenc, zechk),
+                   f"decompress_{n_enc}_concurrent": run(n_enc, rounds, zdec, zdchk),
+                   "path": "Zstd one-call API (compress.go ZStandard: GPU encoder, level-1 class; GPU decoder)"}
     return out
 
 

@@ -743,25 +743,62 @@ __device__ __forceinline__ void put3(g_u8 *dst, int64_t o, uint32_t v) {
     if (l < 3) dst[o + l] = (uint8_t)(v >> (8 * l));
 }
 
-__global__ __launch_bounds__(64) void zstd_encode_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
-                                                        int32_t *__restrict__ ret, uint64_t *__restrict__ scratch) {
-    __shared__ Smem s;
-    const int b = blockIdx.x;
-    if (b >= nblk) return;
+// Frame header size (magic, FHD, [Window_Descriptor], Frame_Content_Size).
+__device__ __forceinline__ int frame_header(int64_t n, bool write, g_u8 *dst) {
     const int l = lane_id();
-    const jfs_dev_block d = ((const gc_blk *)blocks)[b];
-    const gc_u8 *src = (const gc_u8 *)d.src;
-    g_u8 *dst = (g_u8 *)d.dst;
-    const int64_t n = d.src_len, cap = d.dst_cap;
-    uint64_t *seq = (uint64_t *)((uint8_t *)scratch + (int64_t)b * SCR_PER);
-    g_u8 *lscr = (g_u8 *)((uint8_t *)scratch + (int64_t)b * SCR_PER + SEQ_CAP * 8);
-    const int64_t bound = n + (n >> 8) + (n < BLK ? (BLK - n) >> 11 : 0);
-    if (n < 0 || cap < bound) {  // compress.go:86-89: cap(dst) < CompressBound -> "buffer too short"
-        if (l == 0) ret[b] = -2;
-        return;
+    const bool single = n <= (1 << 19);
+    int fcs_flag, fs;
+    if (single) {
+        if (n < 256) { fcs_flag = 0; fs = 1; }
+        else if (n < 65536 + 256) { fcs_flag = 1; fs = 2; }
+        else { fcs_flag = 2; fs = 4; }
+    } else {
+        fcs_flag = n < (1ll << 32) ? 2 : 3;
+        fs = fcs_flag == 2 ? 4 : 8;
     }
+    const uint32_t fhd = (uint32_t)((fcs_flag << 6) | (single ? 0x20 : 0));
+    const int fpos = single ? 5 : 6;  // FCS position
+    const uint64_t fv = (uint64_t)n - (fs == 2 ? 256 : 0);
+    const int hn = fpos + fs;
+    uint32_t byte = 0;
+    if (l < 4) byte = (0xFD2FB528u >> (8 * l)) & 0xFFu;
+    else if (l == 4) byte = fhd;
+    else if (l == 5 && !single) byte = (19 - 10) << 3;  // windowLog 19 (512 KiB), like level 1
+    else if (l >= fpos && l < hn) byte = (uint32_t)(fv >> (8 * (l - fpos))) & 0xFFu;
+    if (write && l < hn) dst[l] = (uint8_t)byte;
+    return hn;
+}
+
+__device__ __forceinline__ int64_t ze_bound(int64_t n) { return n + (n >> 8) + (n < BLK ? (BLK - n) >> 11 : 0); }
+
+// Block-parallel mode (BPAR): one work item = one 128 KiB block of a frame,
+// encoded into its slot dst[hn + k * SLOT] (a block and its literal staging
+// never exceed SLOT bytes); zstd_compact_kernel then moves the blocks down
+// to their frame positions.  The wave's hash table starts from the WARM bytes
+// before the block (every position inserted), the repeat offset starts
+// unknown (no repeat code before the block's first explicit offset): the
+// frames are valid RFC 8878 frames, the window (512 KiB) reaches back into
+// earlier blocks.  Without BPAR one wave encodes a whole frame, block after
+// block.
+constexpr int64_t SLOT = BLK + 16;
+#ifndef JFS_ZE_WARM_KB
+#define JFS_ZE_WARM_KB 64
+#endif
+constexpr int64_t WARM = (int64_t)JFS_ZE_WARM_KB << 10;
+
+template <bool BPAR>
+__global__ __launch_bounds__(64) void zstd_encode_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
+                                                        int32_t *__restrict__ ret, uint64_t *__restrict__ scratch,
+                                                        const int2 *__restrict__ work, int nwork,
+                                                        int32_t *__restrict__ bsize) {
+    __shared__ Smem s;
+    if (!BPAR && (int)blockIdx.x >= nblk) return;
+    const int l = lane_id();
+    // per-wave scratch: sequences and Huffman streams of the current block
+    const int64_t sidx = (int64_t)blockIdx.x;
+    uint64_t *seq = (uint64_t *)((uint8_t *)scratch + sidx * SCR_PER);
+    g_u8 *lscr = (g_u8 *)((uint8_t *)scratch + sidx * SCR_PER + SEQ_CAP * 8);
     // tables
-    for (int k = l; k < (1 << HBITS); k += 64) s.table[k] = 0;
     for (int v = l; v < 64; v += 64) {
         int c = 0;
         while (c + 1 < 36 && LL_BASE[c + 1] <= (uint32_t)v) c++;
@@ -783,37 +820,43 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(const jfs_dev_block *__
     __builtin_amdgcn_wave_barrier();
     build_ctab(s.q.tsym, s.q.cumul, s.ct[2], OF_DEF, 28, 5);
     __syncthreads();
-
-    // ---- frame header: magic, FHD, [Window_Descriptor], Frame_Content_Size
-    int64_t op;
-    {
-        const bool single = n <= (1 << 19);
-        int fcs_flag, fs;
-        if (single) {
-            if (n < 256) { fcs_flag = 0; fs = 1; }
-            else if (n < 65536 + 256) { fcs_flag = 1; fs = 2; }
-            else { fcs_flag = 2; fs = 4; }
-        } else {
-            fcs_flag = n < (1ll << 32) ? 2 : 3;
-            fs = fcs_flag == 2 ? 4 : 8;
-        }
-        const uint32_t fhd = (uint32_t)((fcs_flag << 6) | (single ? 0x20 : 0));
-        const int fpos = single ? 5 : 6;  // FCS position
-        const uint64_t fv = (uint64_t)n - (fs == 2 ? 256 : 0);
-        const int hn = fpos + fs;
-        uint32_t byte = 0;
-        if (l < 4) byte = (0xFD2FB528u >> (8 * l)) & 0xFFu;
-        else if (l == 4) byte = fhd;
-        else if (l == 5 && !single) byte = (19 - 10) << 3;  // windowLog 19 (512 KiB), like level 1
-        else if (l >= fpos && l < hn) byte = (uint32_t)(fv >> (8 * (l - fpos))) & 0xFFu;
-        if (l < hn) dst[l] = (uint8_t)byte;
-        op = hn;
-    }
-
     ZE_DECL
+
+    for (int wi = BPAR ? (int)blockIdx.x : 0; BPAR ? wi < nwork : wi < 1; wi += BPAR ? (int)gridDim.x : 1) {
+    const int b = BPAR ? work[wi].x : (int)blockIdx.x;  // the frame (input)
+    const int kb = BPAR ? work[wi].y : 0;               // its block (BPAR)
+    const jfs_dev_block d = ((const gc_blk *)blocks)[b];
+    const gc_u8 *src = (const gc_u8 *)d.src;
+    g_u8 *dst = (g_u8 *)d.dst;
+    const int64_t n = d.src_len, cap = d.dst_cap;
+    if (n < 0 || cap < ze_bound(n)) {  // compress.go:86-89: cap(dst) < CompressBound -> "buffer too short"
+        if (l == 0) {
+            if (BPAR) bsize[wi] = -1;
+            else ret[b] = -2;
+        }
+        continue;
+    }
+    // ---- frame header (BPAR: written by the frame's first block)
+    const int hn = frame_header(n, !BPAR || kb == 0, dst);
+    const int64_t slot0 = BPAR ? hn + (int64_t)kb * SLOT : hn;
+    int64_t op = slot0;
+    for (int k = l; k < (1 << HBITS); k += 64) s.table[k] = 0;
+    int64_t bs = BPAR ? (int64_t)kb * BLK : 0;
+    if (BPAR && bs > 0) {  // warm-up: the positions of the WARM bytes before the block
+        __builtin_amdgcn_wave_barrier();
+        const int64_t w0 = bs > WARM ? bs - WARM : 0;
+        for (int64_t q0 = w0; q0 + 8 <= bs; q0 += 64) {
+            const int64_t q = q0 + l;
+            if (q + 8 <= bs) {
+                const uint64_t v = ld64u(src + q);
+                s.table[JFS_ZE_HASH == 6 ? hash6(v) : hash4((uint32_t)v)] = (uint32_t)q;
+            }
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+
     // ---- blocks (the repeat offsets carry across the frame's blocks, RFC 8878 3.1.1.5)
-    uint32_t rep0 = 1;  // Repeated_Offset1 (only it is reused: Offset_Value 1 with LL > 0)
-    int64_t bs = 0;
+    uint32_t rep0 = BPAR && bs > 0 ? 0u : 1u;  // Repeated_Offset1 (0: unknown; only it is reused: Offset_Value 1 with LL > 0)
     do {
         const int64_t be = bs + BLK < n ? bs + BLK : n;
         const bool last = be == n;
@@ -854,7 +897,7 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(const jfs_dev_block *__
                         uint32_t h = 0, E = 0;
                         if (on) {
                             const int64_t rp = P + 1;
-                            rep = JFS_ZE_REP && rep0 <= rp && ld32u(src + rp) == ld32u(src + rp - rep0);
+                            rep = JFS_ZE_REP && rep0 > 0 && rep0 <= rp && ld32u(src + rp) == ld32u(src + rp - rep0);
                             v = ld64u(src + P);
                             h = JFS_ZE_HASH == 6 ? hash6(v) : hash4((uint32_t)v);
                             E = s.table[h];
@@ -901,7 +944,7 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(const jfs_dev_block *__
                 {
 #else
                 const int64_t rp = ip + 1;
-                if (JFS_ZE_REP && rep0 <= rp && ld32u(src + rp) == ld32u(src + rp - rep0)) {
+                if (JFS_ZE_REP && rep0 > 0 && rep0 <= rp && ld32u(src + rp) == ld32u(src + rp - rep0)) {
                     cand = rp - rep0;
                     ip = rp;
                     ofv = 1;
@@ -1123,9 +1166,73 @@ __global__ __launch_bounds__(64) void zstd_encode_kernel(const jfs_dev_block *__
         __threadfence_block();
         ZE(6);
         bs = be;
-    } while (bs < n);
+    } while (!BPAR && bs < n);
+    if (l == 0) {
+        if (BPAR) bsize[wi] = (int32_t)(op - slot0);
+        else ret[b] = op <= cap ? (int32_t)op : -2;
+    }
+    }
     ZE_FLUSH();
-    if (l == 0) ret[b] = op <= cap ? (int32_t)op : -2;
+}
+
+// BPAR: move every frame's blocks from their slots to their places (ascending:
+// a block only moves down, over bytes already moved or its own) and report
+// the frame size.  One wave per frame; first[f] = index of its first item.
+__global__ __launch_bounds__(64) void zstd_compact_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
+                                                         int32_t *__restrict__ ret, const int32_t *__restrict__ bsize,
+                                                         const int32_t *__restrict__ first) {
+    const int f = blockIdx.x;
+    if (f >= nblk) return;
+    const int l = lane_id();
+    const jfs_dev_block d = ((const gc_blk *)blocks)[f];
+    g_u8 *dst = (g_u8 *)d.dst;
+    const int64_t n = d.src_len, cap = d.dst_cap;
+    const int i0 = first[f], i1 = first[f + 1];
+    bool bad = n < 0 || cap < ze_bound(n);
+    for (int i = i0; i < i1 && !bad; i++) bad = bsize[i] < 0;
+    if (bad) {
+        if (l == 0) ret[f] = -2;
+        return;
+    }
+    const int hn = frame_header(n, false, dst);
+    int64_t out = hn;
+    for (int i = i0; i < i1; i++) {
+        const int64_t from = hn + (int64_t)(i - i0) * SLOT, sz = bsize[i];
+        if (from != out) {
+            // dst[out, out + sz) <- dst[from, from + sz): 16-byte stores, the
+            // source read as aligned dwords (alignbyte), 1 KiB per wave step
+            int64_t x = 0;
+            const uint32_t hm = (uint32_t)(((uintptr_t)(dst + out)) & 15u), ha = (16u - hm) & 15u;
+            const int64_t head = (int64_t)ha < sz ? (int64_t)ha : sz;
+            uint8_t hb = 0;
+            if (l < head) hb = dst[from + l];
+            __builtin_amdgcn_wave_barrier();
+            if (l < head) dst[out + l] = hb;
+            x = head;
+            for (; x + 16 <= sz; x += 1024) {
+                const int64_t y = x + 16 * l;
+                uint4 o = make_uint4(0, 0, 0, 0);
+                const bool on = y + 16 <= sz;
+                if (on) {
+                    const uintptr_t a = (uintptr_t)(dst + from + y);
+                    const gc_u32 *w = (const gc_u32 *)(a & ~(uintptr_t)3);
+                    const uint32_t sh = (uint32_t)(a & 3u);
+                    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = sh ? w[4] : 0u;
+                    o.x = __builtin_amdgcn_alignbyte(w1, w0, sh);
+                    o.y = __builtin_amdgcn_alignbyte(w2, w1, sh);
+                    o.z = __builtin_amdgcn_alignbyte(w3, w2, sh);
+                    o.w = __builtin_amdgcn_alignbyte(w4, w3, sh);
+                }
+                if (on) *(g_u4 *)(dst + out + y) = o;
+            }
+            const int64_t xe = head + ((sz - head) & ~(int64_t)15);
+            uint8_t tb = 0;
+            if (xe + l < sz) tb = dst[from + xe + l];
+            if (xe + l < sz) dst[out + xe + l] = tb;
+        }
+        out += sz;
+    }
+    if (l == 0) ret[f] = out <= cap ? (int32_t)out : -2;
 }
 
 }  // namespace zstde
@@ -1135,8 +1242,28 @@ namespace {
 struct ZEScratch {
     std::mutex mu;
     uint64_t *d = nullptr;
-    size_t cap = 0;  // inputs
+    size_t cap = 0;  // waves
+    uint8_t *aux = nullptr;  // BPAR work list, frame starts, block sizes
+    size_t aux_cap = 0;
+    int waves = 0;   // resident encoder waves on this device (BPAR grid)
+    bool grow(size_t w) {
+        if (d) (void)hipFree(d);  // hipFree synchronises with work still using it
+        d = nullptr;
+        cap = 0;
+        if (hipMalloc((void **)&d, (size_t)jfs::zstde::SCR_PER * w) != hipSuccess) return false;
+        cap = w;
+        return true;
+    }
 };
+// JFS_ZSTD_BPAR=0: one wave per frame (blocks in order) instead of one work
+// item per 128 KiB block
+bool zstd_bpar() {
+    static const bool v = [] {
+        const char *e = getenv("JFS_ZSTD_BPAR");
+        return !(e && atoi(e) == 0);
+    }();
+    return v;
+}
 ZEScratch g_zes[16];
 }  // namespace
 
@@ -1157,15 +1284,58 @@ extern "C" int jfs_launch_zstd_encode(const jfs_dev_block *d_blocks, int nblk, i
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return -1;
     ZEScratch &z = g_zes[dev];
     std::lock_guard<std::mutex> lk(z.mu);
-    if (z.cap < (size_t)nblk) {
-        if (z.d) (void)hipFree(z.d);  // hipFree synchronises with work still using it
-        z.d = nullptr;
-        z.cap = 0;
-        if (hipMalloc((void **)&z.d, (size_t)SCR_PER * (size_t)nblk) != hipSuccess) return -1;  // bytes
-        z.cap = (size_t)nblk;
+    if (!zstd_bpar()) {
+        if (z.cap < (size_t)nblk && !z.grow((size_t)nblk)) return -1;
+        hipLaunchKernelGGL(zstd_encode_kernel<false>, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, d_ret, z.d,
+                           (const int2 *)nullptr, 0, (int32_t *)nullptr);
+        if (hipGetLastError() != hipSuccess) return -1;
+        // the scratch is shared by every launch on this device: finish before it is reused
+        return hipStreamSynchronize(stream) == hipSuccess ? 0 : -1;
     }
-    hipLaunchKernelGGL(zstd_encode_kernel, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, d_ret, z.d);
+    // block-parallel: one work item per 128 KiB block (the descriptors may
+    // have been written on this stream: read them after it drains)
+    std::vector<jfs_dev_block> h(nblk);
+    if (hipMemcpyAsync(h.data(), d_blocks, sizeof(jfs_dev_block) * nblk, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+        hipStreamSynchronize(stream) != hipSuccess)
+        return -1;
+    std::vector<int2> work;
+    std::vector<int32_t> first(nblk + 1);
+    for (int f = 0; f < nblk; f++) {
+        first[f] = (int32_t)work.size();
+        const int64_t n = h[f].src_len;
+        const int64_t nb = n <= 0 ? 1 : (n + BLK - 1) / BLK;
+        for (int64_t k = 0; k < nb; k++) work.push_back(make_int2(f, (int)k));
+    }
+    first[nblk] = (int32_t)work.size();
+    const int nwork = (int)work.size();
+    if (z.waves == 0) {
+        int per_cu = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, zstd_encode_kernel<true>, 64, 0) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return -1;
+        z.waves = std::max(1, per_cu) * std::max(1, cus);
+    }
+    const int grid = std::min(nwork, z.waves);
+    if (z.cap < (size_t)grid && !z.grow((size_t)grid)) return -1;
+    const size_t wb = sizeof(int2) * nwork, fb = sizeof(int32_t) * (nblk + 1), sb = sizeof(int32_t) * nwork;
+    if (z.aux_cap < wb + fb + sb) {
+        if (z.aux) (void)hipFree(z.aux);
+        z.aux = nullptr;
+        z.aux_cap = 0;
+        if (hipMalloc((void **)&z.aux, wb + fb + sb) != hipSuccess) return -1;
+        z.aux_cap = wb + fb + sb;
+    }
+    int2 *d_work = (int2 *)z.aux;
+    int32_t *d_first = (int32_t *)(z.aux + wb), *d_bsize = (int32_t *)(z.aux + wb + fb);
+    if (hipMemcpyAsync(d_work, work.data(), wb, hipMemcpyHostToDevice, stream) != hipSuccess ||
+        hipMemcpyAsync(d_first, first.data(), fb, hipMemcpyHostToDevice, stream) != hipSuccess)
+        return -1;
+    hipLaunchKernelGGL(zstd_encode_kernel<true>, dim3(grid), dim3(64), 0, stream, d_blocks, nblk, d_ret, z.d,
+                       (const int2 *)d_work, nwork, d_bsize);
     if (hipGetLastError() != hipSuccess) return -1;
-    // the scratch is shared by every launch on this device: finish before it is reused
+    hipLaunchKernelGGL(zstd_compact_kernel, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, d_ret,
+                       (const int32_t *)d_bsize, (const int32_t *)d_first);
+    if (hipGetLastError() != hipSuccess) return -1;
+    // the scratch and the host work list are shared / local: finish first
     return hipStreamSynchronize(stream) == hipSuccess ? 0 : -1;
 }

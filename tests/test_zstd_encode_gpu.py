@@ -149,3 +149,33 @@ def test_zstd_encode_ratio_floor(gpu):
     ratio = sum(len(s) for s in srcs) / sum(r)
     print("zstd GPU ratio", ratio)
     assert ratio >= 3.0, ratio
+
+
+def test_zstd_encode_many_frames_block_parallel(gpu, oracle):
+    """Block-parallel encoding (zstd_encode.hip BPAR): one work item per 128 KiB
+    block, blocks moved into place per frame.  Many frames of 1..33 blocks in
+    one launch, repeat-offset-heavy periodic data across block starts (the
+    first sequence of a block must not use a repeat code it cannot know),
+    sizes at block boundaries; every frame decodes through the oracle and the
+    GPU decoder."""
+    rng = np.random.default_rng(17)
+    srcs = []
+    for i in range(40):
+        n = int(rng.choice([1, 131072, 131073, 262143, 262144, 3 * 131072 + 77, 1 << 20, (4 << 20) + 5]))
+        if i % 3 == 0:
+            pat = rng.integers(0, 256, 7, dtype=np.uint8).tobytes()
+            b = bytearray((pat * (n // 7 + 1))[:n])
+            for j in range(0, n, 4099):  # sparse noise: repeat offsets resume after each break
+                b[j] ^= 0x5A
+            srcs.append(bytes(b))
+        else:
+            srcs.append(gen_block("TZR"[i % 3], 2000 + i, n))
+    r, frames = encode_device(srcs, gpu, dst_mis=5)
+    for s, x, f in zip(srcs, r, frames):
+        assert 0 < x <= _bound(len(s)), (len(s), x)
+        n, out = oracle.zstd_decompress(f, len(s))
+        assert n == len(s) and out == s, (len(s), n)
+    from tests.test_zstd_gpu import run_device
+    r2, outs = run_device(frames, [len(s) for s in srcs], gpu)
+    for s, x, o in zip(srcs, r2, outs):
+        assert x == len(s) and o == s
