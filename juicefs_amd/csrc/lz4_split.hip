@@ -147,10 +147,15 @@ __device__ __forceinline__ Tok parse(const gc_u8 *s, int64_t n, int64_t x, bool 
 }
 
 // block of global segment g (blocks are few: linear search over the seg0's)
+// the block holding segment g: the last b with seg0 <= g (binary search)
 __device__ __forceinline__ int block_of(const SBlock *blk, int nb, int g) {
-    int b = 0;
-    while (b + 1 < nb && blk[b + 1].seg0 <= g) b++;
-    return b;
+    int lo = 0, hi = nb - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (blk[mid].seg0 <= g) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
 }
 
 __global__ void plan_kernel(const jfs_dev_block *__restrict__ desc, int nb, Scratch sc) {

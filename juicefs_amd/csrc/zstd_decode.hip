@@ -1648,6 +1648,9 @@ constexpr int FB = 64;           // far-source prefetch bytes per lane (16 B ali
 constexpr int FBUSE = FB - 16;
 constexpr int BSPAN = R / 2;     // max output span of one lane-parallel batch
 constexpr int LONGI = 1024;      // items longer than this are copied by the whole wave
+#ifndef JFS_ZEXEC_NEARSER
+#define JFS_ZEXEC_NEARSER 1  // near matches: one lane-parallel round, the rest by the whole wave in order
+#endif
 
 struct XSmem {
     alignas(16) uint8_t ring[R];
@@ -1910,10 +1913,39 @@ __device__ __forceinline__ void x_batch(XSmem &s, X &x, bool act, int32_t o, uin
             __builtin_amdgcn_wave_barrier();
         }
     }
-    // matches (ring parts) in rounds
+    // matches (ring parts)
     bool pend = hasm && nfar < (int32_t)ml;
     const int32_t ms2 = ms + nfar, msrc2 = msrc + nfar, ml2 = (int32_t)ml - nfar;
+#if JFS_ZEXEC_NEARSER
+    // one lane-parallel round for every match whose source is final (far, or
+    // wholly before the batch), then the rest by the whole wave in lane order
+    // (output order: every source is final when its match's turn comes)
+    {
+        const int32_t send = msrc + (int32_t)ml < ms ? msrc + (int32_t)ml : ms;
+        const bool ready = pend && (far || send <= O0);
+        if (ready) {
+            cp_ring(s, x, msrc2, ms2, ml2, off);
+            pend = false;
+        }
+        __builtin_amdgcn_wave_barrier();
+        XP_ADD(6, 1);
+        for (uint64_t pm = __ballot(pend); pm; pm &= pm - 1) {
+            const int j = (int)__builtin_ctzll(pm);
+            const int32_t jd = (int32_t)readlane((uint32_t)ms2, j), jsrc = (int32_t)readlane((uint32_t)msrc2, j);
+            const int32_t jn = (int32_t)readlane((uint32_t)ml2, j), D = jd - jsrc;
+            const int32_t stp = D < 64 ? D : 64;
+            for (int32_t k = 0; k < jn; k += stp) {
+                const int32_t i = k + l;
+                if (l < stp && i < jn) s.ring[slot(x, jd + i)] = s.ring[slot(x, jsrc + i)];
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+        pend = false;
+    }
     int guard = 0;
+#else
+    int guard = 0;
+#endif
     while (__ballot(pend)) {
         const int32_t front = (int32_t)dwave_min(pend ? (uint32_t)ms : 0x7FFFFFFFu);
         const int32_t send = msrc + (int32_t)ml < ms ? msrc + (int32_t)ml : ms;
