@@ -310,11 +310,13 @@ typedef struct {
 
 /* one table per mode; returns bytes consumed or -1 */
 static int64_t seq_table(fse_table *t, int *have, int mode, const uint8_t *src, int64_t n, const int16_t *def,
-                         int defal, int maxsym, int maxal) {
+                         int defmax, int defal, int maxsym, int maxal) {
     if (mode == 0) {
+        /* the predefined distribution covers symbols 0..defmax (RFC 8878
+         * 3.1.1.3.2.2; OF: 0..28 while codes go to 31) */
         int16_t norm[64];
-        memcpy(norm, def, sizeof(int16_t) * (maxsym + 1));
-        if (build_fse(t, norm, maxsym, defal)) return -1;
+        memcpy(norm, def, sizeof(int16_t) * (defmax + 1));
+        if (build_fse(t, norm, defmax, defal)) return -1;
         *have = 1;
         return 0;
     }
@@ -421,13 +423,13 @@ static int64_t zo_block(zo_state *st, const uint8_t *src, int64_t n, uint8_t *ds
         int modes = src[ip++];
         if ((modes & 3) && zo_strict_reserved) return ZO_ERR_CORRUPT;
         int64_t c;
-        c = seq_table(&st->ll, &st->have_ll, modes >> 6, src + ip, n - ip, LL_DEF, 6, 35, 9);
+        c = seq_table(&st->ll, &st->have_ll, modes >> 6, src + ip, n - ip, LL_DEF, 35, 6, 35, 9);
         if (c < 0) return ZO_ERR_CORRUPT;
         ip += c;
-        c = seq_table(&st->of, &st->have_of, (modes >> 4) & 3, src + ip, n - ip, OF_DEF, 5, 31, 8);
+        c = seq_table(&st->of, &st->have_of, (modes >> 4) & 3, src + ip, n - ip, OF_DEF, 28, 5, 31, 8);
         if (c < 0) return ZO_ERR_CORRUPT;
         ip += c;
-        c = seq_table(&st->ml, &st->have_ml, (modes >> 2) & 3, src + ip, n - ip, ML_DEF, 6, 52, 9);
+        c = seq_table(&st->ml, &st->have_ml, (modes >> 2) & 3, src + ip, n - ip, ML_DEF, 52, 6, 52, 9);
         if (c < 0) return ZO_ERR_CORRUPT;
         ip += c;
         bbr b;
