@@ -350,17 +350,45 @@ __global__ __launch_bounds__(T) void emit_kernel(int nb, int nseg_all, Scratch s
             st.bad = 1;
             return;
         }
-        for (int64_t i = 0; i < t.ll; i++) org[op + i] = (uint32_t)(-(t.lenip + i) - 1);
+        // origin entries, 16-byte stores where the run is 4-aligned (the
+        // area starts 16-byte aligned: org_off is a multiple of 4 entries)
+        {
+            const uint32_t v0 = (uint32_t)(-(t.lenip) - 1);  // entry i = v0 - i
+            int64_t i = 0;
+            for (; i < t.ll && ((op + i) & 3); i++) org[op + i] = v0 - (uint32_t)i;
+            for (; i + 4 <= t.ll; i += 4) {
+                const uint32_t v = v0 - (uint32_t)i;
+                *(g_u4 *)(org + op + i) = make_uint4(v, v - 1u, v - 2u, v - 3u);
+            }
+            for (; i < t.ll; i++) org[op + i] = v0 - (uint32_t)i;
+        }
         op += t.ll;
         if (t.last) {
             st.last_ok = 1;
             return;
         }
-        const int64_t base = op - t.off;
-        int64_t j = 0;
-        for (int64_t i = 0; i < t.ml; i++) {
-            org[op + i] = (uint32_t)(base + j);
-            j = j + 1 == t.off ? 0 : j + 1;
+        {
+            const int64_t base = op - t.off;
+            const uint32_t off = (uint32_t)t.off;
+            uint32_t j = 0;  // entry i = base + (i mod off)
+            int64_t i = 0;
+            for (; i < t.ml && ((op + i) & 3); i++) {
+                org[op + i] = (uint32_t)(base + j);
+                j = j + 1 == off ? 0u : j + 1;
+            }
+            for (; i + 4 <= t.ml; i += 4) {
+                uint32_t e[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    e[q] = (uint32_t)(base + j);
+                    j = j + 1 == off ? 0u : j + 1;
+                }
+                *(g_u4 *)(org + op + i) = make_uint4(e[0], e[1], e[2], e[3]);
+            }
+            for (; i < t.ml; i++) {
+                org[op + i] = (uint32_t)(base + j);
+                j = j + 1 == off ? 0u : j + 1;
+            }
         }
         op += t.ml;
         x = t.next;
