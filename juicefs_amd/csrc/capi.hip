@@ -1096,7 +1096,7 @@ struct Gather {
 int coalesce_chunk_blocks() {
     static int v = [] {
         const char *e = getenv("JFS_COALESCE_CHUNK");
-        return e ? std::max(0, atoi(e)) : 8;
+        return e ? std::max(0, atoi(e)) : 16;
     }();
     return v;
 }

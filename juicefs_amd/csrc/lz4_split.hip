@@ -395,43 +395,48 @@ __global__ __launch_bounds__(T) void emit_kernel(int nb, int nseg_all, Scratch s
     }
 }
 
-// grid (x: 4 entries per thread, y: block)
+// grid (x: JX workgroups per block, y: block); each thread strides over its
+// block's entries, 4 at a time (a fixed, small grid: the rounds after the
+// first mostly find their block settled, and dispatching a workgroup per
+// 1,024 entries for them cost more than the hops).
 __global__ __launch_bounds__(T) void jump_kernel(Scratch sc, int round) {
     const int b = blockIdx.y;
     BStat &st = sc.st[b];
     if (st.fix[FIX_ROUNDS - 1] || st.bad) return;
     if (round > 0 && !st.jmp[round - 1]) return;
-    const int64_t p = ((int64_t)blockIdx.x * T + threadIdx.x) * 4;
     const int64_t total = st.total;
-    if (p >= total) return;
     const SBlock B = sc.blk[b];
     g_u32 *org = (g_u32 *)(sc.org + B.org_off);
-    const int lim = total - p < 4 ? (int)(total - p) : 4;
-    uint4 v = *(const g_u4 *)(org + p);
-    const uint32_t e0[4] = {v.x, v.y, v.z, v.w};
-    int32_t o[4];
+    bool any = false;
+    for (int64_t p = ((int64_t)blockIdx.x * T + threadIdx.x) * 4; p < total; p += (int64_t)gridDim.x * T * 4) {
+        const int lim = total - p < 4 ? (int)(total - p) : 4;
+        uint4 v = *(const g_u4 *)(org + p);
+        const uint32_t e0[4] = {v.x, v.y, v.z, v.w};
+        int32_t o[4];
 #pragma unroll
-    for (int i = 0; i < 4; i++) o[i] = i < lim ? (int32_t)e0[i] : -1;
-    // the four entries' hops interleaved: four independent loads in flight
-    for (int h = 0; h < HOPS; h++) {
-        if (o[0] < 0 && o[1] < 0 && o[2] < 0 && o[3] < 0) break;
-        int32_t nx[4];
+        for (int i = 0; i < 4; i++) o[i] = i < lim ? (int32_t)e0[i] : -1;
+        // the four entries' hops interleaved: four independent loads in flight
+        for (int h = 0; h < HOPS; h++) {
+            if (o[0] < 0 && o[1] < 0 && o[2] < 0 && o[3] < 0) break;
+            int32_t nx[4];
 #pragma unroll
-        for (int i = 0; i < 4; i++) nx[i] = o[i] >= 0 ? (int32_t)org[o[i]] : o[i];
+            for (int i = 0; i < 4; i++) nx[i] = o[i] >= 0 ? (int32_t)org[o[i]] : o[i];
 #pragma unroll
-        for (int i = 0; i < 4; i++) o[i] = nx[i];
+            for (int i = 0; i < 4; i++) o[i] = nx[i];
+        }
+        uint32_t e[4];
+        bool changed = false;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            e[i] = i < lim ? (uint32_t)o[i] : e0[i];
+            changed |= e[i] != e0[i];
+        }
+        if (changed) {
+            *(g_u4 *)(org + p) = make_uint4(e[0], e[1], e[2], e[3]);
+            any = true;
+        }
     }
-    uint32_t e[4];
-    bool changed = false;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        e[i] = i < lim ? (uint32_t)o[i] : e0[i];
-        changed |= e[i] != e0[i];
-    }
-    if (changed) {
-        *(g_u4 *)(org + p) = make_uint4(e[0], e[1], e[2], e[3]);
-        st.jmp[round] = 1;
-    }
+    if (any) st.jmp[round] = 1;
 }
 
 // blocks decoded by this path / handed to the exact kernel (diagnostics)
@@ -530,7 +535,10 @@ extern "C" int jfs_launch_lz4_split(const jfs_dev_block *d_desc, int nb, int32_t
     }
     hipLaunchKernelGGL(scan_kernel, dim3(nb), dim3(T), 0, st, sc);
     if (nseg_all > 0) hipLaunchKernelGGL(emit_kernel, dim3(gs), dim3(T), 0, st, nb, (int)nseg_all, sc);
-    for (int r = 0; r < JUMP_ROUNDS; r++) hipLaunchKernelGGL(jump_kernel, gp, dim3(T), 0, st, sc, r);
+    // jump grid: about 2,048 workgroups in all (every entry of a 4 MiB block
+    // is covered after a few strides), at most one per 1,024 entries
+    const unsigned jx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((max_cap / 4 + T) / T, (2048 + nb - 1) / nb));
+    for (int r = 0; r < JUMP_ROUNDS; r++) hipLaunchKernelGGL(jump_kernel, dim3(jx, (unsigned)nb), dim3(T), 0, st, sc, r);
     hipLaunchKernelGGL(verdict_kernel, dim3((nb + 63) / 64), dim3(64), 0, st, nb, sc, d_ret, todo);
     hipLaunchKernelGGL(gather_kernel, gp, dim3(T), 0, st, sc);
     if (hipGetLastError() != hipSuccess) return -1;
