@@ -41,7 +41,7 @@ __device__ unsigned long long g_zprof[8];
 #define ZP_NOW() __builtin_amdgcn_s_memtime()
 #define ZP_ADD(i, v) do { if (lane_id() == 0) atomicAdd(&g_zprof[i], (unsigned long long)(v)); } while (0)
 #define XP_ADD(i, v) do { x.pacc[i] += (v); } while (0)
-// zseq: 0 phase A (walk + tables), 1 table staging, 2 phase B decode, 3 phase C, 4 sub-groups, 5 groups
+// zseq: 0 phase A (walk + tables), 1 table staging, 2 phase B decode, 3 phase C, 4 decoder barrier waits (v2), 5 groups
 __device__ unsigned long long g_zsprof[8];
 #define ZS_ADD(i, v) do { if (lane_id() == 0) atomicAdd(&g_zsprof[i], (unsigned long long)(v)); } while (0)
 #else
@@ -1053,6 +1053,56 @@ constexpr int ZK = JFS_ZSEQ_ARENA > 0 ? 8 : 4;
 constexpr int ZRB = JFS_ZSEQ_ARENA > 0 ? 256 : 128;
 static_assert(ZK * 12 + 24 <= ZRB - 16 && ZRB / 16 - 1 <= 15 + 0, "a period's bits must stay resident");
 static_assert(ZARENA == 0 || ZARENA >= 1280 + 8, "one block's largest tables must fit");
+// Round 3 (default): a workgroup of two waves.  Wave 0 walks the headers and
+// builds the tables (phase A), then decodes a group of ZNB blocks (one lane
+// each) with every table cell and bitstream byte read from LDS — it never
+// waits on HBM; its item stores are fire-and-forget.  Wave 1 (the mover)
+// stages the group's tables into LDS and keeps each lane's bitstream ring
+// filled ahead of the decoder, one barrier per period of ZK2 sequences.
+#ifndef JFS_ZSEQ_V2
+#define JFS_ZSEQ_V2 1
+#endif
+#ifndef JFS_ZREP_BR
+#define JFS_ZREP_BR 1  // branchy repeat-offset update: measured faster than the select chain (168.5 vs 189.5 ms)
+#endif
+#ifndef JFS_ZUNROLL
+#define JFS_ZUNROLL 0
+#endif
+constexpr int ZNB = 16;     // blocks per group = decoder lanes (3 workgroups per CU by LDS)
+constexpr int ZK2 = 8;      // sequences per period
+constexpr int ZRB2 = 512;   // bitstream ring bytes per lane (32 blocks of 16 B)
+#ifndef JFS_ZMOVE_D
+#define JFS_ZMOVE_D 2  // periods between a mover load and its landing in the ring
+#endif
+constexpr int ZMD = JFS_ZMOVE_D;
+constexpr int ZAHEAD = ZMD == 2 ? 27 : 24;  // ring blocks the mover keeps below the published position
+// <= 89 bits per sequence: a period moves the position down <= 6 blocks and
+// a refill window reaches 128 bits below it (one block more).  Loads issued
+// in iteration p land during iteration p + ZMD and serve period p + ZMD + 1,
+// whose reads reach (ZMD + 1) periods + 1 block below the position the
+// target came from; and a landing block must not displace (32 slots) one the
+// decoder still reads (<= 1 block above its position).
+constexpr int ZPB = (ZK2 * 89 + 127) / 128;
+static_assert((ZMD + 1) * ZPB + 7 <= ZAHEAD && ZAHEAD <= ZRB2 / 16 - 2 && ZPB + 2 <= 8, "ring budget");
+#if JFS_ZSEQ_V2
+struct SeqSmem {
+    union {
+        struct {  // phase A scratch (wave 0 only, between groups)
+            uint8_t stage[256];
+            int16_t norm[64];
+            uint8_t symat[512], mark[512], ksym[512];
+        };
+        alignas(16) uint8_t bring[ZNB][ZRB2];  // phase B: per-lane bitstream rings
+    };
+    alignas(16) uint16_t arena[ZNB][TAB_CELLS];  // phase B: the group's tables (LL 0, OF 512, ML 768)
+    uint32_t lut_ll[36], lut_ml[53];
+    GBlk g[ZNB];
+    int32_t pos[2][ZNB];  // decoder bit positions published at each period's barrier
+    int32_t more[2];      // any lane still decoding (per period parity)
+    int32_t cmd;          // wave 0 -> wave 1: blocks in the group, 0 = done
+};
+static_assert(sizeof(SeqSmem) * 3 <= 160 * 1024, "three sequence workgroups per CU");
+#else
 struct SeqSmem {
     uint8_t stage[256];
     int16_t norm[64];
@@ -1070,6 +1120,7 @@ struct SeqSmem {
     uint4 ibuf[ZK][ZSUB];                  // items of the current period, flushed together
 #endif
 };
+#endif
 
 // u16 cell = sym | ns << 6  (nb = al - highbit(ns), next-state base = (ns << nb) - 2^al)
 __device__ __forceinline__ void build_seq_fse_g(g_u16 *t, const int16_t *norm, int32_t maxsym, int32_t al,
@@ -1254,7 +1305,7 @@ __device__ __forceinline__ uint32_t lr_read(LR &r, int n) {
 }
 #endif
 
-#if JFS_ZSEQ_ARENA > 0 || JFS_ZSEQ_RING
+#if !JFS_ZSEQ_V2 && (JFS_ZSEQ_ARENA > 0 || JFS_ZSEQ_RING)
 // Phase B with the sequence bitstreams staged in per-lane LDS rings and the
 // items buffered in LDS: one HBM round trip per period of ZK sequences (ring
 // refill + item flush) instead of several per sequence.  TP: table cells in
@@ -1358,6 +1409,7 @@ __device__ __forceinline__ void seq_periods(SeqSmem &sm, const GBlk &d, bool min
 
 #endif
 
+#if !JFS_ZSEQ_V2
 // phases B and C for the collected group
 __device__ __forceinline__ void seq_group(SeqSmem &sm, int gn, const gc_u16 *tabs, uint32_t *e0, uint32_t *e1,
                                           uint32_t *e2) {
@@ -1524,14 +1576,345 @@ __device__ __forceinline__ void seq_group(SeqSmem &sm, int gn, const gc_u16 *tab
     __builtin_amdgcn_wave_barrier();
     { const uint64_t t = ZP_NOW(); ZS_ADD(3, t - zt); }
 }
+#endif  // !JFS_ZSEQ_V2
 
-__global__ __launch_bounds__(64) void zseq_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
-                                                  ZInfo *__restrict__ info, uint16_t *__restrict__ tabs_all,
-                                                  uint4 *__restrict__ items_all, int strict_reserved) {
+#if JFS_ZSEQ_V2
+// LDS-only barrier between the decoder and mover waves (the decoder's item
+// stores stay in flight)
+__device__ __forceinline__ void zsync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Geometry of a block's sequence bitstream in 16-byte blocks relative to the
+// aligned base b16: bytes [m, m + bsz); blocks below lowk precede the input.
+struct ZGeo {
+    const gc_u4 *b16;
+    int32_t m, top, kt, lowk;
+};
+__device__ __forceinline__ ZGeo zgeo(const GBlk &d) {
+    ZGeo g;
+    const uintptr_t a = (uintptr_t)d.bs;
+    g.b16 = (const gc_u4 *)(a & ~(uintptr_t)15);
+    g.m = (int32_t)(a & 15);
+    g.top = g.m + d.bsz;
+    g.kt = (g.top - 1) >> 4;
+    g.lowk = -(int32_t)((((uintptr_t)g.b16) - (((uintptr_t)d.in) & ~(uintptr_t)15)) >> 4);
+    return g;
+}
+__device__ __forceinline__ uint32_t zr_dw(const uint8_t *ring, int32_t q) {
+    return *(const uint32_t *)(ring + (q & (ZRB2 - 1)));
+}
+// Refill: bits [left - 96, left) from the ring (one round of four LDS dword
+// reads; the mover wrote zeros below the stream start, so bits there read as
+// zero, like lr_read).  hi = bits [left - 64, left), lo = bits [left - 96, left - 64).
+__device__ __forceinline__ void zw_fill(const uint8_t *ring, int32_t left, uint64_t &hi, uint32_t &lo) {
+    const int32_t cb = ((left - 96) >> 5) << 2;  // 8 * cb in (left - 128, left - 96]
+    const uint32_t d0 = zr_dw(ring, cb), d1 = zr_dw(ring, cb + 4), d2 = zr_dw(ring, cb + 8), d3 = zr_dw(ring, cb + 12);
+    const uint64_t A = ((uint64_t)d1 << 32) | d0, B = ((uint64_t)d3 << 32) | d2;
+    const int32_t t = left - 8 * cb - 64;  // [32, 64)
+    hi = (A >> t) | (B << (64 - t));
+    lo = (uint32_t)(A >> (t - 32));
+}
+// a ring block as the decoder must see it: blocks before the stream's
+// first byte (k < 0, and bytes [0, m) of block 0) read as zero
+__device__ __forceinline__ uint4 zclip(uint4 v, int32_t k, int32_t m) {
+    if (k < 0) return make_uint4(0, 0, 0, 0);
+    if (k == 0 && m > 0) {
+        const int32_t b0 = m, b1 = m - 4, b2 = m - 8, b3 = m - 12;
+        v.x = b0 >= 4 ? 0u : v.x & (~0u << (8 * b0));
+        v.y = b1 >= 4 ? 0u : b1 <= 0 ? v.y : v.y & (~0u << (8 * b1));
+        v.z = b2 >= 4 ? 0u : b2 <= 0 ? v.z : v.z & (~0u << (8 * b2));
+        v.w = b3 <= 0 ? v.w : v.w & (~0u << (8 * b3));
+    }
+    return v;
+}
+// next n (<= 31) bits below the c already consumed from the top of hi
+__device__ __forceinline__ uint32_t zw_get(uint64_t hi, int32_t &c, uint32_t n) {
+    const uint32_t x = (uint32_t)((hi << c) >> 32);
+    c += (int32_t)n;
+    return __builtin_amdgcn_ubfe(x, 32u - n, n);
+}
+// the 64-bit window after c (<= 63) bits were consumed; its top 32 bits are exact
+__device__ __forceinline__ uint64_t zw_shift(uint64_t hi, uint32_t lo, int32_t c) {
+    return c ? (hi << c) | (((uint64_t)lo << 32) >> (64 - c)) : hi;
+}
+
+// Wave 1: stage the group's tables into the arena, prefill the rings, then
+// one refill round per period until the decoder reports no lane running.
+__device__ __forceinline__ void zmover(SeqSmem &sm, int gn, const gc_u16 *tabs) {
+    const int l = lane_id();
+    [[maybe_unused]] uint64_t zt = ZP_NOW();
+    for (int j0 = 0; j0 < gn; j0 += 4) {
+        uint4 v[4][3];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int j = j0 + u;
+            const GBlk &d = sm.g[j < gn ? j : 0];
+            const uint32_t al = d.al;
+            const int32_t n16l = ((2 << (al & 0xFF)) + 15) >> 4, n16o = ((2 << ((al >> 8) & 0xFF)) + 15) >> 4,
+                          n16m = ((2 << ((al >> 16) & 0xFF)) + 15) >> 4;
+            v[u][0] = v[u][1] = v[u][2] = make_uint4(0, 0, 0, 0);
+            if (j < gn && d.nseq > 0) {
+                if (l < n16l) v[u][0] = ((const gc_u4 *)(tabs + d.tll))[l];
+                if (l < n16o) v[u][1] = ((const gc_u4 *)(tabs + d.tof))[l];
+                if (l < n16m) v[u][2] = ((const gc_u4 *)(tabs + d.tml))[l];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int j = j0 + u;
+            if (j >= gn) break;
+            uint4 *ar = (uint4 *)sm.arena[j];
+            const uint32_t al = sm.g[j].al;
+            if (l < (((2 << (al & 0xFF)) + 15) >> 4)) ar[l] = v[u][0];
+            if (l < (((2 << ((al >> 8) & 0xFF)) + 15) >> 4)) ar[64 + l] = v[u][1];
+            if (l < (((2 << ((al >> 16) & 0xFF)) + 15) >> 4)) ar[96 + l] = v[u][2];
+        }
+    }
+    // lanes j, j + 16, j + 32, j + 48 serve block j (q = lane >> 4)
+    const int j = l & (ZNB - 1), q = l >> 4;
+    const bool on = j < gn && sm.g[j < gn ? j : 0].nseq > 0 && sm.g[j < gn ? j : 0].bsz > 0;
+    const ZGeo g = zgeo(sm.g[j < gn ? j : 0]);
+    uint8_t *ring = sm.bring[j];
+    // blocks below -3 are never read (a lane stops once its position is
+    // below the stream start); blocks [-3, 0) are written as zeros
+    constexpr int32_t KFLOOR = -3;
+    // prefill blocks [kt - (ZAHEAD + 3), kt]
+    int32_t lr = g.kt + 1;
+    {
+        const int32_t lo = g.kt - (ZAHEAD + 3) > KFLOOR ? g.kt - (ZAHEAD + 3) : KFLOOR;
+        uint4 v[(ZAHEAD + 7) / 4];
+#pragma unroll
+        for (int i = 0; i < (ZAHEAD + 7) / 4; ++i) {
+            const int32_t k = g.kt - q - 4 * i;
+            v[i] = make_uint4(0, 0, 0, 0);
+            if (on && k >= lo && k >= 0) v[i] = g.b16[k];
+        }
+#pragma unroll
+        for (int i = 0; i < (ZAHEAD + 7) / 4; ++i) {
+            const int32_t k = g.kt - q - 4 * i;
+            if (on && k >= lo) *(uint4 *)(ring + ((k & (ZRB2 / 16 - 1)) << 4)) = zclip(v[i], k, g.m);
+        }
+        if (on) lr = lo;
+    }
+    { const uint64_t t = ZP_NOW(); ZS_ADD(1, t - zt); }
+    zsync();  // tables and rings ready
+    // pend[0]: loads issued ZMD iterations ago (landed now), pend[ZMD - 1]: newest
+    int32_t pend_k[ZMD][2];
+    uint4 pend_v[ZMD][2];
+    bool pend_on[ZMD][2];
+#pragma unroll
+    for (int d = 0; d < ZMD; ++d)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) { pend_k[d][i] = 0; pend_v[d][i] = make_uint4(0, 0, 0, 0); pend_on[d][i] = false; }
+    for (int p = 0;; ++p) {
+        // land the blocks loaded ZMD periods ago
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+            if (pend_on[0][i]) *(uint4 *)(ring + ((pend_k[0][i] & (ZRB2 / 16 - 1)) << 4)) = zclip(pend_v[0][i], pend_k[0][i], g.m);
+#pragma unroll
+        for (int d = 0; d + 1 < ZMD; ++d)
+#pragma unroll
+            for (int i = 0; i < 2; ++i) { pend_k[d][i] = pend_k[d + 1][i]; pend_v[d][i] = pend_v[d + 1][i]; pend_on[d][i] = pend_on[d + 1][i]; }
+        // next loads: ZAHEAD blocks below the position published at the last barrier
+        const int32_t left = p == 0 ? 0 : sm.pos[(p - 1) & 1][j];
+        const int32_t tgt = p == 0 ? lr : ((left - 1) >> 7) - ZAHEAD;
+        int32_t lo = lr - 8;
+        if (tgt > lo) lo = tgt;
+        if (KFLOOR > lo) lo = KFLOOR;
+        if (lo > lr) lo = lr;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int32_t k = lr - 1 - q - 4 * i;
+            pend_k[ZMD - 1][i] = k;
+            pend_on[ZMD - 1][i] = on && k >= lo;
+            pend_v[ZMD - 1][i] = make_uint4(0, 0, 0, 0);
+            if (pend_on[ZMD - 1][i] && k >= 0) pend_v[ZMD - 1][i] = g.b16[k];
+        }
+        if (on && lo < lr) lr = lo;
+        zsync();
+        if (!sm.more[p & 1]) break;
+    }
+}
+
+// Wave 0: phase B for the group (lane = block), tables and bitstreams in LDS.
+__device__ __forceinline__ void zdecode(SeqSmem &sm, int gn, uint32_t &r0, uint32_t &r1, uint32_t &r2,
+                                        uint32_t &brep) {
+    const int l = lane_id();
+    const bool mine = l < gn;
+    const GBlk d = sm.g[mine ? l : 0];
+    const ZGeo g = zgeo(d);
+    const uint8_t *ring = sm.bring[l & (ZNB - 1)];
+    const uint16_t *tl = sm.arena[l & (ZNB - 1)], *to = tl + 512, *tm = tl + 768;
+    const int32_t all = d.al & 0xFF, alof = (d.al >> 8) & 0xFF, alml = (d.al >> 16) & 0xFF;
+    const int32_t m8 = 8 * g.m;
+    g_u4 *it = d.ib + d.item;
+    zsync();  // the mover has staged the tables and prefilled the rings
+    [[maybe_unused]] uint64_t zt = ZP_NOW();
+    bool run = false;
+    int32_t left = 0, i = 0;
+    uint32_t sll = 0, sof = 0, sml = 0;
+    if (mine) {
+        if (d.nseq == 0) {
+            it[1] = make_uint4(0, 0, 0, IT_BREP);
+            it[2] = make_uint4(0, 0, 0, IT_BEND);
+            brep = 1;
+        } else {
+            const uint32_t last = d.bsz > 0 ? ring[(g.top - 1) & (ZRB2 - 1)] : 0u;
+            if (last == 0) {
+                it[1] = make_uint4(0, 0, (uint32_t)E_CORRUPT, IT_ERR);
+            } else {
+                brep = 1;
+                run = true;
+                left = 8 * (g.top - 1) + (31 - __builtin_clz(last));
+            }
+        }
+    }
+    if (run) {
+        uint64_t hi;
+        uint32_t lo;
+        zw_fill(ring, left, hi, lo);
+        int32_t c = 0;
+        sll = zw_get(hi, c, all);
+        sof = zw_get(hi, c, alof);
+        sml = zw_get(hi, c, alml);
+        left -= c;
+    }
+    const uint32_t szl = 1u << all, szo = 1u << alof, szm = 1u << alml;
+    for (int p = 0;; ++p) {
+#if JFS_ZUNROLL
+#pragma unroll
+#endif
+        for (int k = 0; k < ZK2; ++k) {
+            if (run) {
+                if (left < m8) {  // overflow
+                    it[2 + i] = make_uint4(0, 0, (uint32_t)E_CORRUPT, IT_ERR);
+                    run = false;
+                } else {
+                    const uint32_t cl = tl[sll], co = to[sof], cm = tm[sml];
+                    uint64_t hi;
+                    uint32_t lo;
+                    zw_fill(ring, left, hi, lo);
+                    const uint32_t lv = sm.lut_ll[cl & 63], mv = sm.lut_ml[cm & 63], ofc = co & 63;
+                    int32_t c = 0;
+                    const uint32_t ofv = (1u << ofc) + zw_get(hi, c, ofc);
+                    const uint32_t ml = (mv & 0xFFFFFFu) + zw_get(hi, c, mv >> 24);
+                    const uint32_t ll = (lv & 0xFFFFFFu) + zw_get(hi, c, lv >> 24);
+                    // repeat offsets (RFC 8878 3.1.2.5), branch-free: kk 0..2 = rep
+                    // 1..3 (shifted when ll == 0), 3 = rep1 - 1, 4 = a new offset
+#if JFS_ZREP_BR
+                    uint32_t off;
+                    if (ofv > 3) {
+                        off = ofv - 3;
+                        r2 = r1; r1 = r0; r0 = off;
+                    } else {
+                        const uint32_t kk = ofv - 1 + (ll == 0 ? 1u : 0u);
+                        if (kk == 0) {
+                            off = r0;
+                        } else {
+                            const uint32_t t = kk == 1 ? r1 : kk == 2 ? r2 : rep_dec(r0);
+                            if (kk != 1) r2 = r1;
+                            r1 = r0;
+                            r0 = t;
+                            off = t;
+                        }
+                    }
+#else
+                    const uint32_t kk = ofv > 3 ? 4u : ofv - 1 + (ll == 0 ? 1u : 0u);
+                    const uint32_t rd0 = (r0 & SYMB) ? r0 + 1 : (r0 - 1 == 0 ? 1u : r0 - 1);
+                    const uint32_t off = kk == 0 ? r0 : kk == 1 ? r1 : kk == 2 ? r2 : kk == 3 ? rd0 : ofv - 3;
+                    r2 = kk >= 2 ? r1 : r2;
+                    r1 = kk >= 1 ? r0 : r1;
+                    r0 = off;
+#endif
+                    if (i + 1 < d.nseq) {
+                        const uint64_t h2 = zw_shift(hi, lo, c);
+                        int32_t c2 = 0;
+                        const uint32_t nsl = cl >> 6, nso = co >> 6, nsm = cm >> 6;
+                        const uint32_t nbl = all - (31 - __builtin_clz(nsl));
+                        const uint32_t nbm = alml - (31 - __builtin_clz(nsm));
+                        const uint32_t nbo = alof - (31 - __builtin_clz(nso));
+                        sll = ((nsl << nbl) - szl) + zw_get(h2, c2, nbl);
+                        sml = ((nsm << nbm) - szm) + zw_get(h2, c2, nbm);
+                        sof = ((nso << nbo) - szo) + zw_get(h2, c2, nbo);
+                        c += c2;
+                    }
+                    left -= c;
+                    it[2 + i] = make_uint4(ll, ml, off, IT_SEQ);
+                    if (i + 1 == d.nseq) {
+                        it[3 + i] = left == m8 ? make_uint4(0, 0, 0, IT_BEND) : make_uint4(0, 0, (uint32_t)E_CORRUPT, IT_ERR);
+                        run = false;
+                    }
+                    ++i;
+                }
+            }
+        }
+        if (l < ZNB) sm.pos[p & 1][l] = left;
+        const bool any = __ballot(run) != 0;
+        if (l == 0) sm.more[p & 1] = any ? 1 : 0;
+        [[maybe_unused]] const uint64_t tw = ZP_NOW();
+        zsync();
+        ZS_ADD(4, ZP_NOW() - tw);
+        if (!any) break;
+    }
+    { const uint64_t t = ZP_NOW(); ZS_ADD(2, t - zt); }
+}
+
+// phases B (both waves) and C (wave 0) for the collected group
+__device__ __forceinline__ void seq_group2(SeqSmem &sm, int gn, uint32_t *e0, uint32_t *e1, uint32_t *e2) {
+    const int l = lane_id();
+    ZS_ADD(5, 1);
+    uint32_t r0 = SYMB | (0u << 29), r1 = SYMB | (1u << 29), r2 = SYMB | (2u << 29);
+    uint32_t brep = 0;
+    zdecode(sm, gn, r0, r1, r2, brep);
+    [[maybe_unused]] uint64_t zt = ZP_NOW();
+    for (int gi = 0; gi < gn; gi++) {
+        const uint32_t al = sm.g[gi].al, item = sm.g[gi].item;
+        g_u4 *ib = sm.g[gi].ib;
+        if (al >> 24) { *e0 = 1; *e1 = 4; *e2 = 8; }
+        const uint32_t x0 = readlane(r0, gi), x1 = readlane(r1, gi), x2 = readlane(r2, gi);
+        if (readlane(brep, gi) && l == 0) ib[item + 1] = make_uint4(*e0, *e1, *e2, IT_BREP);
+        const uint32_t n0 = rep_res(x0, *e0, *e1, *e2), n1 = rep_res(x1, *e0, *e1, *e2), n2 = rep_res(x2, *e0, *e1, *e2);
+        *e0 = n0; *e1 = n1; *e2 = n2;
+    }
+    __builtin_amdgcn_wave_barrier();
+    { const uint64_t t = ZP_NOW(); ZS_ADD(3, t - zt); }
+}
+#endif  // JFS_ZSEQ_V2
+
+#if JFS_ZSEQ_V2
+constexpr int ZSEQ_T = 128;
+constexpr int ZGROUP = ZNB;
+#else
+constexpr int ZSEQ_T = 64;
+constexpr int ZGROUP = 64;
+#endif
+__global__ __launch_bounds__(ZSEQ_T) void zseq_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
+                                                      ZInfo *__restrict__ info, uint16_t *__restrict__ tabs_all,
+                                                      uint4 *__restrict__ items_all, int strict_reserved) {
     __shared__ SeqSmem sm;
     const int l = lane_id();
     for (int i = l; i < 36; i += 64) sm.lut_ll[i] = LL_BASE[i] | ((uint32_t)LL_BITS[i] << 24);
     for (int i = l; i < 53; i += 64) sm.lut_ml[i] = ML_BASE[i] | ((uint32_t)ML_BITS[i] << 24);
+#if JFS_ZSEQ_V2
+    if (threadIdx.x >= 64) {  // the mover wave: one group per command from wave 0
+        for (;;) {
+            zsync();
+            const int gn = sm.cmd;
+            if (gn == 0) break;
+            zmover(sm, gn, (const gc_u16 *)tabs_all);
+        }
+        return;
+    }
+    auto flush = [&](int gn, uint32_t *e0, uint32_t *e1, uint32_t *e2) {
+        wait_vm();  // phase A's table stores are complete before the mover stages them
+        if (l == 0) sm.cmd = gn;
+        zsync();
+        seq_group2(sm, gn, e0, e1, e2);
+    };
+#else
+    auto flush = [&](int gn, uint32_t *e0, uint32_t *e1, uint32_t *e2) {
+        seq_group(sm, gn, (const gc_u16 *)tabs_all, e0, e1, e2);
+    };
+#endif
     int gn = 0;
     uint32_t e0 = 1, e1 = 4, e2 = 8;  // repeat offsets carried through phase C (reset at each frame)
     [[maybe_unused]] uint64_t za = ZP_NOW();
@@ -1620,9 +2003,9 @@ __global__ __launch_bounds__(64) void zseq_kernel(const jfs_dev_block *__restric
             first = 0;
             cur = slot + 3 + (uint32_t)nseq;
             gn++;
-            if (gn == 64) {
+            if (gn == ZGROUP) {
                 ZS_ADD(0, ZP_NOW() - za);
-                seq_group(sm, gn, (const gc_u16 *)tabs_all, &e0, &e1, &e2);
+                flush(gn, &e0, &e1, &e2);
                 za = ZP_NOW();
                 gn = 0;
             }
@@ -1630,7 +2013,11 @@ __global__ __launch_bounds__(64) void zseq_kernel(const jfs_dev_block *__restric
         if (l == 0) zi.n_items = bug ? 0xFFFFFFFFu : cur;
     }
     ZS_ADD(0, ZP_NOW() - za);
-    if (gn) seq_group(sm, gn, (const gc_u16 *)tabs_all, &e0, &e1, &e2);
+    if (gn) flush(gn, &e0, &e1, &e2);
+#if JFS_ZSEQ_V2
+    if (l == 0) sm.cmd = 0;
+    zsync();  // releases the mover
+#endif
     wait_vm();
 }
 
@@ -2186,7 +2573,7 @@ int launch_entropy_exec(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret,
     using namespace jfs::zstdd;
     hipLaunchKernelGGL(zlit_kernel, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, d_info, d_lit);
     if (hipGetLastError() != hipSuccess) return -1;
-    hipLaunchKernelGGL(zseq_kernel, dim3((nblk + ZSEQ_INPUTS - 1) / ZSEQ_INPUTS), dim3(64), 0, stream, d_blocks, nblk,
+    hipLaunchKernelGGL(zseq_kernel, dim3((nblk + ZSEQ_INPUTS - 1) / ZSEQ_INPUTS), dim3(ZSEQ_T), 0, stream, d_blocks, nblk,
                        d_info, d_tabs, d_items, g_strict_reserved);
     if (hipGetLastError() != hipSuccess) return -1;
     hipLaunchKernelGGL(zexec_kernel, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, d_info, d_lit, d_items, d_ret);

@@ -19,5 +19,5 @@ names = ["phaseA walk+tables", "table staging", "phaseB decode", "phaseC", "sub-
 tot = sum(buf[:4])
 for i, nm in enumerate(names[:4]):
     print(f"{nm:20s} {buf[i] / tot * 100:6.2f}%  {buf[i] / n / 1e6:8.3f} Mcyc/frame")
-print(f"sub-groups {buf[4]}  groups {buf[5]}  frames {n}")
+print(f"decoder barrier waits {buf[4] / n / 1e6:8.3f} Mcyc/frame ({buf[4] / max(buf[2], 1) * 100:.1f}% of phase B)  groups {buf[5]}  frames {n}")
 print("ok" if b.verify() else "MISMATCH")
