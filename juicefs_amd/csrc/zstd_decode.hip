@@ -62,7 +62,7 @@ enum { FE_FCS = 1, FE_CHECK = 2, FE_MISSING = 4 };
 constexpr uint32_t ZSTD_MAGIC = 0xFD2FB528u;
 constexpr int32_t BLOCK_MAX = 128 << 10;
 
-// per-input bookkeeping (32 bytes)
+// per-input bookkeeping
 struct ZInfo {
     uint64_t item_off;      // first item (host scan)
     uint64_t lit_off;       // first literal byte (host scan)
@@ -73,8 +73,21 @@ struct ZInfo {
     uint32_t lit_err_blk;   // zlit: ordinal of the block whose literals failed
     int32_t lit_err_code;
     uint32_t ovf;           // zplan: the scratch cannot hold this input (ret = E_SCRATCH)
+    uint32_t n_sblk;        // zseqa: compressed blocks described (ZDesc after each table area)
 };
 constexpr int TAB_CELLS = 1280;  // u16 FSE cells per compressed block: LL 512, OF 256, ML 512
+constexpr int TAB_STRIDE = TAB_CELLS + 32;  // table area stride: the cells, then the block's ZDesc (64 B)
+
+// a compressed block's sequence section, written by zseqa after its tables
+struct ZDesc {
+    uint64_t bs;             // sequence bitstream (absolute address)
+    int32_t bsz, nseq;
+    uint32_t item;           // BSTART item index (relative to the input)
+    uint32_t tll, tof, tml;  // table cells relative to the input's first cell
+    uint32_t al;             // al_ll | al_of << 8 | al_ml << 16 | frame-first << 24
+    uint32_t rsv;
+};
+static_assert(sizeof(ZDesc) <= (TAB_STRIDE - TAB_CELLS) * 2, "ZDesc fits after the cells");
 
 __constant__ uint32_t LL_BASE[36] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,   10,  11,  12,   13,   14,   15,    16,    18,
                                      20, 22, 24, 28, 32, 40, 48, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536};
@@ -696,7 +709,7 @@ __global__ __launch_bounds__(PLAN_T) void zplan_kernel(ZInfo *__restrict__ info,
     for (int i = b0; i < b1; i++) {
         a += info[i].n_items;
         c += (info[i].lit_bytes + 15u) & ~15u;
-        d += (uint64_t)info[i].n_cblk * TAB_CELLS;
+        d += (uint64_t)info[i].n_cblk * TAB_STRIDE;
     }
     sh[0][t] = a;
     sh[1][t] = c;
@@ -721,7 +734,7 @@ __global__ __launch_bounds__(PLAN_T) void zplan_kernel(ZInfo *__restrict__ info,
         z.lit_err_code = 0;
         oi += z.n_items;
         ol += (z.lit_bytes + 15u) & ~15u;
-        ot += (uint64_t)z.n_cblk * TAB_CELLS;
+        ot += (uint64_t)z.n_cblk * TAB_STRIDE;
         z.ovf = (oi + 64 > cap_items || ol + 4096 + 64 > cap_lits || ot + 64 > cap_tabs) ? 1u : 0u;
     }
     if (t == PLAN_T - 1) {
@@ -1054,11 +1067,12 @@ constexpr int ZRB = JFS_ZSEQ_ARENA > 0 ? 256 : 128;
 static_assert(ZK * 12 + 24 <= ZRB - 16 && ZRB / 16 - 1 <= 15 + 0, "a period's bits must stay resident");
 static_assert(ZARENA == 0 || ZARENA >= 1280 + 8, "one block's largest tables must fit");
 // Round 3 (default): a workgroup of two waves.  Wave 0 walks the headers and
-// builds the tables (phase A), then decodes a group of ZNB blocks (one lane
-// each) with every table cell and bitstream byte read from LDS — it never
-// waits on HBM; its item stores are fire-and-forget.  Wave 1 (the mover)
-// stages the group's tables into LDS and keeps each lane's bitstream ring
-// filled ahead of the decoder, one barrier per period of ZK2 sequences.
+// builds each block's FSE tables straight into the group's LDS arena (phase
+// A), then decodes the group's ZNB blocks (one lane each) with every table
+// cell and bitstream byte read from LDS — it never waits on HBM; its item
+// stores are fire-and-forget.  Wave 1 (the mover) keeps each lane's
+// bitstream ring filled ahead of the decoder, one barrier per period of ZK2
+// sequences.
 #ifndef JFS_ZSEQ_V2
 #define JFS_ZSEQ_V2 1
 #endif
@@ -1085,16 +1099,14 @@ constexpr int ZAHEAD = ZMD == 2 ? 27 : 24;  // ring blocks the mover keeps below
 constexpr int ZPB = (ZK2 * 89 + 127) / 128;
 static_assert((ZMD + 1) * ZPB + 7 <= ZAHEAD && ZAHEAD <= ZRB2 / 16 - 2 && ZPB + 2 <= 8, "ring budget");
 #if JFS_ZSEQ_V2
-struct SeqSmem {
-    union {
-        struct {  // phase A scratch (wave 0 only, between groups)
-            uint8_t stage[256];
-            int16_t norm[64];
-            uint8_t symat[512], mark[512], ksym[512];
-        };
-        alignas(16) uint8_t bring[ZNB][ZRB2];  // phase B: per-lane bitstream rings
-    };
-    alignas(16) uint16_t arena[ZNB][TAB_CELLS];  // phase B: the group's tables (LL 0, OF 512, ML 768)
+struct ASmem {  // zseqa: table-build scratch
+    uint8_t stage[256];
+    int16_t norm[64];
+    uint8_t symat[512], mark[512], ksym[512];
+};
+struct SeqSmem {  // zseqb
+    alignas(16) uint8_t bring[ZNB][ZRB2];        // per-lane bitstream rings
+    alignas(16) uint16_t arena[ZNB][TAB_CELLS];  // the group's tables (LL 0, OF 512, ML 768)
     uint32_t lut_ll[36], lut_ml[53];
     GBlk g[ZNB];
     int32_t pos[2][ZNB];  // decoder bit positions published at each period's barrier
@@ -1123,7 +1135,8 @@ struct SeqSmem {
 #endif
 
 // u16 cell = sym | ns << 6  (nb = al - highbit(ns), next-state base = (ns << nb) - 2^al)
-__device__ __forceinline__ void build_seq_fse_g(g_u16 *t, const int16_t *norm, int32_t maxsym, int32_t al,
+template <class P>
+__device__ __forceinline__ void build_seq_fse_g(P t, const int16_t *norm, int32_t maxsym, int32_t al,
                                                 uint8_t *mark, uint8_t *ksym, uint8_t *symat) {
     const int l = lane_id();
     const int32_t size = 1 << al, mask = size - 1, step = (size >> 1) + (size >> 3) + 3;
@@ -1179,7 +1192,8 @@ __device__ __forceinline__ void build_seq_fse_g(g_u16 *t, const int16_t *norm, i
 }
 
 // one field's table; returns bytes used or -1.  cur/al/have: the field's state.
-__device__ __forceinline__ int32_t seq_table_g(SeqSmem &sm, g_u16 *tabs, uint32_t area, uint32_t *cur, int32_t *al,
+template <class SM, class P>
+__device__ __forceinline__ int32_t seq_table_g(SM &sm, P tabs, uint32_t area, uint32_t *cur, int32_t *al,
                                                int32_t *have, int32_t mode, const gc_u8 *s, int32_t p, int32_t n,
                                                int which) {
     const int16_t *def = which == 0 ? LL_DEF : which == 1 ? OF_DEF : ML_DEF;
@@ -1637,8 +1651,9 @@ __device__ __forceinline__ uint64_t zw_shift(uint64_t hi, uint32_t lo, int32_t c
     return c ? (hi << c) | (((uint64_t)lo << 32) >> (64 - c)) : hi;
 }
 
-// Wave 1: stage the group's tables into the arena, prefill the rings, then
-// one refill round per period until the decoder reports no lane running.
+// Wave 1: stage the group's tables (built in HBM by zseqa) into the arena,
+// prefill the rings, then one refill round per period until the decoder
+// reports no lane running.
 __device__ __forceinline__ void zmover(SeqSmem &sm, int gn, const gc_u16 *tabs) {
     const int l = lane_id();
     [[maybe_unused]] uint64_t zt = ZP_NOW();
@@ -1881,20 +1896,121 @@ __device__ __forceinline__ void seq_group2(SeqSmem &sm, int gn, uint32_t *e0, ui
 #endif  // JFS_ZSEQ_V2
 
 #if JFS_ZSEQ_V2
-constexpr int ZSEQ_T = 128;
-constexpr int ZGROUP = ZNB;
-#else
-constexpr int ZSEQ_T = 64;
-constexpr int ZGROUP = 64;
-#endif
-__global__ __launch_bounds__(ZSEQ_T) void zseq_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
+// zseqa (phase A): one wave per input walks the headers, builds each
+// compressed block's FSE tables into its HBM table area and writes the
+// block's ZDesc after them; zseqb decodes the sequences.
+__global__ __launch_bounds__(64) void zseqa_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
                                                       ZInfo *__restrict__ info, uint16_t *__restrict__ tabs_all,
                                                       uint4 *__restrict__ items_all, int strict_reserved) {
+    __shared__ ASmem sm;
+    const int l = lane_id();
+    [[maybe_unused]] uint64_t za = ZP_NOW();
+    {
+        const int bi = blockIdx.x;
+        if (bi >= nblk) return;
+        const jfs_dev_block b = blocks[bi];
+        ZInfo &zi = info[bi];
+        if (zi.ovf) return;
+        const gc_u8 *s = (const gc_u8 *)b.src;
+        g_u16 *tabs = (g_u16 *)tabs_all + zi.tab_off;
+        g_u4 *items = (g_u4 *)items_all + zi.item_off;
+        Walk w;
+        walk_init(w, s, b.src_len, b.dst_cap);
+        const uint32_t cap_items = zi.n_items, cap_cblk = zi.n_cblk;
+        uint32_t cur = 0, cblk = 0, nd = 0;  // next item slot, next table area, descriptors
+        int first = 0, bug = 0;
+        uint32_t t_ll = 0, t_of = 0, t_ml = 0;
+        int32_t al_ll = 0, al_of = 0, al_ml = 0, hv_ll = 0, hv_of = 0, hv_ml = 0;
+        auto put = [&](uint32_t x, uint32_t y, uint32_t z, uint32_t kind) {
+            if (cur >= cap_items) { bug = 1; return; }
+            if (l == 0) items[cur] = make_uint4(x, y, z, kind);
+            cur++;
+        };
+        for (;;) {
+            int32_t err = 0;
+            uint32_t fl = 0, chk = 0;
+            int ev = walk_next(w, &err, &fl, &chk);
+            if (ev == EV_DONE) break;
+            if (ev == EV_ERROR) { put(0, 0, (uint32_t)err, IT_ERR); break; }
+            if (ev == EV_FSTART) {
+                hv_ll = hv_of = hv_ml = 0;
+                first = 1;
+                put(0, 0, 0, IT_FSTART);
+                continue;
+            }
+            if (ev == EV_FEND) {
+                put((uint32_t)w.fcs, (uint32_t)(w.fcs >> 32), chk, IT_FEND | (fl << 8));
+                if (fl & FE_MISSING) break;
+                continue;
+            }
+            const uint32_t ord = w.ordinal - 1;
+            if (w.btype != 2) {
+                put(ord, (uint32_t)w.bsize, 0, IT_BSTART);
+                put((uint32_t)w.bsize, 0, 0, IT_SEQ);
+                put(0, 0, 0, IT_BEND);
+                w.lb += w.bsize;
+                continue;
+            }
+            LitHdr h;
+            int32_t e = lit_header(s, w.bpos, w.bsize, h);
+            const uint32_t slot = cur;
+            put(ord, e ? 0u : (uint32_t)h.regen, 0, IT_BSTART);
+            if (e) { put(0, 0, (uint32_t)e, IT_ERR); break; }
+            const int32_t end = w.bpos + w.bsize;
+            int32_t ip = w.bpos + h.sec;
+            int32_t nseq = 0, used = 0;
+            e = nbseq_header(s, ip, end, &nseq, &used);
+            if (e) { put(0, 0, (uint32_t)e, IT_ERR); break; }
+            ip += used;
+            w.lb += (int64_t)h.regen + 3 * (int64_t)nseq;
+            if (cblk >= cap_cblk || slot + 3 + (uint32_t)nseq > cap_items) { bug = 1; break; }
+            const uint32_t area = cblk * TAB_STRIDE;
+            cblk++;
+            if (nseq > 0) {
+                if (ip + 1 > end) { put(0, 0, (uint32_t)E_SRCSIZE, IT_ERR); break; }
+                uint32_t modes = rd8(s, ip++);
+                if ((modes & 3) && strict_reserved) { put(0, 0, (uint32_t)E_CORRUPT, IT_ERR); break; }
+                int32_t c = seq_table_g(sm, tabs, area, &t_ll, &al_ll, &hv_ll, modes >> 6, s, ip, end - ip, 0);
+                if (c >= 0) { ip += c; c = seq_table_g(sm, tabs, area + 512, &t_of, &al_of, &hv_of, (modes >> 4) & 3, s, ip, end - ip, 1); }
+                if (c >= 0) { ip += c; c = seq_table_g(sm, tabs, area + 768, &t_ml, &al_ml, &hv_ml, (modes >> 2) & 3, s, ip, end - ip, 2); }
+                if (c < 0) { put(0, 0, (uint32_t)E_CORRUPT, IT_ERR); break; }
+                ip += c;
+            }
+            if (l == 0) {
+                ZDesc d;
+                d.bs = (uint64_t)(uintptr_t)(s + ip);
+                d.bsz = end - ip;
+                d.nseq = nseq;
+                d.item = slot;
+                d.tll = t_ll; d.tof = t_of; d.tml = t_ml;
+                d.al = (uint32_t)al_ll | ((uint32_t)al_of << 8) | ((uint32_t)al_ml << 16) | ((uint32_t)first << 24);
+                d.rsv = 0;
+                *(JFS_GLOBAL ZDesc *)(tabs + area + TAB_CELLS) = d;
+            }
+            first = 0;
+            cur = slot + 3 + (uint32_t)nseq;
+            nd++;
+        }
+        if (l == 0) {
+            zi.n_items = bug ? 0xFFFFFFFFu : cur;
+            zi.n_sblk = nd;
+        }
+    }
+    ZS_ADD(0, ZP_NOW() - za);
+}
+
+
+// zseqb (phases B and C): wave 0 gathers ZNB blocks' descriptors at a time
+// (in stream order over the workgroup's inputs), decodes their sequences
+// with wave 1 keeping the tables and bitstreams in LDS, then resolves the
+// symbolic repeat offsets in block order.
+__global__ __launch_bounds__(128) void zseqb_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
+                                                    ZInfo *__restrict__ info, uint16_t *__restrict__ tabs_all,
+                                                    uint4 *__restrict__ items_all) {
     __shared__ SeqSmem sm;
     const int l = lane_id();
     for (int i = l; i < 36; i += 64) sm.lut_ll[i] = LL_BASE[i] | ((uint32_t)LL_BITS[i] << 24);
     for (int i = l; i < 53; i += 64) sm.lut_ml[i] = ML_BASE[i] | ((uint32_t)ML_BITS[i] << 24);
-#if JFS_ZSEQ_V2
     if (threadIdx.x >= 64) {  // the mover wave: one group per command from wave 0
         for (;;) {
             zsync();
@@ -1904,17 +2020,59 @@ __global__ __launch_bounds__(ZSEQ_T) void zseq_kernel(const jfs_dev_block *__res
         }
         return;
     }
-    auto flush = [&](int gn, uint32_t *e0, uint32_t *e1, uint32_t *e2) {
-        wait_vm();  // phase A's table stores are complete before the mover stages them
+    int gn = 0;
+    uint32_t e0 = 1, e1 = 4, e2 = 8;  // repeat offsets carried through phase C (reset at each frame)
+    for (int f = 0; f < ZSEQ_INPUTS; ++f) {
+        const int bi = blockIdx.x * ZSEQ_INPUTS + f;
+        if (bi >= nblk) break;
+        const ZInfo zi = info[bi];
+        if (zi.ovf || zi.n_items == 0xFFFFFFFFu) continue;
+        const gc_u16 *tabs = (const gc_u16 *)tabs_all + zi.tab_off;
+        g_u4 *items = (g_u4 *)items_all + zi.item_off;
+        for (uint32_t j = 0; j < zi.n_sblk;) {
+            const uint32_t take = umin32((uint32_t)(ZNB - gn), zi.n_sblk - j);
+            if ((uint32_t)l < take) {
+                const ZDesc d = *(const JFS_GLOBAL ZDesc *)(tabs + (uint64_t)(j + l) * TAB_STRIDE + TAB_CELLS);
+                GBlk &g = sm.g[gn + l];
+                g.bs = (const gc_u8 *)(uintptr_t)d.bs;
+                g.in = g.bs;
+                g.ib = items;
+                g.bsz = d.bsz;
+                g.nseq = d.nseq;
+                g.item = d.item;
+                g.tll = zi.tab_off + d.tll; g.tof = zi.tab_off + d.tof; g.tml = zi.tab_off + d.tml;
+                g.al = d.al;
+            }
+            __builtin_amdgcn_wave_barrier();
+            gn += (int)take;
+            j += take;
+            if (gn == ZNB) {
+                if (l == 0) sm.cmd = gn;
+                zsync();
+                seq_group2(sm, gn, &e0, &e1, &e2);
+                gn = 0;
+            }
+        }
+    }
+    if (gn) {
         if (l == 0) sm.cmd = gn;
         zsync();
-        seq_group2(sm, gn, e0, e1, e2);
-    };
+        seq_group2(sm, gn, &e0, &e1, &e2);
+    }
+    if (l == 0) sm.cmd = 0;
+    zsync();  // releases the mover
+}
 #else
+__global__ __launch_bounds__(64) void zseq_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
+                                                      ZInfo *__restrict__ info, uint16_t *__restrict__ tabs_all,
+                                                      uint4 *__restrict__ items_all, int strict_reserved) {
+    __shared__ SeqSmem sm;
+    const int l = lane_id();
+    for (int i = l; i < 36; i += 64) sm.lut_ll[i] = LL_BASE[i] | ((uint32_t)LL_BITS[i] << 24);
+    for (int i = l; i < 53; i += 64) sm.lut_ml[i] = ML_BASE[i] | ((uint32_t)ML_BITS[i] << 24);
     auto flush = [&](int gn, uint32_t *e0, uint32_t *e1, uint32_t *e2) {
         seq_group(sm, gn, (const gc_u16 *)tabs_all, e0, e1, e2);
     };
-#endif
     int gn = 0;
     uint32_t e0 = 1, e1 = 4, e2 = 8;  // repeat offsets carried through phase C (reset at each frame)
     [[maybe_unused]] uint64_t za = ZP_NOW();
@@ -1977,7 +2135,7 @@ __global__ __launch_bounds__(ZSEQ_T) void zseq_kernel(const jfs_dev_block *__res
             ip += used;
             w.lb += (int64_t)h.regen + 3 * (int64_t)nseq;
             if (cblk >= cap_cblk || slot + 3 + (uint32_t)nseq > cap_items) { bug = 1; break; }
-            const uint32_t area = cblk * TAB_CELLS;
+            const uint32_t area = cblk * TAB_STRIDE;
             cblk++;
             if (nseq > 0) {
                 if (ip + 1 > end) { put(0, 0, (uint32_t)E_SRCSIZE, IT_ERR); break; }
@@ -2003,7 +2161,7 @@ __global__ __launch_bounds__(ZSEQ_T) void zseq_kernel(const jfs_dev_block *__res
             first = 0;
             cur = slot + 3 + (uint32_t)nseq;
             gn++;
-            if (gn == ZGROUP) {
+            if (gn == 64) {
                 ZS_ADD(0, ZP_NOW() - za);
                 flush(gn, &e0, &e1, &e2);
                 za = ZP_NOW();
@@ -2014,12 +2172,10 @@ __global__ __launch_bounds__(ZSEQ_T) void zseq_kernel(const jfs_dev_block *__res
     }
     ZS_ADD(0, ZP_NOW() - za);
     if (gn) flush(gn, &e0, &e1, &e2);
-#if JFS_ZSEQ_V2
-    if (l == 0) sm.cmd = 0;
-    zsync();  // releases the mover
-#endif
     wait_vm();
 }
+
+#endif  // JFS_ZSEQ_V2
 
 // ---------------------------------------------------------------------------
 // kernel 3: execute items
@@ -2573,8 +2729,16 @@ int launch_entropy_exec(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret,
     using namespace jfs::zstdd;
     hipLaunchKernelGGL(zlit_kernel, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, d_info, d_lit);
     if (hipGetLastError() != hipSuccess) return -1;
-    hipLaunchKernelGGL(zseq_kernel, dim3((nblk + ZSEQ_INPUTS - 1) / ZSEQ_INPUTS), dim3(ZSEQ_T), 0, stream, d_blocks, nblk,
+#if JFS_ZSEQ_V2
+    hipLaunchKernelGGL(zseqa_kernel, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, d_info, d_tabs, d_items,
+                       g_strict_reserved);
+    if (hipGetLastError() != hipSuccess) return -1;
+    hipLaunchKernelGGL(zseqb_kernel, dim3((nblk + ZSEQ_INPUTS - 1) / ZSEQ_INPUTS), dim3(128), 0, stream, d_blocks, nblk,
+                       d_info, d_tabs, d_items);
+#else
+    hipLaunchKernelGGL(zseq_kernel, dim3((nblk + ZSEQ_INPUTS - 1) / ZSEQ_INPUTS), dim3(64), 0, stream, d_blocks, nblk,
                        d_info, d_tabs, d_items, g_strict_reserved);
+#endif
     if (hipGetLastError() != hipSuccess) return -1;
     hipLaunchKernelGGL(zexec_kernel, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, d_info, d_lit, d_items, d_ret);
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -2664,7 +2828,7 @@ extern "C" void jfs_zstd_plan_host(const uint8_t *const *srcs, const int32_t *le
         z.ovf = 0;
         oi += z.n_items;
         ol += (z.lit_bytes + 15u) & ~15u;
-        ot += (uint64_t)z.n_cblk * TAB_CELLS;
+        ot += (uint64_t)z.n_cblk * TAB_STRIDE;
     }
     totals[0] = oi + 64;
     totals[1] = ol + 4096 + 64;
