@@ -1082,7 +1082,14 @@ static_assert(ZARENA == 0 || ZARENA >= 1280 + 8, "one block's largest tables mus
 #ifndef JFS_ZUNROLL
 #define JFS_ZUNROLL 0
 #endif
-constexpr int ZNB = 16;     // blocks per group = decoder lanes (3 workgroups per CU by LDS)
+#ifndef JFS_ZNB
+#define JFS_ZNB 16
+#endif
+// blocks per group = decoder lanes: 16 fit three workgroups per CU in LDS
+// (12 fit four, one decoder wave per SIMD, but measured slower: 161-171 vs
+// 152 ms on configs[3])
+constexpr int ZNB = JFS_ZNB;
+constexpr int ZMQ = 64 / ZNB < 4 ? 64 / ZNB : 4;  // mover lanes per block
 constexpr int ZK2 = 8;      // sequences per period
 constexpr int ZRB2 = 512;   // bitstream ring bytes per lane (32 blocks of 16 B)
 #ifndef JFS_ZMOVE_D
@@ -1113,7 +1120,8 @@ struct SeqSmem {  // zseqb
     int32_t more[2];      // any lane still decoding (per period parity)
     int32_t cmd;          // wave 0 -> wave 1: blocks in the group, 0 = done
 };
-static_assert(sizeof(SeqSmem) * 3 <= 160 * 1024, "three sequence workgroups per CU");
+static_assert(sizeof(SeqSmem) * (ZNB <= 12 ? 4 : 3) <= 160 * 1024, "sequence workgroups per CU (one decoder wave per SIMD)");
+static_assert(ZMQ == 4, "the mover serves each block with four lanes (stride-4 block loads)");
 #else
 struct SeqSmem {
     uint8_t stage[256];
@@ -1685,10 +1693,10 @@ __device__ __forceinline__ void zmover(SeqSmem &sm, int gn, const gc_u16 *tabs) 
         }
     }
     // lanes j, j + 16, j + 32, j + 48 serve block j (q = lane >> 4)
-    const int j = l & (ZNB - 1), q = l >> 4;
-    const bool on = j < gn && sm.g[j < gn ? j : 0].nseq > 0 && sm.g[j < gn ? j : 0].bsz > 0;
+    const int q = l / ZNB, j = l - q * ZNB;  // lanes j + ZNB * q (q < ZMQ) serve block j
+    const bool on = q < ZMQ && j < gn && sm.g[j < gn ? j : 0].nseq > 0 && sm.g[j < gn ? j : 0].bsz > 0;
     const ZGeo g = zgeo(sm.g[j < gn ? j : 0]);
-    uint8_t *ring = sm.bring[j];
+    uint8_t *ring = sm.bring[q < ZMQ ? j : 0];
     // blocks below -3 are never read (a lane stops once its position is
     // below the stream start); blocks [-3, 0) are written as zeros
     constexpr int32_t KFLOOR = -3;
@@ -1757,8 +1765,8 @@ __device__ __forceinline__ void zdecode(SeqSmem &sm, int gn, uint32_t &r0, uint3
     const bool mine = l < gn;
     const GBlk d = sm.g[mine ? l : 0];
     const ZGeo g = zgeo(d);
-    const uint8_t *ring = sm.bring[l & (ZNB - 1)];
-    const uint16_t *tl = sm.arena[l & (ZNB - 1)], *to = tl + 512, *tm = tl + 768;
+    const uint8_t *ring = sm.bring[l < ZNB ? l : 0];
+    const uint16_t *tl = sm.arena[l < ZNB ? l : 0], *to = tl + 512, *tm = tl + 768;
     const int32_t all = d.al & 0xFF, alof = (d.al >> 8) & 0xFF, alml = (d.al >> 16) & 0xFF;
     const int32_t m8 = 8 * g.m;
     g_u4 *it = d.ib + d.item;
@@ -1832,6 +1840,18 @@ __device__ __forceinline__ void zdecode(SeqSmem &sm, int gn, uint32_t &r0, uint3
                             off = t;
                         }
                     }
+#elif JFS_ZREP_BR == 2
+                    // select by masks (no exec-mask branches)
+                    const uint32_t kk = ofv > 3 ? 4u : ofv - 1 + (ll == 0 ? 1u : 0u);
+                    const uint32_t rd0 = (r0 & SYMB) ? r0 + 1 : umax32(r0 - 1, 1u);
+                    const uint32_t m0 = 0u - (uint32_t)(kk == 0), m1 = 0u - (uint32_t)(kk == 1),
+                                   m2 = 0u - (uint32_t)(kk == 2), m3 = 0u - (uint32_t)(kk == 3),
+                                   m4 = 0u - (uint32_t)(kk == 4);
+                    const uint32_t off = (r0 & m0) | (r1 & m1) | (r2 & m2) | (rd0 & m3) | ((ofv - 3) & m4);
+                    const uint32_t ge2 = m2 | m3 | m4, ge1 = ge2 | m1;
+                    r2 = (r1 & ge2) | (r2 & ~ge2);
+                    r1 = (r0 & ge1) | (r1 & ~ge1);
+                    r0 = off;
 #else
                     const uint32_t kk = ofv > 3 ? 4u : ofv - 1 + (ll == 0 ? 1u : 0u);
                     const uint32_t rd0 = (r0 & SYMB) ? r0 + 1 : (r0 - 1 == 0 ? 1u : r0 - 1);
