@@ -1012,7 +1012,14 @@ __device__ __forceinline__ void lit_wave(LitSmem &sm, const jfs_dev_block &b, ZI
     }
 }
 
-__global__ __launch_bounds__(64) void zlit_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
+#ifndef JFS_ZLIT_WAVES
+#define JFS_ZLIT_WAVES 4  // <= 128 VGPRs: 16 one-wave workgroups per CU (LDS 10,124 B), no spills
+#endif
+__global__ __launch_bounds__(64)
+#if JFS_ZLIT_WAVES
+__attribute__((amdgpu_waves_per_eu(JFS_ZLIT_WAVES)))
+#endif
+void zlit_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
                                                   ZInfo *__restrict__ info, uint8_t *__restrict__ litbuf) {
     __shared__ LitSmem sm;
     const int bi = blockIdx.x;
@@ -1043,8 +1050,15 @@ struct GBlk {
 };
 // Inputs per sequence workgroup: a 4 MiB frame has 32 compressed blocks, so
 // two inputs fill the 64 lanes of phase B.
+#ifndef JFS_ZSEQ_V2
+#define JFS_ZSEQ_V2 1
+#endif
 #ifndef JFS_ZSEQ_INPUTS
+#if JFS_ZSEQ_V2
+#define JFS_ZSEQ_INPUTS 1  // zseqb: one input per workgroup packs the CUs better (123.3 vs 125.9 ms)
+#else
 #define JFS_ZSEQ_INPUTS 2
+#endif
 #endif
 constexpr int ZSEQ_INPUTS = JFS_ZSEQ_INPUTS;
 // Phase B decodes with the tables in LDS: the blocks of a group are taken in
@@ -1073,9 +1087,6 @@ static_assert(ZARENA == 0 || ZARENA >= 1280 + 8, "one block's largest tables mus
 // stores are fire-and-forget.  Wave 1 (the mover) keeps each lane's
 // bitstream ring filled ahead of the decoder, one barrier per period of ZK2
 // sequences.
-#ifndef JFS_ZSEQ_V2
-#define JFS_ZSEQ_V2 1
-#endif
 #ifndef JFS_ZREP_BR
 #define JFS_ZREP_BR 1  // branchy repeat-offset update: measured faster than the select chain (168.5 vs 189.5 ms)
 #endif
@@ -2215,12 +2226,19 @@ constexpr int LONGI = 1024;      // items longer than this are copied by the who
 #define JFS_ZEXEC_NEARSER 1  // near matches: one lane-parallel round, the rest by the whole wave in order
 #endif
 
+// 10,240 bytes: 16 workgroups (one per frame of a 4,096-frame launch) fit a
+// CU's 160 KiB, so a launch is one round (at 10,304 bytes it was 15 per CU and
+// the 256 leftover frames ran as a second round).  Over-reads past lw and
+// farbuf (dword/alignbyte tails) only fetch bytes that are never used.
 struct XSmem {
     alignas(16) uint8_t ring[R];
-    alignas(16) uint8_t lw[LW + 16];
-    alignas(16) uint8_t farbuf[64 * FB + 16];
-    uint64_t xxh[4];
+    alignas(16) uint8_t lw[LW];
+    union {
+        alignas(16) uint8_t farbuf[64 * FB];  // within a batch
+        uint64_t xxh[4];                      // frame checksum (between batches)
+    };
 };
+static_assert(sizeof(XSmem) * 16 <= 160 * 1024, "16 zexec workgroups per CU");
 
 struct X {
 #ifdef JFS_PROF
