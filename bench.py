@@ -747,7 +747,8 @@ def measured_traffic(path, nblk, U):
         return None, "traffic file is for another workload"
     if tj.get("kernel_src_sha256") != kernel_src_sha256():
         return None, "traffic file is stale (kernel sources changed since it was measured)"
-    return tj.get("hbm_bytes_per_launch"), f"rocprofv3 PMC at {tj.get('git_head')}"
+    stamp = tj.get("git_head") or f"kernel sources sha256 {tj.get('kernel_src_sha256', '')[:12]}"
+    return tj.get("hbm_bytes_per_launch"), f"rocprofv3 PMC FETCH_SIZE/WRITE_SIZE ({stamp})"
 
 
 def main():
