@@ -1123,7 +1123,7 @@ struct ASmem {  // zseqa: table-build scratch
     uint8_t symat[512], mark[512], ksym[512];
 };
 struct SeqSmem {  // zseqb
-    alignas(16) uint8_t bring[ZNB][ZRB2];        // per-lane bitstream rings
+    alignas(16) uint8_t bring[ZNB][ZRB2 + 16];   // per-lane bitstream rings (+ a mirror of block slot 0)
     alignas(16) uint16_t arena[ZNB][TAB_CELLS];  // the group's tables (LL 0, OF 512, ML 768)
     uint32_t lut_ll[36], lut_ml[53];
     GBlk g[ZNB];
@@ -1632,15 +1632,20 @@ __device__ __forceinline__ ZGeo zgeo(const GBlk &d) {
     g.lowk = -(int32_t)((((uintptr_t)g.b16) - (((uintptr_t)d.in) & ~(uintptr_t)15)) >> 4);
     return g;
 }
-__device__ __forceinline__ uint32_t zr_dw(const uint8_t *ring, int32_t q) {
-    return *(const uint32_t *)(ring + (q & (ZRB2 - 1)));
+// a ring slot write; slot 0 is mirrored after the ring so that a refill's
+// four dwords never wrap
+__device__ __forceinline__ void zr_put(uint8_t *ring, int32_t k, const uint4 &v) {
+    const int32_t sl = k & (ZRB2 / 16 - 1);
+    *(uint4 *)(ring + (sl << 4)) = v;
+    if (sl == 0) *(uint4 *)(ring + ZRB2) = v;
 }
 // Refill: bits [left - 96, left) from the ring (one round of four LDS dword
 // reads; the mover wrote zeros below the stream start, so bits there read as
 // zero, like lr_read).  hi = bits [left - 64, left), lo = bits [left - 96, left - 64).
 __device__ __forceinline__ void zw_fill(const uint8_t *ring, int32_t left, uint64_t &hi, uint32_t &lo) {
     const int32_t cb = ((left - 96) >> 5) << 2;  // 8 * cb in (left - 128, left - 96]
-    const uint32_t d0 = zr_dw(ring, cb), d1 = zr_dw(ring, cb + 4), d2 = zr_dw(ring, cb + 8), d3 = zr_dw(ring, cb + 12);
+    const uint32_t *w = (const uint32_t *)(ring + (cb & (ZRB2 - 1)));  // + 16 bytes: the mirror
+    const uint32_t d0 = w[0], d1 = w[1], d2 = w[2], d3 = w[3];
     const uint64_t A = ((uint64_t)d1 << 32) | d0, B = ((uint64_t)d3 << 32) | d2;
     const int32_t t = left - 8 * cb - 64;  // [32, 64)
     hi = (A >> t) | (B << (64 - t));
@@ -1725,7 +1730,7 @@ __device__ __forceinline__ void zmover(SeqSmem &sm, int gn, const gc_u16 *tabs) 
 #pragma unroll
         for (int i = 0; i < (ZAHEAD + 7) / 4; ++i) {
             const int32_t k = g.kt - q - 4 * i;
-            if (on && k >= lo) *(uint4 *)(ring + ((k & (ZRB2 / 16 - 1)) << 4)) = zclip(v[i], k, g.m);
+            if (on && k >= lo) zr_put(ring, k, zclip(v[i], k, g.m));
         }
         if (on) lr = lo;
     }
@@ -1743,7 +1748,7 @@ __device__ __forceinline__ void zmover(SeqSmem &sm, int gn, const gc_u16 *tabs) 
         // land the blocks loaded ZMD periods ago
 #pragma unroll
         for (int i = 0; i < 2; ++i)
-            if (pend_on[0][i]) *(uint4 *)(ring + ((pend_k[0][i] & (ZRB2 / 16 - 1)) << 4)) = zclip(pend_v[0][i], pend_k[0][i], g.m);
+            if (pend_on[0][i]) zr_put(ring, pend_k[0][i], zclip(pend_v[0][i], pend_k[0][i], g.m));
 #pragma unroll
         for (int d = 0; d + 1 < ZMD; ++d)
 #pragma unroll
@@ -1813,6 +1818,8 @@ __device__ __forceinline__ void zdecode(SeqSmem &sm, int gn, uint32_t &r0, uint3
         left -= c;
     }
     const uint32_t szl = 1u << all, szo = 1u << alof, szm = 1u << alml;
+    const uint32_t kl31 = (uint32_t)all - 31u, ko31 = (uint32_t)alof - 31u, km31 = (uint32_t)alml - 31u;
+    g_u4 *itp = it + 2;  // the next sequence's item
     for (int p = 0;; ++p) {
 #if JFS_ZUNROLL
 #pragma unroll
@@ -1820,7 +1827,7 @@ __device__ __forceinline__ void zdecode(SeqSmem &sm, int gn, uint32_t &r0, uint3
         for (int k = 0; k < ZK2; ++k) {
             if (run) {
                 if (left < m8) {  // overflow
-                    it[2 + i] = make_uint4(0, 0, (uint32_t)E_CORRUPT, IT_ERR);
+                    *itp = make_uint4(0, 0, (uint32_t)E_CORRUPT, IT_ERR);
                     run = false;
                 } else {
                     const uint32_t cl = tl[sll], co = to[sof], cm = tm[sml];
@@ -1875,21 +1882,23 @@ __device__ __forceinline__ void zdecode(SeqSmem &sm, int gn, uint32_t &r0, uint3
                         const uint64_t h2 = zw_shift(hi, lo, c);
                         int32_t c2 = 0;
                         const uint32_t nsl = cl >> 6, nso = co >> 6, nsm = cm >> 6;
-                        const uint32_t nbl = all - (31 - __builtin_clz(nsl));
-                        const uint32_t nbm = alml - (31 - __builtin_clz(nsm));
-                        const uint32_t nbo = alof - (31 - __builtin_clz(nso));
+                        // nb = al - highbit(ns) = (al - 31) + clz(ns)
+                        const uint32_t nbl = kl31 + (uint32_t)__builtin_clz(nsl);
+                        const uint32_t nbm = km31 + (uint32_t)__builtin_clz(nsm);
+                        const uint32_t nbo = ko31 + (uint32_t)__builtin_clz(nso);
                         sll = ((nsl << nbl) - szl) + zw_get(h2, c2, nbl);
                         sml = ((nsm << nbm) - szm) + zw_get(h2, c2, nbm);
                         sof = ((nso << nbo) - szo) + zw_get(h2, c2, nbo);
                         c += c2;
                     }
                     left -= c;
-                    it[2 + i] = make_uint4(ll, ml, off, IT_SEQ);
+                    itp[0] = make_uint4(ll, ml, off, IT_SEQ);
                     if (i + 1 == d.nseq) {
-                        it[3 + i] = left == m8 ? make_uint4(0, 0, 0, IT_BEND) : make_uint4(0, 0, (uint32_t)E_CORRUPT, IT_ERR);
+                        itp[1] = left == m8 ? make_uint4(0, 0, 0, IT_BEND) : make_uint4(0, 0, (uint32_t)E_CORRUPT, IT_ERR);
                         run = false;
                     }
                     ++i;
+                    ++itp;
                 }
             }
         }
