@@ -1101,7 +1101,10 @@ static_assert(ZARENA == 0 || ZARENA >= 1280 + 8, "one block's largest tables mus
 // 152 ms on configs[3])
 constexpr int ZNB = JFS_ZNB;
 constexpr int ZMQ = 64 / ZNB < 4 ? 64 / ZNB : 4;  // mover lanes per block
-constexpr int ZK2 = 8;      // sequences per period
+#ifndef JFS_ZK2
+#define JFS_ZK2 8
+#endif
+constexpr int ZK2 = JFS_ZK2;  // sequences per period
 constexpr int ZRB2 = 512;   // bitstream ring bytes per lane (32 blocks of 16 B)
 #ifndef JFS_ZMOVE_D
 #define JFS_ZMOVE_D 2  // periods between a mover load and its landing in the ring
