@@ -2234,6 +2234,9 @@ constexpr int FB = 64;           // far-source prefetch bytes per lane (16 B ali
 constexpr int FBUSE = FB - 16;
 constexpr int BSPAN = R / 2;     // max output span of one lane-parallel batch
 constexpr int LONGI = 1024;      // items longer than this are copied by the whole wave
+#ifndef JFS_ZEXEC_LEVELS
+#define JFS_ZEXEC_LEVELS 0  // 1: near matches in dependency rounds (binary search over lanes); measured slower (119 vs 114 ms)
+#endif
 #ifndef JFS_ZEXEC_NEARSER
 #define JFS_ZEXEC_NEARSER 1  // near matches: one lane-parallel round, the rest by the whole wave in order
 #endif
@@ -2522,6 +2525,32 @@ __device__ __forceinline__ void x_batch(XSmem &s, X &x, bool act, int32_t o, uin
         }
         __builtin_amdgcn_wave_barrier();
         XP_ADD(6, 1);
+#if JFS_ZEXEC_LEVELS
+        // dependency rounds: a pending match goes when no still-pending match
+        // of an earlier lane writes into its source.  Pending match regions are
+        // disjoint and in lane order, so with M = prefix max of their ends the
+        // first lane whose M passes this lane's source start is the only
+        // candidate (binary search over lanes with ds_bpermute).  The lowest
+        // pending lane always goes, so rounds <= pending lanes.
+        for (int guard2 = 0; __ballot(pend); ++guard2) {
+            const uint32_t pe = pend ? (uint32_t)(ms2 + ml2) : 0u;
+            const uint32_t M = dpp_scan_max(pe);
+            const int32_t sendp = msrc2 + ml2 < ms2 ? msrc2 + ml2 : ms2;
+            int32_t pos = 0;
+#pragma unroll
+            for (int st = 32; st; st >>= 1) {
+                const int32_t q = pos + st - 1;
+                const uint32_t mq = (uint32_t)__builtin_amdgcn_ds_bpermute((q & 63) << 2, (int)M);
+                if (q < l && mq <= (uint32_t)msrc2) pos += st;
+            }
+            const int32_t ps = __builtin_amdgcn_ds_bpermute((pos & 63) << 2, pend ? ms2 : 0x7FFFFFFF);
+            const bool go = pend && !(pos < l && ps < sendp);
+            if (go) cp_ring(s, x, msrc2, ms2, ml2, off);
+            __builtin_amdgcn_wave_barrier();
+            pend = pend && !go;
+            if (guard2 > 64) { x.bug = 104; break; }
+        }
+#endif
         for (uint64_t pm = __ballot(pend); pm; pm &= pm - 1) {
             const int j = (int)__builtin_ctzll(pm);
             const int32_t jd = (int32_t)readlane((uint32_t)ms2, j), jsrc = (int32_t)readlane((uint32_t)msrc2, j);

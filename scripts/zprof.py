@@ -7,14 +7,15 @@ import torch
 from juicefs_amd import _lib, device as D
 lib = _lib.load()
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 64
-b = D.ZstdBatch(n, 4 << 20, "T", level=3, distinct=16, seed_base=1)
+b = D.ZstdBatch(n, 4 << 20, "T", level=3, distinct=16, seed_base=1,
+                cache_dir=os.path.join(ROOT, "gpurun_out", "frames"))
 b.decompress(); torch.cuda.synchronize()
 lib.jfs_zprof_reset()
 b.decompress(); torch.cuda.synchronize()
 buf = (ctypes.c_ulonglong * 8)()
 lib.jfs_zprof_read(buf)
-names = ["batch_load", "-", "classify", "write", "-", "chunks", "runs", "total"]
+names = ["item_load", "flush+far_issue", "literals", "far_land", "matches", "batches", "match_rounds", "total"]
 for i, nm in enumerate(names):
     print(f"{nm:12s} per frame {buf[i] / n:14.0f}")
-print(f"per chunk: classify {buf[2] / max(buf[5], 1):.0f} write {buf[3] / max(buf[5], 1):.0f}; per run batch_load {buf[0] / max(buf[6], 1):.0f}")
+print(f"per batch: flush+far {buf[1] / max(buf[5], 1):.0f} literals {buf[2] / max(buf[5], 1):.0f} far_land {buf[3] / max(buf[5], 1):.0f} matches {buf[4] / max(buf[5], 1):.0f} ticks; match rounds per batch {buf[6] / max(buf[5], 1):.2f}")
 print("ok" if b.verify() else "MISMATCH")
