@@ -290,13 +290,17 @@ def host_path_rate(comp_blocks, raw_blocks, U, nblk, reps=2, device_mask=0):
     ncb = min(nblk, 1024)
     raws = (raw_blocks * (ncb // len(raw_blocks) + 1))[:ncb]
     cpairs = [(bytearray(bound), rb) for rb in raws]
-    t0 = time.perf_counter()
-    res = c.CompressBatch(cpairs, device_mask=device_mask)
-    dt = time.perf_counter() - t0
-    assert all(n > 0 and e is None for n, e in res)
+    res_c = 0.0
+    for _ in range(reps):  # best of reps: the first call may grow the staging (4 GiB LZ4-compress chunks)
+        t0 = time.perf_counter()
+        res = c.CompressBatch(cpairs, device_mask=device_mask)
+        dt = time.perf_counter() - t0
+        assert all(n > 0 and e is None for n, e in res)
+        res_c = max(res_c, len(cpairs) * U / dt / 2**30)
     return {"lz4_decompress": {"value": res_d, "unit": "GiB/s"},
-            "lz4_compress": {"value": len(cpairs) * U / dt / 2**30, "unit": "GiB/s"},
+            "lz4_compress": {"value": res_c, "unit": "GiB/s"},
             "blocks": nblk, "compress_blocks": ncb, "chunk_mb": int(os.environ.get("JFS_HOST_CHUNK_MB", "2048")),
+            "chunk_mb_lz4_compress": int(os.environ.get("JFS_HOST_CHUNK_MB_LZ4C", "4096")),
             "path": "jfs_{de,}compress_batch: host buffers -> pinned (16 threads) -> H2D -> kernel -> D2H -> "
                     "host buffers, 2-stream chunk pipeline, 1 GPU, GiB/s of uncompressed bytes"}
 
@@ -437,6 +441,7 @@ def configs0_roundtrip(dev, nblk, U, seed_base=90001):
     bound = c.CompressBound(U)
     comp = np.zeros(nblk * bound, dtype=np.uint8)
     pairs = [(comp[i * bound:(i + 1) * bound], raw[i * U:(i + 1) * U]) for i in range(nblk)]
+    c.CompressBatch(pairs)  # warm: the library's pinned staging grows to its chunk size once per process
     t0 = time.perf_counter()
     res = c.CompressBatch(pairs)
     tc = time.perf_counter() - t0

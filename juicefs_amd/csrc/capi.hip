@@ -451,6 +451,20 @@ int64_t chunk_limit() {
     return v;
 }
 
+// LZ4 compress chunks: the serial-parse encoder holds 8 blocks per CU and a
+// launch lasts one block's parse (~0.5 s) whatever its size, so a 2 GiB chunk
+// (256 blocks at ~8 MiB staged each) fills an eighth of the GPU; 4 GiB chunks
+// (512 blocks) with two chunk kernels side by side fill half of it.
+// JFS_HOST_CHUNK_MB_LZ4C overrides.
+int64_t chunk_limit_lz4c() {
+    static int64_t v = [] {
+        const char *e = getenv("JFS_HOST_CHUNK_MB_LZ4C");
+        long long mb = e ? atoll(e) : 4096;
+        return (int64_t)std::max(mb, 16ll) << 20;
+    }();
+    return v;
+}
+
 // Batches of at most this many LZ4 decode blocks take the small-batch path
 // (lz4_split.hip: every block spread over the whole GPU) instead of one
 // workgroup per block; JFS_LZ4_SPLIT_MAX overrides (0 = never).
@@ -658,7 +672,7 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
     };
     std::vector<Chunk> ch;
     {
-        const int64_t limit = chunk_limit();
+        const int64_t limit = algo == JFS_ALGO_LZ4 && dir == COMPRESS && !ae ? chunk_limit_lz4c() : chunk_limit();
         int s = 0;
         while (s < nblk) {
             Chunk c{s, s, (int)(ch.size() % NSLOT), 0, 0, kstream((int)ch.size())};
