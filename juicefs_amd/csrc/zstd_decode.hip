@@ -1105,12 +1105,15 @@ constexpr int ZMQ = 64 / ZNB < 4 ? 64 / ZNB : 4;  // mover lanes per block
 #define JFS_ZK2 8
 #endif
 constexpr int ZK2 = JFS_ZK2;  // sequences per period
-constexpr int ZRB2 = 512;   // bitstream ring bytes per lane (32 blocks of 16 B)
+#ifndef JFS_ZRB2
+#define JFS_ZRB2 512
+#endif
+constexpr int ZRB2 = JFS_ZRB2;  // bitstream ring bytes per lane (blocks of 16 B)
 #ifndef JFS_ZMOVE_D
 #define JFS_ZMOVE_D 2  // periods between a mover load and its landing in the ring
 #endif
 constexpr int ZMD = JFS_ZMOVE_D;
-constexpr int ZAHEAD = ZMD == 2 ? 27 : 24;  // ring blocks the mover keeps below the published position
+constexpr int ZAHEAD = ZRB2 == 512 ? (ZMD == 2 ? 27 : 24) : ZRB2 / 16 - 2;  // ring blocks the mover keeps below the published position
 // <= 89 bits per sequence: a period moves the position down <= 6 blocks and
 // a refill window reaches 128 bits below it (one block more).  Loads issued
 // in iteration p land during iteration p + ZMD and serve period p + ZMD + 1,
@@ -1118,6 +1121,7 @@ constexpr int ZAHEAD = ZMD == 2 ? 27 : 24;  // ring blocks the mover keeps below
 // target came from; and a landing block must not displace (32 slots) one the
 // decoder still reads (<= 1 block above its position).
 constexpr int ZPB = (ZK2 * 89 + 127) / 128;
+constexpr int ZPRE = ZAHEAD + 3 < ZRB2 / 16 - 2 ? ZAHEAD + 3 : ZRB2 / 16 - 2;  // prefill depth below the top block
 static_assert((ZMD + 1) * ZPB + 7 <= ZAHEAD && ZAHEAD <= ZRB2 / 16 - 2 && ZPB + 2 <= 8, "ring budget");
 #if JFS_ZSEQ_V2
 struct ASmem {  // zseqa: table-build scratch
@@ -1719,10 +1723,10 @@ __device__ __forceinline__ void zmover(SeqSmem &sm, int gn, const gc_u16 *tabs) 
     // blocks below -3 are never read (a lane stops once its position is
     // below the stream start); blocks [-3, 0) are written as zeros
     constexpr int32_t KFLOOR = -3;
-    // prefill blocks [kt - (ZAHEAD + 3), kt]
+    // prefill blocks [kt - ZPRE, kt]
     int32_t lr = g.kt + 1;
     {
-        const int32_t lo = g.kt - (ZAHEAD + 3) > KFLOOR ? g.kt - (ZAHEAD + 3) : KFLOOR;
+        const int32_t lo = g.kt - ZPRE > KFLOOR ? g.kt - ZPRE : KFLOOR;
         uint4 v[(ZAHEAD + 7) / 4];
 #pragma unroll
         for (int i = 0; i < (ZAHEAD + 7) / 4; ++i) {
@@ -2803,9 +2807,64 @@ bool grow_dev(T **p, size_t *cap, size_t need) {
 // reference pins 1.5.6); see oracle/zstd_oracle.c.
 constexpr int g_strict_reserved = 1;
 
+// zlit overlapped with zseqa/zseqb on a low-priority side stream
+// (JFS_ZSTD_OVERLAP=1): the sequence kernels dispatch first and zlit's
+// workgroups take what LDS they leave.  One side stream and event pair per
+// (device, caller stream).
+struct AuxPair {
+    int dev;
+    hipStream_t caller, aux;
+    hipEvent_t fork, join;
+};
+std::mutex g_aux_mu;
+std::vector<AuxPair> g_aux;
+AuxPair *aux_for(hipStream_t s) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(g_aux_mu);
+    for (auto &a : g_aux)
+        if (a.dev == dev && a.caller == s) return &a;
+    if (g_aux.size() >= 64) return nullptr;
+    AuxPair a{dev, s, nullptr, nullptr, nullptr};
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) return nullptr;
+    if (hipStreamCreateWithPriority(&a.aux, hipStreamNonBlocking, lo) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&a.fork, hipEventDisableTiming) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&a.join, hipEventDisableTiming) != hipSuccess) return nullptr;
+    g_aux.reserve(64);
+    g_aux.push_back(a);
+    return &g_aux.back();
+}
+bool zstd_overlap() {
+    static const bool v = [] {
+        const char *e = getenv("JFS_ZSTD_OVERLAP");
+        return e && atoi(e) > 0;
+    }();
+    return v;
+}
+
 int launch_entropy_exec(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, jfs::zstdd::ZInfo *d_info,
                         uint8_t *d_lit, uint16_t *d_tabs, uint4 *d_items, hipStream_t stream) {
     using namespace jfs::zstdd;
+#if JFS_ZSEQ_V2
+    AuxPair *ap = zstd_overlap() ? aux_for(stream) : nullptr;
+    if (ap) {
+        if (hipEventRecord(ap->fork, stream) != hipSuccess) return -1;
+        hipLaunchKernelGGL(zseqa_kernel, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, d_info, d_tabs, d_items,
+                           g_strict_reserved);
+        if (hipGetLastError() != hipSuccess) return -1;
+        hipLaunchKernelGGL(zseqb_kernel, dim3((nblk + ZSEQ_INPUTS - 1) / ZSEQ_INPUTS), dim3(128), 0, stream, d_blocks,
+                           nblk, d_info, d_tabs, d_items);
+        if (hipGetLastError() != hipSuccess) return -1;
+        if (hipStreamWaitEvent(ap->aux, ap->fork, 0) != hipSuccess) return -1;
+        hipLaunchKernelGGL(zlit_kernel, dim3(nblk), dim3(64), 0, ap->aux, d_blocks, nblk, d_info, d_lit);
+        if (hipGetLastError() != hipSuccess) return -1;
+        if (hipEventRecord(ap->join, ap->aux) != hipSuccess) return -1;
+        if (hipStreamWaitEvent(stream, ap->join, 0) != hipSuccess) return -1;
+        hipLaunchKernelGGL(zexec_kernel, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, d_info, d_lit, d_items, d_ret);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
+#endif
     hipLaunchKernelGGL(zlit_kernel, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, d_info, d_lit);
     if (hipGetLastError() != hipSuccess) return -1;
 #if JFS_ZSEQ_V2
