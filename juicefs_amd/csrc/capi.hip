@@ -852,16 +852,17 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
             if (lk == 0 && algo == JFS_ALGO_LZ4) {
                 if (n <= split_max()) {
                     std::vector<int32_t> lens(n), caps(n);
-                    int64_t nseg = 0, max_cap = 0;
+                    int64_t nseg = 0, max_cap = 0, norg = 0;
                     for (int k = 0; k < n; k++) {
                         lens[k] = h_desc[k].src_len;
                         caps[k] = h_desc[k].dst_cap;
                         nseg += (std::max(lens[k], 0) + JFS_LZ4_SPLIT_SEG - 1) / JFS_LZ4_SPLIT_SEG;
                         max_cap = std::max<int64_t>(max_cap, caps[k]);
+                        norg += (std::max<int64_t>(caps[k], 0) + 3) & ~3ll;
                     }
                     if (!sl.ensure_split(jfs_lz4_split_scratch_bytes(n, lens.data(), caps.data())))
                         return JFS_ERR_NO_MEMORY;
-                    lk = jfs_launch_lz4_split(d_desc, n, d_ret, sl.sp, nseg, max_cap, c.ks);
+                    lk = jfs_launch_lz4_split(d_desc, n, d_ret, sl.sp, nseg, max_cap, norg, c.ks);
                 } else {
                     lk = jfs_launch_lz4_decode(d_desc, n, d_ret, c.ks);
                 }
@@ -935,15 +936,16 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
             lk = jfs_launch_zstd_decode_planned(d_desc, n, d_ret, d_zi, sl.z_lit, sl.z_tabs, sl.z_items, c.ks);
         } else if (algo == JFS_ALGO_LZ4 && dir == DECOMPRESS && n <= split_max()) {
             std::vector<int32_t> lens(n), caps(n);
-            int64_t nseg = 0, max_cap = 0;
+            int64_t nseg = 0, max_cap = 0, norg = 0;
             for (int k = 0; k < n; k++) {
                 lens[k] = h_desc[k].src_len;
                 caps[k] = h_desc[k].dst_cap;
                 nseg += (std::max(lens[k], 0) + JFS_LZ4_SPLIT_SEG - 1) / JFS_LZ4_SPLIT_SEG;
                 max_cap = std::max<int64_t>(max_cap, caps[k]);
+                norg += (std::max<int64_t>(caps[k], 0) + 3) & ~3ll;
             }
             if (!sl.ensure_split(jfs_lz4_split_scratch_bytes(n, lens.data(), caps.data()))) return JFS_ERR_NO_MEMORY;
-            lk = jfs_launch_lz4_split(d_desc, n, d_ret, sl.sp, nseg, max_cap, c.ks);
+            lk = jfs_launch_lz4_split(d_desc, n, d_ret, sl.sp, nseg, max_cap, norg, c.ks);
         } else if (algo == JFS_ALGO_LZ4 && dir == COMPRESS) {
             const int64_t r = lz4_encode(sl, h_desc, d_desc, n, d_ret, c.ks);
             if (r == JFS_ERR_NO_MEMORY) return r;
@@ -1618,10 +1620,11 @@ int64_t jfs_lz4_decompress_device_small(const jfs_dev_block *d_blocks, const int
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return JFS_ERR_HIP;
     stat_launch(JFS_ALGO_LZ4, DECOMPRESS, nblk);
-    int64_t nseg = 0, max_cap = 0;
+    int64_t nseg = 0, max_cap = 0, norg = 0;
     for (int k = 0; k < nblk; k++) {
         nseg += (std::max(src_len[k], 0) + JFS_LZ4_SPLIT_SEG - 1) / JFS_LZ4_SPLIT_SEG;
         max_cap = std::max<int64_t>(max_cap, dst_cap[k]);
+        norg += (std::max<int64_t>(dst_cap[k], 0) + 3) & ~3ll;
     }
     const int64_t need = jfs_lz4_split_scratch_bytes(nblk, src_len, dst_cap);
     SplitScratch &z = g_split[dev];
@@ -1639,7 +1642,7 @@ int64_t jfs_lz4_decompress_device_small(const jfs_dev_block *d_blocks, const int
     }
     hipStream_t st = (hipStream_t)stream;
     if (hipStreamWaitEvent(st, z.ev_done, 0) != hipSuccess) return JFS_ERR_HIP;
-    if (jfs_launch_lz4_split(d_blocks, nblk, d_ret, z.p, nseg, max_cap, st) != 0) return JFS_ERR_HIP;
+    if (jfs_launch_lz4_split(d_blocks, nblk, d_ret, z.p, nseg, max_cap, norg, st) != 0) return JFS_ERR_HIP;
     return hipEventRecord(z.ev_done, st) == hipSuccess ? JFS_OK : JFS_ERR_HIP;
 }
 

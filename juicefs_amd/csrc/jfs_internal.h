@@ -52,11 +52,12 @@ int jfs_launch_lz4_decode_todo(const jfs_dev_block *d_blocks, int nblk, int32_t 
                                hipStream_t stream);
 // small-batch LZ4 decode (lz4_split.hip): compressed bytes per segment (one
 // lane each), scratch bytes for these blocks, and
-// the launch (nseg_all = sum of ceil(src_len / 256), max_cap = largest dst_cap)
+// the launch (nseg_all = sum of ceil(src_len / 256), max_cap = largest dst_cap,
+// norg_all = sum of dst_cap rounded up to 4: the host sizes the scratch with them)
 #define JFS_LZ4_SPLIT_SEG 256
 int64_t jfs_lz4_split_scratch_bytes(int nb, const int32_t *src_len, const int32_t *cap);
 int jfs_launch_lz4_split(const jfs_dev_block *d_desc, int nb, int32_t *d_ret, void *d_scratch, int64_t nseg_all,
-                         int64_t max_cap, hipStream_t st);
+                         int64_t max_cap, int64_t norg_all, hipStream_t st);
 // ret value of a fused chain's second step when its first step failed
 #define JFS_CHAIN_FAILED (-2147483647 - 1)
 int jfs_launch_gen(uint8_t *d_dst, int nblk, int64_t block_bytes, char cls, uint64_t seed_base,

@@ -158,7 +158,15 @@ __device__ __forceinline__ int block_of(const SBlock *blk, int nb, int g) {
     return lo;
 }
 
-__global__ void plan_kernel(const jfs_dev_block *__restrict__ desc, int nb, Scratch sc) {
+// The scratch and the grids were sized on the host from its own (src_len,
+// dst_cap) copies (nseg_all, max_cap, norg_all).  A block whose device
+// descriptor asks for more than that budget leaves -- it would overrun the
+// segment or origin-map scratch -- is planned empty and marked bad, so the
+// exact one-workgroup kernel decodes it from its descriptor instead.
+__global__ void plan_kernel(const jfs_dev_block *__restrict__ desc, int nb, Scratch sc, int64_t nseg_all,
+                            int64_t max_cap, int64_t norg_all) {
+    for (int i = threadIdx.x; i < nb * (int)(sizeof(BStat) / 4); i += blockDim.x) ((int32_t *)sc.st)[i] = 0;
+    __syncthreads();
     if (threadIdx.x == 0 && blockIdx.x == 0) {
         int32_t seg = 0;
         int64_t bits = 0, org = 0;
@@ -169,6 +177,12 @@ __global__ void plan_kernel(const jfs_dev_block *__restrict__ desc, int nb, Scra
             s.dst = d.dst;
             s.n = d.src_len > 0 ? d.src_len : 0;
             s.cap = d.dst_cap > 0 ? d.dst_cap : 0;
+            const int64_t ns = (s.n + SEG - 1) / SEG, no = ((int64_t)s.cap + 3) & ~3ll;
+            if (s.cap > max_cap || seg + ns > nseg_all || org + no > norg_all) {
+                s.n = 0;
+                s.cap = 0;
+                sc.st[b].bad = 1;
+            }
             s.seg0 = seg;
             s.nseg = (s.n + SEG - 1) / SEG;
             s.bits_off = bits;
@@ -178,7 +192,6 @@ __global__ void plan_kernel(const jfs_dev_block *__restrict__ desc, int nb, Scra
             org += ((int64_t)s.cap + 3) & ~3ll;
         }
     }
-    for (int i = threadIdx.x; i < nb * (int)(sizeof(BStat) / 4); i += blockDim.x) ((int32_t *)sc.st)[i] = 0;
 }
 
 __global__ __launch_bounds__(T) void spec_kernel(int nb, int nseg_all, Scratch sc) {
@@ -287,7 +300,7 @@ __global__ __launch_bounds__(T) void count_kernel(int nb, int nseg_all, Scratch 
         if (c > B.cap) break;
         x = t.next;
     }
-    sc.cnt[g] = (int32_t)(c < B.cap ? c : (int64_t)B.cap + 1);
+    sc.cnt[g] = (int32_t)(c <= B.cap ? c : (int64_t)B.cap + 1);
 }
 
 // one workgroup per block: cnt -> exclusive output offsets, block total
@@ -506,7 +519,7 @@ extern "C" int64_t jfs_lz4_split_scratch_bytes(int nb, const int32_t *src_len, c
 // host computes both from the same (src_len, cap) it sized the scratch with.
 // d_todo (nb int32, optional): 1 for the blocks the exact kernel must redo.
 extern "C" int jfs_launch_lz4_split(const jfs_dev_block *d_desc, int nb, int32_t *d_ret, void *d_scratch,
-                                    int64_t nseg_all, int64_t max_cap, hipStream_t st) {
+                                    int64_t nseg_all, int64_t max_cap, int64_t norg_all, hipStream_t st) {
     if (nb <= 0) return 0;
     uint8_t *p = (uint8_t *)(((uintptr_t)d_scratch + 255) & ~(uintptr_t)255);
     Scratch sc;
@@ -527,7 +540,7 @@ extern "C" int jfs_launch_lz4_split(const jfs_dev_block *d_desc, int nb, int32_t
     sc.org = (int32_t *)p;
     const int gs = (int)((nseg_all + T - 1) / T);
     const dim3 gp((unsigned)((max_cap / 4 + T) / T), (unsigned)nb);
-    hipLaunchKernelGGL(plan_kernel, dim3(1), dim3(T), 0, st, d_desc, nb, sc);
+    hipLaunchKernelGGL(plan_kernel, dim3(1), dim3(T), 0, st, d_desc, nb, sc, nseg_all, max_cap, norg_all);
     if (nseg_all > 0) {
         hipLaunchKernelGGL(spec_kernel, dim3(gs), dim3(T), 0, st, nb, (int)nseg_all, sc);
         for (int r = 0; r < FIX_ROUNDS; r++) hipLaunchKernelGGL(fix_kernel, dim3(gs), dim3(T), 0, st, nb, (int)nseg_all, sc, r);

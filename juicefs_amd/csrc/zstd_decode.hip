@@ -2807,64 +2807,9 @@ bool grow_dev(T **p, size_t *cap, size_t need) {
 // reference pins 1.5.6); see oracle/zstd_oracle.c.
 constexpr int g_strict_reserved = 1;
 
-// zlit overlapped with zseqa/zseqb on a low-priority side stream
-// (JFS_ZSTD_OVERLAP=1): the sequence kernels dispatch first and zlit's
-// workgroups take what LDS they leave.  One side stream and event pair per
-// (device, caller stream).
-struct AuxPair {
-    int dev;
-    hipStream_t caller, aux;
-    hipEvent_t fork, join;
-};
-std::mutex g_aux_mu;
-std::vector<AuxPair> g_aux;
-AuxPair *aux_for(hipStream_t s) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    std::lock_guard<std::mutex> lk(g_aux_mu);
-    for (auto &a : g_aux)
-        if (a.dev == dev && a.caller == s) return &a;
-    if (g_aux.size() >= 64) return nullptr;
-    AuxPair a{dev, s, nullptr, nullptr, nullptr};
-    int lo = 0, hi = 0;
-    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) return nullptr;
-    if (hipStreamCreateWithPriority(&a.aux, hipStreamNonBlocking, lo) != hipSuccess) return nullptr;
-    if (hipEventCreateWithFlags(&a.fork, hipEventDisableTiming) != hipSuccess) return nullptr;
-    if (hipEventCreateWithFlags(&a.join, hipEventDisableTiming) != hipSuccess) return nullptr;
-    g_aux.reserve(64);
-    g_aux.push_back(a);
-    return &g_aux.back();
-}
-bool zstd_overlap() {
-    static const bool v = [] {
-        const char *e = getenv("JFS_ZSTD_OVERLAP");
-        return e && atoi(e) > 0;
-    }();
-    return v;
-}
-
 int launch_entropy_exec(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, jfs::zstdd::ZInfo *d_info,
                         uint8_t *d_lit, uint16_t *d_tabs, uint4 *d_items, hipStream_t stream) {
     using namespace jfs::zstdd;
-#if JFS_ZSEQ_V2
-    AuxPair *ap = zstd_overlap() ? aux_for(stream) : nullptr;
-    if (ap) {
-        if (hipEventRecord(ap->fork, stream) != hipSuccess) return -1;
-        hipLaunchKernelGGL(zseqa_kernel, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, d_info, d_tabs, d_items,
-                           g_strict_reserved);
-        if (hipGetLastError() != hipSuccess) return -1;
-        hipLaunchKernelGGL(zseqb_kernel, dim3((nblk + ZSEQ_INPUTS - 1) / ZSEQ_INPUTS), dim3(128), 0, stream, d_blocks,
-                           nblk, d_info, d_tabs, d_items);
-        if (hipGetLastError() != hipSuccess) return -1;
-        if (hipStreamWaitEvent(ap->aux, ap->fork, 0) != hipSuccess) return -1;
-        hipLaunchKernelGGL(zlit_kernel, dim3(nblk), dim3(64), 0, ap->aux, d_blocks, nblk, d_info, d_lit);
-        if (hipGetLastError() != hipSuccess) return -1;
-        if (hipEventRecord(ap->join, ap->aux) != hipSuccess) return -1;
-        if (hipStreamWaitEvent(stream, ap->join, 0) != hipSuccess) return -1;
-        hipLaunchKernelGGL(zexec_kernel, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, d_info, d_lit, d_items, d_ret);
-        return hipGetLastError() == hipSuccess ? 0 : -1;
-    }
-#endif
     hipLaunchKernelGGL(zlit_kernel, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, d_info, d_lit);
     if (hipGetLastError() != hipSuccess) return -1;
 #if JFS_ZSEQ_V2

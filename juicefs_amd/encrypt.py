@@ -59,11 +59,29 @@ def _err_of(code: int, dst_len: int, src_len: int, op: str) -> CompressError:
     return _err(code, dst_len, src_len, op)
 
 
+NONCE_SIZE = 12  # encrypt.go:239: aead.NonceSize() of all three ciphers
+
+
+def _check_keys(algo: str, keys, nonces) -> None:
+    """The C ABI reads jfs_cipher_key_size() key bytes and 12 nonce bytes per
+    block through plain pointers; a shorter buffer would be read past its end.
+    dataEncryptor.aead (encrypt.go:182-202, used at :235, :276) refuses a wrong key size with an
+    error, and so does this, before anything reaches the library."""
+    ks = key_size(algo)
+    for i, k in enumerate(keys):
+        if len(k) != ks:
+            raise ValueError(f"block {i}: {algo or 'aes256gcm-rsa'} needs a {ks}-byte key, got {len(k)}")
+    for i, n in enumerate(nonces or ()):
+        if len(n) != NONCE_SIZE:
+            raise ValueError(f"block {i}: nonce must be {NONCE_SIZE} bytes, got {len(n)}")
+
+
 def compress_seal_batch(codec: int, algo: str, pairs, params, device_mask: int = 0, crcs: list | None = None):
     """pairs: [(dst, raw block)], params: [(key, nonce, wrapped_key)] -> [(envelope bytes, err)];
     with crcs=[], it receives each envelope's CRC-32C (generateChecksum)."""
     lib = L.load()
     nb = len(pairs)
+    _check_keys(algo, [p[0] for p in params], [p[1] for p in params])
     iov = (L.JfsIov * max(nb, 1))()
     sp = (L.JfsSealParam * max(nb, 1))()
     keep = []
@@ -91,6 +109,7 @@ def open_decompress_batch(codec: int, algo: str, pairs, keys, device_mask: int =
     """pairs: [(dst, envelope)], keys: [data key] -> [(n, err)] (n as jfs_decompress returns it)"""
     lib = L.load()
     nb = len(pairs)
+    _check_keys(algo, keys, None)
     iov = (L.JfsIov * max(nb, 1))()
     kp = (ctypes.c_void_p * max(nb, 1))()
     keep = []

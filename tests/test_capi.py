@@ -119,3 +119,23 @@ def test_codec_selector_env():
     # an empty device selection leaves no device (and no CPU fallback)
     mode, ndev, rc = _mode_in_subprocess("force", devices="0x0")
     assert (mode, ndev, rc) == (L.MODE_FORCE, 0, L.JFS_ERR_NO_DEVICE)
+
+
+def test_seal_and_open_refuse_wrong_key_and_nonce_sizes(lib):
+    # dataEncryptor.aead (pkg/object/encrypt.go:182-202) errors on a wrong key
+    # size; the batch ABI reads key_size / 12 bytes through plain pointers, so
+    # the Python layer refuses short buffers before any library call
+    import pytest
+    from juicefs_amd import encrypt as E
+    raw = b"x" * 100
+    dst = bytearray(1024)
+    for algo, ks in [(E.AES256GCM_RSA, 32), (E.CHACHA20_RSA, 32), (E.SM4GCM, 16)]:
+        assert E.key_size(algo) == ks
+        with pytest.raises(ValueError, match="key"):
+            E.compress_seal_batch(0, algo, [(dst, raw)], [(b"k" * (ks - 1), b"n" * 12, b"w")])
+        with pytest.raises(ValueError, match="key"):
+            E.compress_seal_batch(0, algo, [(dst, raw)], [(b"k" * (ks + 1), b"n" * 12, b"w")])
+        with pytest.raises(ValueError, match="nonce"):
+            E.compress_seal_batch(0, algo, [(dst, raw)], [(b"k" * ks, b"n" * 8, b"w")])
+        with pytest.raises(ValueError, match="key"):
+            E.open_decompress_batch(0, algo, [(dst, raw)], [b"k" * 16 if ks == 32 else b"k" * 32])

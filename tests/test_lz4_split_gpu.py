@@ -168,3 +168,50 @@ def test_split_through_one_call_api(gpu, oracle):
     assert err is not None and n == r
     done, handed = D.lz4_split_counts()[:2]
     assert done + handed == 2 and done >= 1, (done, handed)
+
+
+def test_split_one_segment_exact_cap_stays_on_split_path(gpu, oracle):
+    """A block of <= 256 compressed bytes decoded into exactly its size (the
+    one-call path's dst) is decoded by the split path itself: the count of a
+    segment that ends exactly at dst_cap is not an overflow."""
+    srcs = [gen_block("T", 5100 + i, n) for i, n in enumerate((40, 100, 300, 500))] + [b"a" * 200, b"ab" * 150]
+    comps = [oracle.lz4_compress(s)[1] for s in srcs]
+    assert all(len(c) <= 256 for c in comps), [len(c) for c in comps]
+    D.lz4_split_counts(reset=True)
+    r, outs = run_small(comps, [len(s) for s in srcs], gpu)
+    assert r == [len(s) for s in srcs]
+    assert all(o == s for o, s in zip(outs, srcs))
+    done, handed = D.lz4_split_counts()[:2]
+    assert done == len(srcs) and handed == 0, (done, handed)
+
+
+def test_split_device_sizes_beyond_host_budget_go_exact(gpu, oracle):
+    """jfs_lz4_decompress_device_small sizes its scratch from the HOST
+    (src_len, dst_cap) arrays; a device descriptor asking for more (a caller
+    bug) must not overrun that scratch: the block is handed to the exact
+    kernel, which decodes it from its descriptor."""
+    srcs = [gen_block("T", 5200 + i, 65536 + 17 * i) for i in range(4)]
+    comps = [oracle.lz4_compress(s)[1] for s in srcs]
+    so, off = [], 0
+    for c in comps:
+        so.append(off)
+        off = (off + len(c) + 64 + 15) & ~15
+    host = np.zeros(off + 64, dtype=np.uint8)
+    for c, o in zip(comps, so):
+        host[o:o + len(c)] = np.frombuffer(c, dtype=np.uint8)
+    src_t = torch.from_numpy(host).to(gpu)
+    caps = [len(s) for s in srcs]
+    do = [i * (70000 + 64) for i in range(len(srcs))]
+    dst_t = torch.full((do[-1] + 70000 + 64,), 0xEE, dtype=torch.uint8, device=gpu)
+    desc = D.make_desc(src_t, so, [len(c) for c in comps], dst_t, do, caps)
+    ret = torch.zeros(len(srcs), dtype=torch.int32, device=gpu)
+    # host copies claim much smaller inputs and outputs than the descriptors
+    D.lz4_split_counts(reset=True)
+    D.lz4_decompress_small(desc, ret, [64] * len(srcs), [1000] * len(srcs))
+    torch.cuda.synchronize()
+    assert ret.cpu().tolist() == caps
+    dh = dst_t.cpu().numpy()
+    for o, s in zip(do, srcs):
+        assert dh[o:o + len(s)].tobytes() == s
+    done, handed = D.lz4_split_counts()[:2]
+    assert handed == len(srcs), (done, handed)

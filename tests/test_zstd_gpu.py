@@ -128,9 +128,11 @@ def test_zstandard_decompress_contract(gpu, golden):
 
 
 def test_zstd_device_call_is_async_and_stream_safe(gpu, golden, frames_bin, oracle):
-    """jfs_zstd_decompress_device enqueues everything on the caller's stream
-    (no host wait): inputs the current scratch cannot hold answer -4 and fit
-    on the next call; two streams sharing the device scratch stay correct."""
+    """jfs_zstd_decompress_device enqueues the decode on the caller's stream;
+    after zscan/zplan it waits once for the planned scratch sizes and grows
+    the device scratch itself, so the result is always final (never a -4
+    "resubmit", jfs_gpucodec.h); two streams sharing the device scratch stay
+    correct."""
     import torch
     f = [e for e in golden["zstd"]["frames"] if e["size"] == 4 << 20][0]
     c = frames_bin[f["off"]:f["off"] + f["csize"]]
