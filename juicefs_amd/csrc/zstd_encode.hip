@@ -1,77 +1,513 @@
-// Zstd frame encoder for gfx950 -- one wavefront per input.
+// Zstd level-1 frame encoder for gfx950, byte-identical to libzstd's
+// ZSTD_compress(dst, cap, src, n, 1).
 //
-// Replaces ZSTD_compress(level 1) reached from pkg/compress/compress.go:82-91
-// (ZStandard.Compress -> zstd.CompressLevel(dst, src, ZSTD_LEVEL)).  The
-// reference pins DataDog/zstd v1.5.6, whose encoder is not available offline,
-// so byte parity with it is unpinnable; what this encoder
-// guarantees is an RFC 8878 frame that libzstd and the GPU decoder both turn
-// back into the input, no larger than ZSTD_COMPRESSBOUND (the capacity the Go
-// adapter requires), with the frame layout libzstd uses (FCS always present,
-// no checksum, no dictionary, raw blocks for incompressible data, smallest
-// literal-header format).
+// Replaces ZStandard.Compress (pkg/compress/compress.go:82-91 ->
+// zstd.CompressLevel(dst, src, 1) of github.com/DataDog/zstd).  The reference
+// pins v1.5.6, which is not available offline; the frames here are pinned to
+// libzstd 1.4.9 (the library of this image) through oracle/zstd_l1_oracle.c
+// and the committed fixtures.  The rules restated are
+// libzstd's: ZSTD_getCParams(1, n) + ZSTD_adjustCParams, ZSTD_compressBlock_fast
+// (two positions per step, repeat offset at +2, skip step (d >> 7) + 2),
+// ZSTD_compressBlock_internal (raw / RLE / compressed, repcode and entropy
+// confirmation), ZSTD_compressLiterals + HUF_compress (table reuse), and
+// ZSTD_entropyCompressSequences (FSE table choice, normalisation, bitstream).
 //
-// Per 128 KiB block:
-//   1. greedy LZ77 parse (4-byte hash of the position, table of 8192 positions
-//      in LDS, acceleration skip on misses like LZ4's, forward extension 64
-//      bytes per step across the wave, backward catch-up); literals go
-//      straight to the output, sequences to a per-input scratch list;
-//   2. literals section: Huffman-compressed (Compressed_Literals_Block, 4
-//      streams, code lengths <= 11, the tree description FSE-compressed or as
-//      direct 4-bit weights), RLE for one repeated byte, else raw -- whichever
-//      is smallest, like HUF_compress in libzstd;
-//   3. sequences section: Predefined_Mode for all three codes (no table
-//      descriptions), FSE-encoded backwards exactly as RFC 8878 section 4.1.2
-//      reads it (offsets are sent as offset + 3: no repeat codes);
-//   4. if that is not smaller than the block, the block is stored raw.
+// Three kernels per launch, the serial parts kept serial only where the format
+// makes them so:
+//   zl1_parse_kernel  one wave per FRAME: the greedy parse of every 128 KiB
+//                     block in order (the hash table and repeat offsets carry
+//                     across blocks); the hash table lives in LDS as 20-bit
+//                     window-relative entries (40 KiB: four frames per CU);
+//                     each search step tries the next 64 positions of the skip
+//                     schedule at once (one per lane) and keeps exactly the
+//                     serial loop's result.  Output: the blocks' sequences.
+//   zl1_seq_kernel    one wave per BLOCK: gathers the block's literals (and
+//                     their histograms per Huffman stream) and writes the
+//                     complete sequences section (FSE tables + bitstream).
+//   zl1_lit_kernel    one wave per FRAME, block after block: the literal
+//                     section (Huffman table build / reuse decision, exact
+//                     sizes), the raw / RLE / compressed choice, and the
+//                     block bytes written in place.
+// A block that ends up raw or RLE does not pass its repeat offsets on
+// (ZSTD_confirmRepcodesAndEntropyTables); the parse predicts that (RLE blocks
+// are known exactly, others are assumed compressed) and the literal kernel
+// checks the prediction: a frame whose wrong guess changed the offsets handed
+// to the next block is parsed again with the now known outcomes (the host
+// loop below; every pass settles at least one more block).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <cstring>
 #include <mutex>
+#include <vector>
 
 #include "jfs_internal.h"
 #include "wave.cuh"
 
 namespace jfs {
-namespace zstde {
+namespace zl1 {
 
-constexpr int32_t BLK = 128 << 10;          // Block_Maximum_Size
-constexpr int64_t SEQ_CAP = BLK / 4 + 64;   // sequences per block (every match is >= 4 bytes)
-constexpr int64_t LSTREAM = 36 << 10;       // one Huffman stream (<= 32 KiB of literals) in scratch
-constexpr int64_t SCR_PER = SEQ_CAP * 8 + 4 * LSTREAM;  // scratch bytes per input
-constexpr int HUF_MAXB = 11;                // code length limit (HUF_TABLELOG_DEFAULT)
-constexpr int HUF_MINL = 64;                // fewer literals stay raw
-#ifndef JFS_ZE_HBITS
-#define JFS_ZE_HBITS 13  // libzstd level 1 for inputs > 256 KiB: hashLog 13
-#endif
-constexpr int32_t HBITS = JFS_ZE_HBITS;     // hash table: 2^HBITS positions in LDS
+constexpr int32_t BLK = 128 << 10;  // ZSTD_BLOCKSIZE_MAX
 
-#ifdef JFS_PROF
-// diagnostic build only: per-phase s_memtime sums of the encoder waves
-// (0 parse, 1 literal histogram + Huffman build, 2 Huffman streams, 3 literal
-// section writes, 4 sequence tables, 5 sequence bitstream, 6 block header /
-// raw fallback; 8 blocks, 9 sequences)
-__device__ unsigned long long g_zeprof[12];
-#define ZE_DECL uint64_t ze_t = __builtin_amdgcn_s_memtime(), ze_acc[12] = {0};
-#define ZE(k) do { const uint64_t x_ = __builtin_amdgcn_s_memtime(); ze_acc[k] += x_ - ze_t; ze_t = x_; } while (0)
-#define ZEC(k, n) (ze_acc[k] += (n))
-#define ZE_FLUSH() do { if (lane_id() == 0) for (int i_ = 0; i_ < 12; ++i_) atomicAdd(&g_zeprof[i_], (unsigned long long)ze_acc[i_]); } while (0)
-#else
-#define ZE_DECL
-#define ZE(k) do { } while (0)
-#define ZEC(k, n) do { } while (0)
-#define ZE_FLUSH() do { } while (0)
-#endif
+// ---------------------------------------------------------------------------
+// parameters: ZSTD_getCParams(1, n, 0) (level-1 row of the size tier, then
+// ZSTD_adjustCParams_internal); strategy fast, targetLength 0 (step 2)
+// ---------------------------------------------------------------------------
+struct Params {
+    uint32_t wlog, hlog, mls;
+};
+__host__ __device__ inline uint32_t hbit(uint32_t v) { return 31u - (uint32_t)__builtin_clz(v); }
+__host__ __device__ inline Params params_of(int64_t n) {
+    Params p;
+    if (n > (256 << 10)) { p.wlog = 19; p.hlog = 14; p.mls = 7; }
+    else if (n > (128 << 10)) { p.wlog = 18; p.hlog = 14; p.mls = 6; }
+    else if (n > (16 << 10)) { p.wlog = 17; p.hlog = 13; p.mls = 6; }
+    else { p.wlog = 14; p.hlog = 15; p.mls = 5; }
+    const uint32_t t = (uint32_t)n;
+    const uint32_t srclog = t < 64 ? 6u : hbit(t - 1) + 1;
+    if (p.wlog > srclog) p.wlog = srclog;
+    if (p.hlog > p.wlog + 1) p.hlog = p.wlog + 1;
+    if (p.wlog < 10) p.wlog = 10;
+    return p;
+}
+__host__ __device__ inline int64_t zbound(int64_t n) { return n + (n >> 8) + (n < BLK ? (BLK - n) >> 11 : 0); }
 
-// RFC 8878 3.1.1.3.2.1 code tables and 3.1.1.3.2.2 predefined distributions
-__constant__ uint32_t LL_BASE[36] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,   10,  11,  12,   13,   14,   15,    16,    18,
-                                     20, 22, 24, 28, 32, 40, 48, 64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536};
+// per frame / per block records (host-built, device-updated)
+struct FInfo {
+    const uint8_t *src;
+    uint8_t *dst;
+    int32_t n, cap;
+    int32_t nb, b0;  // blocks, index of the first in the block array
+    uint32_t wlog, hlog, mls;
+    int32_t status;  // 0 done, 1 parse again (a confirmation guess was wrong), -2 dst too small
+};
+enum : int32_t { F_NOCOMP = 1, F_RLE = 2, F_ASSUMED = 4, F_LASTNC = 8 };
+struct BInfo {
+    int64_t seq_off;  // u64 records in the sequence scratch
+    int64_t lit_off;  // bytes: literals (bsz), then the sequences section (bsz + 512)
+    int32_t frame, bs, be;
+    int32_t ns, nl;                    // sequences, literals
+    uint32_t rin0, rin1, rout0, rout1;  // repeat offsets in / out (offset_1, offset_2)
+    int32_t flags;
+    int32_t conf;   // outcome known from an earlier pass: 0 unknown, 1 confirmed, 2 not
+    int32_t secsz;  // sequences section bytes, -1 = larger than the block
+};
+constexpr int64_t SEC_EXTRA = 512;
+__host__ __device__ inline int64_t seq_cap(int32_t bsz) { return bsz / 4 + 4; }
+
+// sequence record: ll | mlb << 17 | Offset_Value << 34
+__device__ __forceinline__ uint64_t seq_pack(uint32_t ll, uint32_t mlb, uint32_t ofv) {
+    return (uint64_t)ll | ((uint64_t)mlb << 17) | ((uint64_t)ofv << 34);
+}
+
+// ---------------------------------------------------------------------------
+// source access: aligned dword loads that never touch a dword holding no input
+// byte (so never a page the input does not reach), bytes past the end read 0
+// ---------------------------------------------------------------------------
+struct Src {
+    const gc_u32 *w;
+    uint32_t sh;
+    int32_t nw;  // dwords holding at least one input byte
+    const gc_u8 *b;
+};
+__device__ __forceinline__ Src make_src(const uint8_t *p, int32_t n) {
+    Src s;
+    s.w = (const gc_u32 *)((uintptr_t)p & ~(uintptr_t)3);
+    s.sh = (uint32_t)((uintptr_t)p & 3u);
+    s.nw = n > 0 ? (int32_t)((n - 1 + s.sh) >> 2) + 1 : 0;
+    s.b = (const gc_u8 *)p;
+    return s;
+}
+__device__ __forceinline__ uint32_t wd(const Src &S, int32_t i) { return (i >= 0 && i < S.nw) ? S.w[i] : 0u; }
+// 4 bytes at position p (p may be negative / past the end: those bytes read as 0)
+__device__ __forceinline__ uint32_t ld32(const Src &S, int32_t p) {
+    const int32_t b = p + (int32_t)S.sh;
+    const int32_t i = b >> 2;
+    const uint32_t s = (uint32_t)b & 3u;
+    const uint32_t w0 = wd(S, i), w1 = wd(S, i + 1);
+    return __builtin_amdgcn_alignbyte(w1, w0, s);
+}
+__device__ __forceinline__ uint64_t ld64(const Src &S, int32_t p) {
+    const int32_t b = p + (int32_t)S.sh;
+    const int32_t i = b >> 2;
+    const uint32_t s = (uint32_t)b & 3u;
+    const uint32_t w0 = wd(S, i), w1 = wd(S, i + 1), w2 = wd(S, i + 2);
+    return (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, s) | ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, s) << 32);
+}
+// 16 bytes at position p
+__device__ __forceinline__ uint4 ld128(const Src &S, int32_t p) {
+    const int32_t b = p + (int32_t)S.sh;
+    const int32_t i = b >> 2;
+    const uint32_t s = (uint32_t)b & 3u;
+    const uint32_t w0 = wd(S, i), w1 = wd(S, i + 1), w2 = wd(S, i + 2), w3 = wd(S, i + 3), w4 = wd(S, i + 4);
+    uint4 r;
+    r.x = __builtin_amdgcn_alignbyte(w1, w0, s);
+    r.y = __builtin_amdgcn_alignbyte(w2, w1, s);
+    r.z = __builtin_amdgcn_alignbyte(w3, w2, s);
+    r.w = __builtin_amdgcn_alignbyte(w4, w3, s);
+    return r;
+}
+
+// ZSTD_hashPtr for minMatch 5 / 6 / 7 of the 8 little-endian bytes at a position
+__device__ __forceinline__ uint32_t zhash(uint64_t v, uint32_t hlog, uint32_t mls) {
+    const uint64_t prime = mls == 5 ? 889523592379ull : mls == 6 ? 227718039650203ull : 58295818150454627ull;
+    return (uint32_t)(((v << (64 - 8 * mls)) * prime) >> (64 - hlog));
+}
+
+__device__ __forceinline__ uint64_t ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ int ctz64(uint64_t m) { return m ? __builtin_ctzll(m) : 64; }
+
+// ---------------------------------------------------------------------------
+// hash table in LDS.  Entries hold index = position + 1 (0 = empty).  WIDE
+// tables keep 20 bits (16 in lo[], 4 in a nibble array) and decode relative to
+// the block end R: the entry is the unique index = e (mod 2^20) in
+// (R - 2^20, R].  Entries that fall out of the 2^wlog window are rewritten as
+// the window's lowest index at each block start, so every live entry is
+// within 640 KiB of R and decodes exactly.  Narrow tables (frames < 64 KiB)
+// keep the whole index in 16 bits.
+// ---------------------------------------------------------------------------
+template <bool WIDE>
+struct Tab {
+    uint16_t *lo;
+    uint32_t *hi;
+    __device__ __forceinline__ uint32_t raw(uint32_t h) const {
+        return WIDE ? (uint32_t)lo[h] | (((hi[h >> 3] >> ((h & 7) * 4)) & 15u) << 16) : (uint32_t)lo[h];
+    }
+    __device__ __forceinline__ uint32_t get(uint32_t h, uint32_t R) const {
+        const uint32_t e = raw(h);
+        return WIDE ? R - ((R - e) & 0xFFFFFu) : e;
+    }
+    __device__ __forceinline__ void put(uint32_t h, uint32_t idx) {
+        lo[h] = (uint16_t)idx;
+        if (WIDE) {
+            const uint32_t sh = (h & 7) * 4;
+            const uint32_t nv = ((idx >> 16) & 15u) << sh;
+            const uint32_t cur = hi[h >> 3];
+            if (((cur >> sh) & 15u) != ((idx >> 16) & 15u)) {
+                atomicAnd(&hi[h >> 3], ~(15u << sh));
+                atomicOr(&hi[h >> 3], nv);
+            }
+        }
+    }
+};
+
+// ---------------------------------------------------------------------------
+// byte compares (wave-parallel)
+// ---------------------------------------------------------------------------
+// count of i in [0, lim) with s[a + i] == s[b + i] before the first mismatch
+__device__ int32_t fwd_count(const Src &S, int32_t a, int32_t b, int32_t lim) {
+    const int l = lane_id();
+    if (lim <= 0) return 0;
+    {
+        bool eq = false;
+        if (l < lim) eq = S.b[a + l] == S.b[b + l];
+        const int r = ctz64(~ballot(eq));
+        if (r < 64) return r;
+    }
+    int32_t m = 64;
+    for (int guard = 0; guard < 256 && m < lim; guard++) {
+        const int32_t o = m + 16 * l;
+        uint32_t d = 16;  // first differing byte of this lane's 16 (16: none)
+        if (o < lim) {
+            const uint4 x = ld128(S, a + o), y = ld128(S, b + o);
+            const uint32_t e0 = x.x ^ y.x, e1 = x.y ^ y.y, e2 = x.z ^ y.z, e3 = x.w ^ y.w;
+            d = e0 ? (uint32_t)__builtin_ctz(e0) >> 3
+                   : e1 ? 4 + ((uint32_t)__builtin_ctz(e1) >> 3)
+                        : e2 ? 8 + ((uint32_t)__builtin_ctz(e2) >> 3) : e3 ? 12 + ((uint32_t)__builtin_ctz(e3) >> 3) : 16u;
+            if ((int32_t)d > lim - o) d = (uint32_t)(lim - o);
+        } else {
+            d = 0;
+        }
+        const int f = ctz64(~ballot(d == 16));
+        if (f < 64) return m + 16 * f + (int32_t)readlane(d, f);
+        m += 1024;
+    }
+    return lim < m ? lim : m;
+}
+// count of i in [0, lim) with s[a - 1 - i] == s[b - 1 - i] before the first mismatch
+__device__ int32_t back_count(const Src &S, int32_t a, int32_t b, int32_t lim) {
+    const int l = lane_id();
+    int32_t m = 0;
+    for (int guard = 0; guard < 4096 && m < lim; guard++) {
+        const int32_t k = m + l;
+        bool eq = false;
+        if (k < lim) eq = S.b[a - 1 - k] == S.b[b - 1 - k];
+        const int r = ctz64(~ballot(eq));
+        if (r < 64) return m + r;
+        m += 64;
+    }
+    return lim < m ? lim : m;
+}
+
+// step-schedule position of search iteration l from ip0 (ZSTD_compressBlock_fast:
+// ip += ((ip - anchor) >> 7) + 2 on a miss)
+__device__ __forceinline__ int32_t sched_pos(int32_t ip0, int32_t anchor, uint32_t l) {
+    uint32_t d = (uint32_t)(ip0 - anchor), r = l;
+    for (int guard = 0; guard < 80 && ballot(r > 0); guard++) {
+        if (r > 0) {
+            const uint32_t k = d >> 7, st = k + 2, rem = ((k + 1) << 7) - d;
+            uint32_t c = 1;
+            if (st < rem) {
+                c = (uint32_t)((float)rem * __builtin_amdgcn_rcpf((float)st));
+                c += (c * st < rem);
+                c += (c * st < rem);
+                c -= (c > 1 && (c - 1) * st >= rem);
+            }
+            const uint32_t t = r < c ? r : c;
+            d += t * st;
+            r -= t;
+        }
+    }
+    return anchor + (int32_t)d;
+}
+
+// all bytes of [a, b) equal (ZSTD_isRLE)
+__device__ bool all_equal(const Src &S, int32_t a, int32_t b) {
+    const int l = lane_id();
+    const uint32_t c = S.b[a];
+    const uint32_t c4 = c * 0x01010101u;
+    for (int32_t p0 = a; p0 < b; p0 += 1024) {
+        const int32_t p = p0 + 16 * l;
+        bool bad = false;
+        if (p < b) {
+            const uint4 x = ld128(S, p);
+            const int32_t k = b - p;  // valid bytes of the 16
+            const uint32_t v[4] = {x.x ^ c4, x.y ^ c4, x.z ^ c4, x.w ^ c4};
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int32_t vb = k - 4 * i;
+                const uint32_t m = vb >= 4 ? 0xFFFFFFFFu : vb <= 0 ? 0u : (0xFFFFFFFFu >> (32 - 8 * vb));
+                bad |= (v[i] & m) != 0;
+            }
+        }
+        if (ballot(bad)) return false;
+    }
+    return true;
+}
+
+// ---------------------------------------------------------------------------
+// kernel 1: the parse (one wave per frame)
+// ---------------------------------------------------------------------------
+template <bool WIDE>
+__global__ __launch_bounds__(64) void zl1_parse_kernel(const FInfo *__restrict__ fi, const int32_t *__restrict__ flist,
+                                                       BInfo *__restrict__ bi, uint64_t *__restrict__ seqs) {
+    extern __shared__ uint32_t smem[];
+    const int l = lane_id();
+    const FInfo F = fi[flist[blockIdx.x]];
+    if (F.status < 0) return;
+    const uint32_t hlog = F.hlog, mls = F.mls, tsize = 1u << hlog;
+    const int32_t maxDist = 1 << F.wlog;
+    Tab<WIDE> T;
+    T.lo = (uint16_t *)smem;
+    T.hi = smem + (tsize >> 1);
+    for (uint32_t k = l; k < (tsize >> 1); k += 64) smem[k] = 0;
+    if (WIDE)
+        for (uint32_t k = l; k < (tsize >> 3); k += 64) T.hi[k] = 0;
+    __syncthreads();
+    const Src S = make_src(F.src, F.n);
+    uint32_t off1 = 1, off2 = 4;  // repStartValue
+    for (int32_t k = 0; k < F.nb; k++) {
+        BInfo &B = bi[F.b0 + k];
+        const int32_t bs = B.bs, be = B.be;
+        const uint32_t rin0 = off1, rin1 = off2;
+        if (be - bs < 7) {  // ZSTD_buildSeqStore: too small to compress, match state untouched
+            if (l == 0) {
+                B.ns = 0;
+                B.nl = be - bs;
+                B.rin0 = rin0; B.rin1 = rin1; B.rout0 = rin0; B.rout1 = rin1;
+                B.flags = F_NOCOMP;
+            }
+            continue;
+        }
+        const bool rle = k > 0 && all_equal(S, bs, be);
+        const int32_t prefixPos = be > maxDist ? be - maxDist : 0;
+        const uint32_t prefixIdx = (uint32_t)prefixPos + 1, R = (uint32_t)be;
+        if (WIDE && prefixPos > 0) {  // entries that left the window: the window's lowest index
+            __syncthreads();
+            for (uint32_t h = l; h < tsize; h += 64)
+                if (T.get(h, R) <= prefixIdx) T.put(h, prefixIdx);
+            __syncthreads();
+        }
+        // ---- ZSTD_compressBlock_fast_generic
+        uint64_t *sq = seqs + B.seq_off;
+        const int32_t ilimit = be - 8;
+        int32_t ip0 = bs, anchor = bs, ns = 0, nl = 0;
+        uint32_t o1 = off1, o2 = off2, saved = 0;
+        if (ip0 == prefixPos) ip0++;
+        {
+            const uint32_t maxRep = (uint32_t)(ip0 > maxDist ? maxDist : ip0);
+            if (o2 > maxRep) { saved = o2; o2 = 0; }
+            if (o1 > maxRep) { saved = o1; o1 = 0; }
+        }
+        int pend = 0;  // 1: after a search match (insert ip0-2, then the repeat loop); 2: after a repeat-loop match
+        for (int guard = 0; guard < 4 * BLK; guard++) {
+            // positions of this search step (after a match: ip0 + 2 l)
+            const int32_t q = pend ? ip0 + 2 * l : sched_pos(ip0, anchor, (uint32_t)l);
+            const bool on = q + 1 < ilimit;
+            const bool ld = on || (pend && l == 0 && ip0 <= ilimit);
+            uint4 W = make_uint4(0, 0, 0, 0);  // bytes [q - 2, q + 14)
+            uint64_t rw = 0;                   // bytes [q + 1 - o1, q + 9 - o1)
+            uint32_t r2 = 0;                   // (lane 0, pend) 4 bytes at ip0 - o2
+            if (ld) {
+                W = ld128(S, q - 2);
+                if (o1 > 0) rw = ld64(S, q + 1 - (int32_t)o1);
+                if (pend && l == 0 && o2 > 0) r2 = ld32(S, ip0 - (int32_t)o2);
+            }
+            const uint64_t v0 = (uint64_t)__builtin_amdgcn_alignbyte(W.y, W.x, 2) | ((uint64_t)__builtin_amdgcn_alignbyte(W.z, W.y, 2) << 32);
+            const uint64_t v1 = (uint64_t)__builtin_amdgcn_alignbyte(W.y, W.x, 3) | ((uint64_t)__builtin_amdgcn_alignbyte(W.z, W.y, 3) << 32);
+            const uint32_t val0 = (uint32_t)v0, val1 = (uint32_t)v1, val2 = W.y;
+            const uint32_t h0 = zhash(v0, hlog, mls), h1 = zhash(v1, hlog, mls);
+            if (pend) {
+                const uint32_t cur = readlane(val0, 0);  // 4 bytes at ip0
+                if (pend == 1) {  // hashTable[hash(ip0 - 2)] = ip0 - 2
+                    const uint64_t vm2 = (uint64_t)W.x | ((uint64_t)W.y << 32);
+                    const uint32_t hm2 = readlane(zhash(vm2, hlog, mls), 0);
+                    if (l == 0) T.put(hm2, (uint32_t)(ip0 - 2 + 1));
+                    __syncthreads();
+                }
+                pend = 0;
+                if (o2 > 0 && ip0 <= ilimit && cur == readlane(r2, 0)) {
+                    // repeat-offset match at ip0 (offset_2), then swap
+                    const int32_t rl = 4 + fwd_count(S, ip0 + 4, ip0 + 4 - (int32_t)o2, be - (ip0 + 4));
+                    const uint32_t t = o2;
+                    o2 = o1;
+                    o1 = t;
+                    if (l == 0) T.put(readlane(h0, 0), (uint32_t)(ip0 + 1));
+                    __syncthreads();
+                    if (l == 0) sq[ns] = seq_pack(0, (uint32_t)(rl - 3), 1);
+                    ns++;
+                    ip0 += rl;
+                    anchor = ip0;
+                    if (ip0 <= ilimit) pend = 2;
+                    continue;
+                }
+            }
+            const uint64_t onm = ballot(on);
+            if (!onm) break;  // ip1 >= ilimit: no more positions in this block
+            const int non = 64 - __builtin_clzll(onm);  // lanes [0, non) are on
+            // table reads (before any write of this step), then tags to find
+            // lanes sharing a bucket
+            uint32_t olo0 = 0, olo1 = 0, i0 = 0, i1 = 0;
+            if (on) {
+                olo0 = T.lo[h0];
+                olo1 = T.lo[h1];
+                i0 = T.get(h0, R);
+                i1 = T.get(h1, R);
+            }
+            __syncthreads();
+            if (on) {
+                T.lo[h0] = (uint16_t)l;
+                T.lo[h1] = (uint16_t)l;
+            }
+            __syncthreads();
+            uint32_t cm = 64;
+            if (on) {
+                const uint32_t t0 = T.lo[h0], t1 = T.lo[h1];
+                if (t0 != (uint32_t)l) cm = umin32((uint32_t)l, t0);
+                if (t1 != (uint32_t)l) cm = umin32(cm, umin32((uint32_t)l, t1));
+            }
+            const int cut = (int)dwave_min(cm) + 1;
+            const int nbt = cut < non ? cut : non;  // lanes [0, nbt) read exactly what the serial loop reads
+            const bool dec = l < nbt;
+            const bool rep = dec && o1 > 0 && (uint32_t)(rw >> 8) == val2;
+            const bool c0 = dec && i0 > prefixIdx, c1 = dec && i1 > prefixIdx;
+            uint32_t m0 = 0, m1 = 0;
+            if (c0) m0 = ld32(S, (int32_t)i0 - 1);
+            if (c1) m1 = ld32(S, (int32_t)i1 - 1);
+            const bool k0 = c0 && m0 == val0, k1 = c1 && m1 == val1;
+            const int j = ctz64(ballot(rep || k0 || k1));
+            // lanes after the first hit (and past the cut) put their buckets
+            // back; then the lanes up to the hit insert ip0 and ip1
+            __syncthreads();
+            if (on && (l >= nbt || l > j)) {
+                T.lo[h0] = (uint16_t)olo0;
+                T.lo[h1] = (uint16_t)olo1;
+            }
+            __syncthreads();
+            if (on && l < nbt && l <= j) {
+                T.put(h0, (uint32_t)q + 1);
+                T.put(h1, (uint32_t)q + 2);
+            }
+            __syncthreads();
+            if (j >= 64) {
+                const int32_t ql = (int32_t)readlane((uint32_t)q, nbt - 1);
+                ip0 = ql + ((ql - anchor) >> 7) + 2;
+                continue;
+            }
+            // ---- a match at iteration j
+            const int32_t qj = (int32_t)readlane((uint32_t)q, j);
+            const bool jrep = readlane(rep ? 1u : 0u, j) != 0, jk0 = readlane(k0 ? 1u : 0u, j) != 0;
+            const uint32_t h2 = zhash((uint64_t)W.y | ((uint64_t)W.z << 32), hlog, mls);  // hash at q + 2
+            const uint32_t jh2 = readlane(h2, j);
+            int32_t start, mst, mlen;
+            uint32_t ofv;
+            if (jrep) {
+                const uint32_t bq1 = readlane(W.x >> 24, j), brp = readlane((uint32_t)rw & 0xFFu, j);
+                const int32_t ml0 = bq1 == brp ? 1 : 0;
+                start = qj + 2 - ml0;
+                mst = start - (int32_t)o1;
+                mlen = 4 + ml0;
+                ofv = 1;
+            } else {
+                start = jk0 ? qj : qj + 1;
+                mst = (int32_t)readlane(jk0 ? i0 : i1, j) - 1;
+                o2 = o1;
+                o1 = (uint32_t)(start - mst);
+                ofv = o1 + 3;
+                mlen = 4;
+                const int32_t lim = umin32((uint32_t)(start - anchor), (uint32_t)(mst - prefixPos));
+                const int32_t bk = back_count(S, start, mst, lim);
+                start -= bk;
+                mst -= bk;
+                mlen += bk;
+            }
+            mlen += fwd_count(S, start + mlen, mst + mlen, be - (start + mlen));
+            if (l == 0) sq[ns] = seq_pack((uint32_t)(start - anchor), (uint32_t)(mlen - 3), ofv);
+            ns++;
+            nl += start - anchor;
+            ip0 = start + mlen;
+            anchor = ip0;
+            if (ip0 <= ilimit) {
+                if (l == 0) T.put(jh2, (uint32_t)(qj + 2 + 1));  // hashTable[hash(current0 + 2)]
+                __syncthreads();
+                pend = 1;
+            }
+        }
+        nl += be - anchor;
+        const uint32_t ro0 = o1 ? o1 : saved, ro1 = o2 ? o2 : saved;
+        const bool assumed = B.conf ? B.conf == 1 : !rle;
+        if (l == 0) {
+            B.ns = ns;
+            B.nl = nl;
+            B.rin0 = rin0; B.rin1 = rin1; B.rout0 = ro0; B.rout1 = ro1;
+            B.flags = (rle ? F_RLE : 0) | (assumed ? F_ASSUMED : 0);
+        }
+        if (assumed) {
+            off1 = ro0;
+            off2 = ro1;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// FSE / Huffman tables (FSE_buildCTable_wksp, FSE_normalizeCount,
+// FSE_writeNCount, HUF_buildCTable_wksp, HUF_writeCTable) -- serial, lane 0
+// ---------------------------------------------------------------------------
 __constant__ uint8_t LL_BITS[36] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,  0,  1,  1,
                                     1, 1, 2, 2, 3, 3, 4, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
-__constant__ uint32_t ML_BASE[53] = {3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13,  14,  15,  16,   17,   18,   19,   20,
-                                     21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31,  32,  33,  34,   35,   37,   39,   41,
-                                     43, 47, 51, 59, 67, 83, 99, 131, 259, 515, 1027, 2051, 4099, 8195, 16387, 32771, 65539};
-__constant__ uint8_t ML_BITS[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,  0,  0,  0,  0,  0,  0,  0,  0,  0, 0,
+__constant__ uint8_t ML_BITS[53] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
                                     0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 3, 3, 4, 4, 5, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16};
+__constant__ uint8_t LL_CODE[64] = {0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15,
+                                    16, 16, 17, 17, 18, 18, 19, 19, 20, 20, 20, 20, 21, 21, 21, 21,
+                                    22, 22, 22, 22, 22, 22, 22, 22, 23, 23, 23, 23, 23, 23, 23, 23,
+                                    24, 24, 24, 24, 24, 24, 24, 24, 24, 24, 24, 24, 24, 24, 24, 24};
+__constant__ uint8_t ML_CODE[128] = {
+    0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25,
+    26, 27, 28, 29, 30, 31, 32, 32, 33, 33, 34, 34, 35, 35, 36, 36, 36, 36, 37, 37, 37, 37, 38, 38, 38, 38,
+    38, 38, 38, 38, 39, 39, 39, 39, 39, 39, 39, 39, 40, 40, 40, 40, 40, 40, 40, 40, 40, 40, 40, 40, 40, 40,
+    40, 40, 41, 41, 41, 41, 41, 41, 41, 41, 41, 41, 41, 41, 41, 41, 41, 41, 42, 42, 42, 42, 42, 42, 42, 42,
+    42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42, 42};
 __constant__ int16_t LL_DEF[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2,
                                    2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1, 1, 1, -1, -1, -1, -1};
 __constant__ int16_t ML_DEF[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1,
@@ -80,308 +516,133 @@ __constant__ int16_t ML_DEF[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 
 __constant__ int16_t OF_DEF[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1,
                                    1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
 
-// FSE compression table (FSE_buildCTable semantics) of one code type; N =
-// state-table capacity (512 for a block's own tables, 64 for the predefined
-// and Huffman-weight tables, table log <= 6)
-template <int N>
-struct CTabN {
-    uint16_t st[N];    // state table: tableSize + spread position, by cumulative symbol rank
-    int32_t dnb[53];   // deltaNbBits
-    int16_t dfs[53];   // deltaFindState (|.| <= 512)
-};
-typedef CTabN<512> CTab;
-typedef CTabN<64> CTab64;
-// read view of either size
-struct CView {
-    const uint16_t *st;
-    const int32_t *dnb;
-    const int16_t *dfs;
-};
-template <int N>
-__device__ __forceinline__ CView cview(const CTabN<N> &t) { return CView{t.st, t.dnb, t.dfs}; }
+__device__ __forceinline__ uint32_t ll_code(uint32_t ll) { return ll > 63 ? hbit(ll) + 19 : LL_CODE[ll]; }
+__device__ __forceinline__ uint32_t ml_code(uint32_t mlb) { return mlb > 127 ? hbit(mlb) + 36 : ML_CODE[mlb]; }
 
-// Huffman literal coding state of the current block (lane 0 builds, lanes 0-3 encode)
-struct HufSmem {
-    uint32_t cnt[256];
-    union {
-        uint32_t w[512];  // tree node weights (leaves 0..n-1, sorted by count; huf_build)
-        struct {          // the tree description's FSE table (huf_describe)
-            CTab64 wct;   // Huffman weights (log 6)
-            uint8_t tsym[512];
-            int32_t cumul[64];
-        } d;
-    };
-    uint16_t par[512];
-    uint8_t dep[512];
-    uint16_t sym[256];  // leaf -> symbol
-    uint16_t code[256];
-    uint8_t len[256];
-    uint8_t wt[256];    // Huffman weights of symbols 0..maxsym
-    int16_t norm[16];   // FSE normalized counts of the weights
-    uint8_t hdr[192];   // tree description (header byte first)
-    int32_t hsize, maxbits, maxsym, nsym;
-    int32_t ssz[4];     // stream sizes
+// FSE encoding table; N = state capacity
+template <int N, int NS>
+struct CTab {
+    uint16_t st[N];
+    int32_t dnb[NS];
+    int16_t dfs[NS];
+    int32_t tlog;
 };
 
-// Sequence-table state of the current block (after its literals are written)
-struct SeqSmem {
-    CTab act[3];           // FSE_Compressed tables (LL, ML, OF)
-    uint32_t scnt[3][64];  // code histograms of the block's sequences
-    int16_t snorm[3][64];
-    uint8_t shdr[3][96];   // their normalized-count headers
-    uint8_t tsym[512];     // build_ctab scratch
-    int32_t cumul[64];
-};
+__device__ uint32_t fse_min_tlog(uint32_t src, uint32_t maxsv) {
+    const uint32_t a = hbit(src) + 1, b = hbit(maxsv) + 2;
+    return a < b ? a : b;
+}
+__device__ uint32_t fse_opt_tlog(uint32_t maxtl, uint32_t src, uint32_t maxsv, uint32_t minus) {
+    const uint32_t maxBitsSrc = hbit(src - 1) - minus;
+    uint32_t tl = maxtl;
+    const uint32_t minBits = fse_min_tlog(src, maxsv);
+    if (maxBitsSrc < tl) tl = maxBitsSrc;
+    if (minBits > tl) tl = minBits;
+    if (tl < 5) tl = 5;
+    if (tl > 12) tl = 12;
+    return tl;
+}
 
-// <= 40 KiB: four inputs (waves) per CU
-struct Smem {
-    uint32_t table[1 << HBITS];
-    CTab64 ct[3];  // 0 LL (log 6), 1 ML (log 6), 2 OF (log 5)
-    uint8_t lut_ll[64], lut_ml[128];
-    int32_t shsz[3], smode[3], slog[3];
-    union {  // a block's literal coding, then its sequence tables
-        HufSmem h;
-        SeqSmem q;
-    };
-};
-static_assert(sizeof(Smem) <= 40960, "four encoder waves per CU");
-
-__device__ __forceinline__ uint32_t highbit(uint32_t v) { return 31u - (uint32_t)__builtin_clz(v); }
-
-// Build the encoding table of a predefined distribution (lane 0 writes).
-// Spread and state numbering are the decoder's (FSE_buildDTable): -1
-// ("less than 1") symbols at the top, the others spread with step
-// (size>>1)+(size>>3)+3 skipping the top; state table in symbol order.
-template <int N>
-__device__ void build_ctab(uint8_t *tsym, int32_t *cumul, CTabN<N> &t, const int16_t *norm, int maxsv, int tlog) {
-    if (lane_id() == 0) {
-        const int size = 1 << tlog, mask = size - 1, step = (size >> 1) + (size >> 3) + 3;
-        int high = size - 1;
-        cumul[0] = 0;
-        for (int u = 1; u <= maxsv + 1; u++) {
-            if (norm[u - 1] == -1) {
-                cumul[u] = cumul[u - 1] + 1;
-                tsym[high--] = (uint8_t)(u - 1);
-            } else {
-                cumul[u] = cumul[u - 1] + norm[u - 1];
-            }
-        }
-        int pos = 0;
-        for (int sym = 0; sym <= maxsv; sym++) {
-            for (int k = 0; k < norm[sym]; k++) {
-                tsym[pos] = (uint8_t)sym;
-                do { pos = (pos + step) & mask; } while (pos > high);
-            }
-        }
-        for (int u = 0; u < size; u++) {
-            const int sym = tsym[u];
-            t.st[cumul[sym]++] = (uint16_t)(size + u);
-        }
-        int total = 0;
-        for (int sym = 0; sym <= maxsv; sym++) {
-            const int nc = norm[sym];
-            if (nc == 0) {
-                t.dnb[sym] = ((tlog + 1) << 16) - size;
-                t.dfs[sym] = 0;
-            } else if (nc == -1 || nc == 1) {
-                t.dnb[sym] = (tlog << 16) - size;
-                t.dfs[sym] = total - 1;
-                total += 1;
-            } else {
-                const int mbo = tlog - (int)highbit((uint32_t)(nc - 1));
-                t.dnb[sym] = (mbo << 16) - (nc << mbo);
-                t.dfs[sym] = total - nc;
-                total += nc;
+__device__ int fse_norm_m2(int16_t *norm, uint32_t tlog, const uint32_t *count, uint32_t total, uint32_t maxsv,
+                           int16_t lowProb) {
+    const int16_t NYA = -2;
+    uint32_t s, distributed = 0, toDist;
+    const uint32_t lowThreshold = total >> tlog;
+    uint32_t lowOne = (uint32_t)(((uint64_t)total * 3) >> (tlog + 1));
+    for (s = 0; s <= maxsv; s++) {
+        if (count[s] == 0) { norm[s] = 0; continue; }
+        if (count[s] <= lowThreshold) { norm[s] = lowProb; distributed++; total -= count[s]; continue; }
+        if (count[s] <= lowOne) { norm[s] = 1; distributed++; total -= count[s]; continue; }
+        norm[s] = NYA;
+    }
+    toDist = (1u << tlog) - distributed;
+    if (toDist == 0) return 0;
+    if ((total / toDist) > lowOne) {
+        lowOne = (uint32_t)(((uint64_t)total * 3) / (toDist * 2));
+        for (s = 0; s <= maxsv; s++)
+            if (norm[s] == NYA && count[s] <= lowOne) { norm[s] = 1; distributed++; total -= count[s]; }
+        toDist = (1u << tlog) - distributed;
+    }
+    if (distributed == maxsv + 1) {
+        uint32_t maxV = 0, maxC = 0;
+        for (s = 0; s <= maxsv; s++)
+            if (count[s] > maxC) { maxV = s; maxC = count[s]; }
+        norm[maxV] = (int16_t)(norm[maxV] + (int16_t)toDist);
+        return 0;
+    }
+    if (total == 0) {
+        for (s = 0; toDist > 0; s = (s + 1) % (maxsv + 1))
+            if (norm[s] > 0) { toDist--; norm[s]++; }
+        return 0;
+    }
+    {
+        const uint64_t vStepLog = 62 - tlog;
+        const uint64_t mid = (1ull << (vStepLog - 1)) - 1;
+        const uint64_t rStep = ((((uint64_t)1 << vStepLog) * toDist) + mid) / total;
+        uint64_t tmpTotal = mid;
+        for (s = 0; s <= maxsv; s++) {
+            if (norm[s] == NYA) {
+                const uint64_t end = tmpTotal + (count[s] * rStep);
+                const uint32_t sStart = (uint32_t)(tmpTotal >> vStepLog), sEnd = (uint32_t)(end >> vStepLog);
+                const uint32_t weight = sEnd - sStart;
+                if (weight < 1) return -1;
+                norm[s] = (int16_t)weight;
+                tmpTotal = end;
             }
         }
     }
+    return 0;
 }
 
-// ---------------------------------------------------------------------------
-// byte access (the input is read-only; uniform addresses)
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t ld32u(const gc_u8 *p) {
-    const uintptr_t a = (uintptr_t)p;
-    const gc_u32 *w = (const gc_u32 *)(a & ~(uintptr_t)3);
-    const uint32_t sh = (uint32_t)(a & 3);
-    const uint32_t w0 = w[0];
-    if (sh == 0) return w0;
-    return __builtin_amdgcn_alignbyte(w[1], w0, sh);
-}
-
-__device__ __forceinline__ uint32_t hash4(uint32_t v) { return (v * 2654435761u) >> (32 - HBITS); }
-// ZSTD_hash6Ptr: the low 6 bytes of an 8-byte little-endian read
-__device__ __forceinline__ uint32_t hash6(uint64_t v) { return (uint32_t)(((v << 16) * 227718039650203ull) >> (64 - HBITS)); }
-__device__ __forceinline__ uint64_t ld64u(const gc_u8 *p) {
-    const uintptr_t a = (uintptr_t)p;
-    const gc_u32 *w = (const gc_u32 *)(a & ~(uintptr_t)3);
-    const uint32_t sh = (uint32_t)(a & 3);
-    const uint32_t w0 = w[0], w1 = w[1];
-    if (sh == 0) return (uint64_t)w0 | ((uint64_t)w1 << 32);
-    const uint32_t w2 = w[2];
-    return (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32);
-}
-#ifndef JFS_ZE_WLOG
-#define JFS_ZE_WLOG 19
-#endif
-#ifndef JFS_ZE_HASH
-#define JFS_ZE_HASH 4  // bytes hashed for match candidates (libzstd level 1: 6)
-#endif
-#ifndef JFS_ZE_PSEARCH
-#define JFS_ZE_PSEARCH 1  // lane-parallel search (the serial loop's parse, 64 positions per step)
-#endif
-#ifndef JFS_ZE_REP
-#define JFS_ZE_REP 1   // try the repeat offset one byte ahead first (zstd_fast)
-#endif
-constexpr int64_t WMAX = 1 << JFS_ZE_WLOG;  // match window (windowLog 19, like level 1)
-
-// ---------------------------------------------------------------------------
-// backward bitstream writer (BIT_CStream semantics), uniform; bytes go to HBM
-// ---------------------------------------------------------------------------
-struct BitW {
-    g_u8 *dst;
-    int64_t wp, lim;  // next byte position; writes at or beyond lim are refused
-    uint64_t bc;
-    int bp;
-    bool ovf;
-};
-
-__device__ __forceinline__ void bw_add(BitW &w, uint32_t v, int nb) {
-    w.bc |= ((uint64_t)v & ((1ull << nb) - 1ull)) << w.bp;
-    w.bp += nb;
-}
-__device__ __forceinline__ void bw_flush(BitW &w) {
-    const int nbytes = w.bp >> 3;
-    const int l = lane_id();
-    if (w.wp + nbytes > w.lim) w.ovf = true;
-    if (!w.ovf && l < nbytes) w.dst[w.wp + l] = (uint8_t)(w.bc >> (8 * l));
-    w.wp += nbytes;
-    w.bc = nbytes >= 8 ? 0ull : (w.bc >> (8 * nbytes));
-    w.bp &= 7;
-}
-
-__device__ __forceinline__ uint32_t fse_init(const CView &t, uint32_t sym) {
-    const int32_t dnb = t.dnb[sym];
-    const uint32_t nbo = (uint32_t)((dnb + (1 << 15)) >> 16);
-    const uint32_t v = (nbo << 16) - (uint32_t)dnb;
-    return t.st[(v >> nbo) + (uint32_t)t.dfs[sym]];
-}
-__device__ __forceinline__ void fse_enc(BitW &w, const CView &t, uint32_t &st, uint32_t sym) {
-    const uint32_t nbo = (uint32_t)(((int32_t)st + t.dnb[sym]) >> 16);
-    bw_add(w, st, (int)nbo);
-    st = t.st[(st >> nbo) + (uint32_t)t.dfs[sym]];
-}
-__device__ __forceinline__ void fse_fin(BitW &w, uint32_t st, int tlog) {
-    bw_add(w, st, tlog);
-    bw_flush(w);
-}
-
-__device__ __forceinline__ uint32_t ll_code(const Smem &s, uint32_t ll) { return ll < 64 ? s.lut_ll[ll] : highbit(ll) + 19; }
-__device__ __forceinline__ uint32_t ml_code(const Smem &s, uint32_t mlb) {
-    return mlb < 128 ? s.lut_ml[mlb] : highbit(mlb) + 36;
-}
-
-__device__ __forceinline__ void seq_fields(const uint64_t *seq, int64_t i, uint32_t &ll, uint32_t &ml, uint32_t &off) {
-    const uint64_t r = seq[i];
-    ll = (uint32_t)(r & 0x1FFFFu);
-    ml = (uint32_t)((r >> 17) & 0x3FFFFu);
-    off = (uint32_t)(r >> 35);
-}
-
-// Encode sequences [0, ns) (scratch records: ll | ml << 17 | Offset_Value << 35 as
-// u64) as the predefined-mode FSE bitstream at w.wp (ZSTD_encodeSequences
-// order: last sequence first, states OF/ML/LL, extra bits LL/ML/OF).
-// Per 64 sequences the lanes load the records and look up, in parallel,
-// everything that does not depend on the FSE states (codes, extra-bit fields,
-// each symbol's deltaNbBits / deltaFindState); the serial loop then only
-// steps the three states (one LDS round trip per sequence) and packs bits.
-__device__ void encode_sequences(const Smem &s, BitW &w, const uint64_t *seq, int64_t ns) {
-    // per table: the block's FSE_Compressed table (mode 2) or the predefined one
-    const CView TL = s.smode[0] == 2 ? cview(s.q.act[0]) : cview(s.ct[0]);
-    const CView TM = s.smode[1] == 2 ? cview(s.q.act[1]) : cview(s.ct[1]);
-    const CView TO = s.smode[2] == 2 ? cview(s.q.act[2]) : cview(s.ct[2]);
-    const int l = lane_id();
-    uint32_t sML = 0, sOF = 0, sLL = 0;
-    for (int64_t c0 = ns - 1; c0 >= 0; c0 -= 64) {
-        const int64_t i = c0 - l;
-        uint32_t ll = 0, ml = 3, ofv = 1;
-        if (i >= 0) seq_fields(seq, i, ll, ml, ofv);
-        const uint32_t lc = ll_code(s, ll), mc = ml_code(s, ml - 3), oc = highbit(ofv);
-        const int32_t dO = TO.dnb[oc], dM = TM.dnb[mc], dL = TL.dnb[lc];
-        const uint32_t fOM = ((uint32_t)(uint16_t)TO.dfs[oc]) | ((uint32_t)(uint16_t)TM.dfs[mc] << 16);
-        const int32_t fL = TL.dfs[lc];
-        const uint32_t eLL = ll - LL_BASE[lc], eML = ml - ML_BASE[mc], eOF = ofv - (1u << oc);
-        const uint32_t nb = (uint32_t)LL_BITS[lc] | ((uint32_t)ML_BITS[mc] << 8) | (oc << 16);
-        const int nj = c0 + 1 < 64 ? (int)(c0 + 1) : 64;
-        for (int j = 0; j < nj; ++j) {
-            const int32_t jdO = (int32_t)readlane((uint32_t)dO, j), jdM = (int32_t)readlane((uint32_t)dM, j),
-                          jdL = (int32_t)readlane((uint32_t)dL, j);
-            const uint32_t jf = readlane(fOM, j);
-            const int32_t jfO = (int16_t)(jf & 0xFFFFu), jfM = (int16_t)(jf >> 16), jfL = (int32_t)readlane((uint32_t)fL, j);
-            const uint32_t jnb = readlane(nb, j);
-            const uint32_t jeLL = readlane(eLL, j), jeML = readlane(eML, j), jeOF = readlane(eOF, j);
-            if (c0 == ns - 1 && j == 0) {
-                // FSE_initCState2: the last sequence only sets the states
-                const uint32_t nM = (uint32_t)((jdM + (1 << 15)) >> 16), nO = (uint32_t)((jdO + (1 << 15)) >> 16),
-                               nL = (uint32_t)((jdL + (1 << 15)) >> 16);
-                const uint32_t vM = ((nM << 16) - (uint32_t)jdM) >> nM, vO = ((nO << 16) - (uint32_t)jdO) >> nO,
-                               vL = ((nL << 16) - (uint32_t)jdL) >> nL;
-                sML = TM.st[vM + (uint32_t)jfM];
-                sOF = TO.st[vO + (uint32_t)jfO];
-                sLL = TL.st[vL + (uint32_t)jfL];
-            } else {
-                const uint32_t nO = (uint32_t)(((int32_t)sOF + jdO) >> 16), nM = (uint32_t)(((int32_t)sML + jdM) >> 16),
-                               nL = (uint32_t)(((int32_t)sLL + jdL) >> 16);
-                bw_add(w, sOF, (int)nO);
-                bw_add(w, sML, (int)nM);
-                bw_add(w, sLL, (int)nL);
-                // the three table reads are independent: one LDS round trip
-                const uint32_t tO = TO.st[(sOF >> nO) + (uint32_t)jfO], tM = TM.st[(sML >> nM) + (uint32_t)jfM],
-                               tL = TL.st[(sLL >> nL) + (uint32_t)jfL];
-                sOF = tO;
-                sML = tM;
-                sLL = tL;
-                bw_flush(w);
+__device__ int fse_normalize(int16_t *norm, uint32_t tlog, const uint32_t *count, uint32_t total, uint32_t maxsv,
+                             bool lowprob) {
+    const uint32_t rtb[8] = {0, 473195, 504333, 520860, 550000, 700000, 750000, 830000};
+    const int16_t lowProbCount = lowprob ? -1 : 1;
+    const uint64_t scale = 62 - tlog;
+    const uint64_t step = ((uint64_t)1 << 62) / total;
+    const uint64_t vStep = 1ull << (scale - 20);
+    int still = 1 << tlog;
+    uint32_t s, largest = 0;
+    int16_t largestP = 0;
+    const uint32_t lowThreshold = total >> tlog;
+    for (s = 0; s <= maxsv; s++) {
+        if (count[s] == total) return 0;
+        if (count[s] == 0) { norm[s] = 0; continue; }
+        if (count[s] <= lowThreshold) {
+            norm[s] = lowProbCount;
+            still--;
+        } else {
+            int16_t proba = (int16_t)((count[s] * step) >> scale);
+            if (proba < 8) {
+                const uint64_t restToBeat = vStep * rtb[proba];
+                proba += (count[s] * step) - ((uint64_t)proba << scale) > restToBeat;
             }
-            bw_add(w, jeLL, (int)(jnb & 0xFFu));
-            bw_add(w, jeML, (int)((jnb >> 8) & 0xFFu));
-            bw_flush(w);
-            bw_add(w, jeOF, (int)(jnb >> 16));
-            bw_flush(w);
+            if (proba > largestP) { largestP = proba; largest = s; }
+            norm[s] = proba;
+            still -= proba;
         }
     }
-    fse_fin(w, sML, s.slog[1]);
-    fse_fin(w, sOF, s.slog[2]);
-    fse_fin(w, sLL, s.slog[0]);
-    bw_add(w, 1, 1);  // end mark
-    bw_flush(w);
-    if (w.bp > 0) {   // last partial byte
-        if (w.wp + 1 > w.lim) w.ovf = true;
-        if (!w.ovf && lane_id() == 0) w.dst[w.wp] = (uint8_t)w.bc;
-        w.wp++;
-        w.bp = 0;
-        w.bc = 0;
+    if (-still >= (norm[largest] >> 1)) {
+        if (fse_norm_m2(norm, tlog, count, total, maxsv, lowProbCount) < 0) return -1;
+    } else {
+        norm[largest] = (int16_t)(norm[largest] + still);
     }
+    return (int)tlog;
 }
 
-
-// ---------------------------------------------------------------------------
-// Huffman-compressed literals (RFC 8878 4.2.1; the choices of libzstd's
-// HUF_compress: code lengths limited to 11, 4 streams, tree description
-// FSE-compressed with two interleaved states or as direct 4-bit weights)
-// ---------------------------------------------------------------------------
-// FSE normalized-count header (RFC 8878 4.1.1; FSE_writeNCount layout).
-__device__ int write_ncount(uint8_t *out, const int16_t *norm, int maxsv, int tlog) {
+// FSE_writeNCount layout into out (LDS), returns bytes
+__device__ int write_ncount(uint8_t *out, const int16_t *norm, uint32_t maxsv, uint32_t tlog) {
     int o = 0;
     const int tsize = 1 << tlog;
-    int remaining = tsize + 1, threshold = tsize, nbits = tlog + 1;
-    uint32_t bs = (uint32_t)(tlog - 5);
+    int remaining = tsize + 1, threshold = tsize, nbits = (int)tlog + 1;
+    uint32_t bs = tlog - 5;
     int bc = 4;
-    int sym = 0, prev0 = 0;
-    const int alpha = maxsv + 1;
+    uint32_t sym = 0;
+    const uint32_t alpha = maxsv + 1;
+    int prev0 = 0;
     while (sym < alpha && remaining > 1) {
         if (prev0) {
-            int start = sym;
+            uint32_t start = sym;
             while (sym < alpha && !norm[sym]) sym++;
             if (sym == alpha) break;
             while (sym >= start + 24) {
@@ -397,7 +658,7 @@ __device__ int write_ncount(uint8_t *out, const int16_t *norm, int maxsv, int tl
                 bs += 3u << bc;
                 bc += 2;
             }
-            bs += (uint32_t)(sym - start) << bc;
+            bs += (sym - start) << bc;
             bc += 2;
             if (bc > 16) {
                 out[o] = (uint8_t)bs;
@@ -434,908 +695,1108 @@ __device__ int write_ncount(uint8_t *out, const int16_t *norm, int maxsv, int tl
     return o;
 }
 
-// lane-local backward bitstream into LDS (the tree description)
-struct LBits {
-    uint8_t *out;
-    int o, lim;
+template <int N, int NS>
+__device__ void build_ctab(uint8_t *tsym, CTab<N, NS> &t, const int16_t *norm, uint32_t maxsv, uint32_t tlog) {
+    const uint32_t size = 1u << tlog, mask = size - 1, step = (size >> 1) + (size >> 3) + 3;
+    uint32_t high = size - 1;
+    uint32_t cumul[NS + 1];
+    t.tlog = (int32_t)tlog;
+    cumul[0] = 0;
+    for (uint32_t u = 1; u <= maxsv + 1; u++) {
+        if (norm[u - 1] == -1) {
+            cumul[u] = cumul[u - 1] + 1;
+            tsym[high--] = (uint8_t)(u - 1);
+        } else {
+            cumul[u] = cumul[u - 1] + (uint32_t)norm[u - 1];
+        }
+    }
+    uint32_t pos = 0;
+    for (uint32_t s = 0; s <= maxsv; s++) {
+        for (int k = 0; k < norm[s]; k++) {
+            tsym[pos] = (uint8_t)s;
+            pos = (pos + step) & mask;
+            while (pos > high) pos = (pos + step) & mask;
+        }
+    }
+    for (uint32_t u = 0; u < size; u++) t.st[cumul[tsym[u]]++] = (uint16_t)(size + u);
+    uint32_t total = 0;
+    for (uint32_t s = 0; s <= maxsv; s++) {
+        const int nc = norm[s];
+        if (nc == 0) {
+            t.dnb[s] = (int32_t)(((tlog + 1) << 16) - size);
+            t.dfs[s] = 0;
+        } else if (nc == -1 || nc == 1) {
+            t.dnb[s] = (int32_t)((tlog << 16) - size);
+            t.dfs[s] = (int16_t)((int32_t)total - 1);
+            total += 1;
+        } else {
+            const uint32_t mbo = tlog - hbit((uint32_t)nc - 1);
+            t.dnb[s] = (int32_t)((mbo << 16) - ((uint32_t)nc << mbo));
+            t.dfs[s] = (int16_t)((int32_t)total - nc);
+            total += (uint32_t)nc;
+        }
+    }
+}
+template <int N, int NS>
+__device__ void build_rle(CTab<N, NS> &t, uint32_t sym) {
+    t.tlog = 0;
+    t.st[0] = 0;
+    t.st[1] = 0;
+    t.dnb[sym] = 0;
+    t.dfs[sym] = 0;
+}
+
+// ---------------------------------------------------------------------------
+// backward bitstream into global memory (BIT_CStream bit order)
+// ---------------------------------------------------------------------------
+struct BitW {
+    g_u8 *dst;
+    int64_t wp, lim;
     uint64_t bc;
     int bp;
+    bool ovf;
 };
-__device__ __forceinline__ void lb_add(LBits &b, uint32_t v, int nb) {
-    b.bc |= ((uint64_t)v & ((1ull << nb) - 1ull)) << b.bp;
-    b.bp += nb;
+__device__ __forceinline__ void bw_add(BitW &w, uint32_t v, int nb) {
+    w.bc |= ((uint64_t)v & ((1ull << nb) - 1ull)) << w.bp;
+    w.bp += nb;
 }
-__device__ __forceinline__ void lb_flush(LBits &b) {
-    while (b.bp >= 8) {
-        if (b.o < b.lim) b.out[b.o] = (uint8_t)b.bc;
-        b.o++;
-        b.bc >>= 8;
-        b.bp -= 8;
-    }
-}
-__device__ __forceinline__ void lb_enc(LBits &b, const CView &t, uint32_t &st, uint32_t sym) {
-    const uint32_t nbo = (uint32_t)(((int32_t)st + t.dnb[sym]) >> 16);
-    lb_add(b, st, (int)nbo);
-    st = t.st[(st >> nbo) + (uint32_t)t.dfs[sym]];
-}
-
-// Code lengths (<= HUF_MAXB, complete code) of the counted literals; lane 0.
-// Returns max length, 0 when Huffman does not apply (fewer than 2 symbols or
-// no exact length limit found).
-__device__ int huf_build(HufSmem &h) {
-    int n = 0;
-    for (int c = 0; c < 256; c++) {
-        h.len[c] = 0;
-        if (h.cnt[c]) h.sym[n++] = (uint16_t)c;
-    }
-    h.nsym = n;
-    if (n < 2) return 0;
-    for (int i = 1; i < n; i++) {  // insertion sort by count (stable in symbol order)
-        const uint16_t x = h.sym[i];
-        const uint32_t cx = h.cnt[x];
-        int j = i - 1;
-        while (j >= 0 && h.cnt[h.sym[j]] > cx) {
-            h.sym[j + 1] = h.sym[j];
-            j--;
-        }
-        h.sym[j + 1] = x;
-    }
-    for (int i = 0; i < n; i++) h.w[i] = h.cnt[h.sym[i]];
-    int li = 0, qi = n;
-    for (int k = n; k < 2 * n - 1; k++) {  // two-queue merge
-        int x, y;
-        if (li < n && (qi >= k || h.w[li] <= h.w[qi])) x = li++;
-        else x = qi++;
-        if (li < n && (qi >= k || h.w[li] <= h.w[qi])) y = li++;
-        else y = qi++;
-        h.w[k] = h.w[x] + h.w[y];
-        h.par[x] = h.par[y] = (uint16_t)k;
-    }
-    const int root = 2 * n - 2;
-    h.dep[root] = 0;
-    for (int k = root - 1; k >= 0; k--) h.dep[k] = (uint8_t)(h.dep[h.par[k]] + 1);
-    // limit to HUF_MAXB: clamp; while the code is over-subscribed lengthen the
-    // rarest code still below the limit; then, while under-subscribed, shorten
-    // the most frequent codes whose step still fits (Kraft sum in units of
-    // 2^-HUF_MAXB; every step is a power of two and codes at the limit step
-    // by 1, so the sum lands exactly on 2^HUF_MAXB: a complete prefix code)
-    const int64_t full = 1ll << HUF_MAXB;
-    int64_t kraft = 0;
-    for (int i = 0; i < n; i++) {
-        const int d = h.dep[i] > HUF_MAXB ? HUF_MAXB : h.dep[i];
-        h.dep[i] = (uint8_t)d;
-        kraft += 1ll << (HUF_MAXB - d);
-    }
-    for (int guard = 0; kraft > full && guard < 4096; guard++) {
-        int i = 0;  // leaves are sorted by count: index 0 is the rarest
-        while (i < n && h.dep[i] >= HUF_MAXB) i++;
-        if (i == n) return 0;
-        kraft -= 1ll << (HUF_MAXB - h.dep[i] - 1);
-        h.dep[i]++;
-    }
-    for (int guard = 0; kraft < full && guard < 64; guard++) {
-        for (int i = n - 1; i >= 0 && kraft < full; i--) {  // most frequent first
-            const int64_t add = h.dep[i] > 1 ? 1ll << (HUF_MAXB - h.dep[i]) : full;
-            if (kraft + add <= full) {
-                h.dep[i]--;
-                kraft += add;
-            }
-        }
-    }
-    if (kraft != full) return 0;
-    int maxb = 0;
-    for (int i = 0; i < n; i++) {
-        h.len[h.sym[i]] = h.dep[i];
-        maxb = h.dep[i] > maxb ? h.dep[i] : maxb;
-    }
-    // canonical codes: longest first, symbol order within a length
-    uint32_t c = 0;
-    for (int nb = maxb; nb >= 1; nb--) {
-        for (int v = 0; v < 256; v++)
-            if (h.len[v] == nb) h.code[v] = (uint16_t)c++;
-        c >>= 1;
-    }
-    int maxsym = 0;
-    for (int v = 0; v < 256; v++) {
-        h.wt[v] = h.len[v] ? (uint8_t)(maxb + 1 - h.len[v]) : 0;
-        if (h.len[v]) maxsym = v;
-    }
-    h.maxsym = maxsym;
-    return maxb;
-}
-
-// Tree description into h.hdr: FSE-compressed weights (2 states, table log
-// 6) when that is smaller, else direct 4-bit weights (<= 128 transmitted).
-// Returns its size, or -1 when neither applies.  Lane 0 (h.d: table + scratch).
-__device__ int huf_describe(Smem &s) {
-    HufSmem &h = s.h;
-    const int nw = h.maxsym;  // weights of symbols 0..maxsym-1 (the last one is implied)
-    int fse = -1;
-    if (nw >= 2) {
-        int wc[16] = {0};
-        int maxsv = 0;
-        for (int i = 0; i < nw; i++) {
-            wc[h.wt[i]]++;
-            maxsv = h.wt[i] > maxsv ? h.wt[i] : maxsv;
-        }
-        const int tlog = 6, tsize = 1 << tlog;
-        int sum = 0, big = 0;
-        for (int v = 0; v <= maxsv; v++) {
-            h.norm[v] = (int16_t)(wc[v] ? (wc[v] * tsize / nw > 0 ? wc[v] * tsize / nw : 1) : 0);
-            sum += h.norm[v];
-            if (wc[v] > wc[big]) big = v;
-        }
-        h.norm[big] = (int16_t)(h.norm[big] + (tsize - sum));
-        if (h.norm[big] >= 1) {
-            int o = 1 + write_ncount(h.hdr + 1, h.norm, maxsv, tlog);
-            build_ctab(h.d.tsym, h.d.cumul, h.d.wct, h.norm, maxsv, tlog);
-            LBits b;
-            b.out = h.hdr;
-            b.o = o;
-            b.lim = 128;
-            b.bc = 0;
-            b.bp = 0;
-            // FSE_compress_usingCTable order: two states, last symbols first
-            int ip = nw;
-            uint32_t s1, s2;
-            if (nw & 1) {
-                s1 = fse_init(cview(h.d.wct), h.wt[--ip]);
-                s2 = fse_init(cview(h.d.wct), h.wt[--ip]);
-                lb_enc(b, cview(h.d.wct), s1, h.wt[--ip]);
-                lb_flush(b);
-            } else {
-                s2 = fse_init(cview(h.d.wct), h.wt[--ip]);
-                s1 = fse_init(cview(h.d.wct), h.wt[--ip]);
-            }
-            if ((nw - 2) & 2) {
-                lb_enc(b, cview(h.d.wct), s2, h.wt[--ip]);
-                lb_enc(b, cview(h.d.wct), s1, h.wt[--ip]);
-                lb_flush(b);
-            }
-            while (ip > 0) {
-                lb_enc(b, cview(h.d.wct), s2, h.wt[--ip]);
-                lb_enc(b, cview(h.d.wct), s1, h.wt[--ip]);
-                lb_enc(b, cview(h.d.wct), s2, h.wt[--ip]);
-                lb_enc(b, cview(h.d.wct), s1, h.wt[--ip]);
-                lb_flush(b);
-            }
-            lb_add(b, s2, tlog);
-            lb_flush(b);
-            lb_add(b, s1, tlog);
-            lb_flush(b);
-            lb_add(b, 1, 1);  // end mark
-            lb_flush(b);
-            if (b.bp > 0) {
-                if (b.o < b.lim) b.out[b.o] = (uint8_t)b.bc;
-                b.o++;
-            }
-            if (b.o - 1 < 128) {
-                h.hdr[0] = (uint8_t)(b.o - 1);
-                fse = b.o;
-            }
-        }
-    }
-    const int direct = nw <= 128 ? 1 + (nw + 1) / 2 : -1;
-    if (fse > 0 && (direct < 0 || fse <= direct)) return fse;
-    if (direct < 0) return -1;
-    h.hdr[0] = (uint8_t)(127 + nw);
-    for (int i = 0; i < nw; i += 2) h.hdr[1 + i / 2] = (uint8_t)((h.wt[i] << 4) | (i + 1 < nw ? h.wt[i + 1] : 0));
-    return direct;
-}
-
-// Encode literals lit[0, L) as four Huffman streams into the scratch (lanes
-// 0-3, one stream each, last symbol first); returns the streams' total size.
-__device__ int64_t huf_streams(Smem &s, const gc_u8 *lit, int64_t L, g_u8 *scr) {
-    HufSmem &h = s.h;
+__device__ __forceinline__ void bw_flush(BitW &w) {
+    const int nbytes = w.bp >> 3;
     const int l = lane_id();
-    const int64_t seg = (L + 3) / 4;
-    if (l < 4) {
-        const int64_t a = l * seg, e = (l + 1) * seg < L ? (l + 1) * seg : L;
-        g_u8 *out = scr + l * LSTREAM;
-        int64_t o = 0;
-        uint64_t bc = 0;
-        int bp = 0;
-        for (int64_t i = e - 1; i >= a; --i) {
-            const uint32_t v = lit[i];
-            bc |= (uint64_t)h.code[v] << bp;
-            bp += h.len[v];
-            if (bp >= 32) {
-                out[o] = (uint8_t)bc;
-                out[o + 1] = (uint8_t)(bc >> 8);
-                out[o + 2] = (uint8_t)(bc >> 16);
-                out[o + 3] = (uint8_t)(bc >> 24);
-                o += 4;
-                bc >>= 32;
-                bp -= 32;
-            }
-        }
-        bc |= 1ull << bp;  // end mark
-        bp += 1;
-        while (bp > 0) {
-            out[o++] = (uint8_t)bc;
-            bc >>= 8;
-            bp -= 8;
-        }
-        h.ssz[l] = (int32_t)o;
-    }
-    __syncthreads();
-    return (int64_t)h.ssz[0] + h.ssz[1] + h.ssz[2] + h.ssz[3];
+    if (w.wp + nbytes > w.lim) w.ovf = true;
+    if (!w.ovf && l < nbytes) w.dst[w.wp + l] = (uint8_t)(w.bc >> (8 * l));
+    w.wp += nbytes;
+    w.bc = nbytes >= 8 ? 0ull : (w.bc >> (8 * nbytes));
+    w.bp &= 7;
 }
 
-// Sequence tables of one block (RFC 8878 3.1.1.3.2.1): FSE_Compressed when the
-// estimated bits (symbols + table header) beat the predefined distribution.
-// All lanes histogram the codes; lane 0 normalizes, writes the headers and
-// builds the tables.  Sets s.smode / s.slog / s.shdr / s.shsz.
-__device__ void choose_seq_tables(Smem &s, const uint64_t *seq, int64_t ns) {
+// ---------------------------------------------------------------------------
+// kernel 2: literals + sequences section of one block (one wave per block)
+// ---------------------------------------------------------------------------
+struct SeqSmem {
+    uint32_t h4[4][256];  // literal histograms per Huffman stream segment
+    uint32_t cnt[3][64];  // LL / OF / ML code histograms
+    int16_t norm[64];
+    uint8_t tsym[512];
+    CTab<512, 36> tLL;
+    CTab<256, 32> tOF;
+    CTab<512, 53> tML;
+    uint8_t hdr[3][128];
+    int32_t hsz[3], type[3];
+    uint32_t lastc[3];
+};
+
+__global__ __launch_bounds__(64) void zl1_seq_kernel(const FInfo *__restrict__ fi, const int32_t *__restrict__ blist,
+                                                     BInfo *__restrict__ bi, const uint64_t *__restrict__ seqs,
+                                                     uint8_t *__restrict__ bytes, uint32_t *__restrict__ hist) {
+    __shared__ SeqSmem s;
     const int l = lane_id();
-    for (int k = l; k < 3 * 64; k += 64) (&s.q.scnt[0][0])[k] = 0;
-    __syncthreads();
-    for (int64_t i = l; i < ns; i += 64) {
-        uint32_t ll, ml, off;
-        seq_fields(seq, i, ll, ml, off);
-        atomicAdd(&s.q.scnt[0][ll_code(s, ll)], 1u);
-        atomicAdd(&s.q.scnt[1][ml_code(s, ml - 3)], 1u);
-        atomicAdd(&s.q.scnt[2][highbit(off)], 1u);
-    }
-    __syncthreads();
-    if (l == 0) {
-        const int16_t *pre[3] = {LL_DEF, ML_DEF, OF_DEF};
-        const int prelog[3] = {6, 6, 5}, premax[3] = {35, 52, 28}, maxlog[3] = {9, 9, 8}, nsym[3] = {36, 53, 32};
-        for (int t = 0; t < 3; t++) {
-            s.smode[t] = 0;
-            s.slog[t] = prelog[t];
-            s.shsz[t] = 0;
-            const uint32_t *cnt = s.q.scnt[t];
-            int maxsv = 0, distinct = 0;
-            for (int v = 0; v < nsym[t]; v++)
-                if (cnt[v]) { maxsv = v; distinct++; }
-            if (ns < 64 || distinct < 2) continue;
-            // predefined cost (bits); a code it cannot express forces mode 2
-            float pc = 0.f;
-            bool pre_ok = maxsv <= premax[t];
-            for (int v = 0; v <= maxsv && pre_ok; v++) {
-                if (!cnt[v]) continue;
-                const int pn = pre[t][v] == -1 ? 1 : pre[t][v];
-                if (pn <= 0) { pre_ok = false; break; }
-                pc += (float)cnt[v] * ((float)prelog[t] - __log2f((float)pn));
-            }
-            int tlog = (int)highbit((uint32_t)(ns - 1)) - 2;
-            tlog = tlog < 5 ? 5 : tlog > maxlog[t] ? maxlog[t] : tlog;
-            while ((1 << tlog) < 2 * distinct && tlog < maxlog[t]) tlog++;
-            const int tsize = 1 << tlog;
-            int16_t *norm = s.q.snorm[t];
-            int sum = 0, big = 0;
-            for (int v = 0; v <= maxsv; v++) {
-                int nv = 0;
-                if (cnt[v]) {
-                    nv = (int)(((uint64_t)cnt[v] * (uint64_t)tsize) / (uint64_t)ns);
-                    nv = nv < 1 ? 1 : nv;
-                }
-                norm[v] = (int16_t)nv;
-                sum += nv;
-                if (cnt[v] > cnt[big]) big = v;
-            }
-            norm[big] = (int16_t)(norm[big] + (tsize - sum));
-            if (norm[big] < 1) continue;  // (cannot happen with 2 * distinct <= tsize)
-            float cc = 0.f;
-            for (int v = 0; v <= maxsv; v++)
-                if (cnt[v]) cc += (float)cnt[v] * ((float)tlog - __log2f((float)norm[v]));
-            const int hs = write_ncount(s.q.shdr[t], norm, maxsv, tlog);
-            cc += 8.f * (float)hs;
-            if (pre_ok && pc <= cc) continue;
-            build_ctab(s.q.tsym, s.q.cumul, s.q.act[t], norm, maxsv, tlog);
-            s.smode[t] = 2;
-            s.slog[t] = tlog;
-            s.shsz[t] = hs;
-        }
-    }
-    __syncthreads();
-}
-
-// wave-parallel byte copy src[a, a+len) -> dst[o, o+len)
-__device__ __forceinline__ void copy_bytes(g_u8 *dst, int64_t o, const gc_u8 *src, int64_t a, int64_t len) {
-    const int l = lane_id();
-    for (int64_t k = l; k < len; k += 64) dst[o + k] = src[a + k];
-}
-
-__device__ __forceinline__ void put3(g_u8 *dst, int64_t o, uint32_t v) {
-    const int l = lane_id();
-    if (l < 3) dst[o + l] = (uint8_t)(v >> (8 * l));
-}
-
-// Frame header size (magic, FHD, [Window_Descriptor], Frame_Content_Size).
-__device__ __forceinline__ int frame_header(int64_t n, bool write, g_u8 *dst) {
-    const int l = lane_id();
-    const bool single = n <= (1 << 19);
-    int fcs_flag, fs;
-    if (single) {
-        if (n < 256) { fcs_flag = 0; fs = 1; }
-        else if (n < 65536 + 256) { fcs_flag = 1; fs = 2; }
-        else { fcs_flag = 2; fs = 4; }
-    } else {
-        fcs_flag = n < (1ll << 32) ? 2 : 3;
-        fs = fcs_flag == 2 ? 4 : 8;
-    }
-    const uint32_t fhd = (uint32_t)((fcs_flag << 6) | (single ? 0x20 : 0));
-    const int fpos = single ? 5 : 6;  // FCS position
-    const uint64_t fv = (uint64_t)n - (fs == 2 ? 256 : 0);
-    const int hn = fpos + fs;
-    uint32_t byte = 0;
-    if (l < 4) byte = (0xFD2FB528u >> (8 * l)) & 0xFFu;
-    else if (l == 4) byte = fhd;
-    else if (l == 5 && !single) byte = (19 - 10) << 3;  // windowLog 19 (512 KiB), like level 1
-    else if (l >= fpos && l < hn) byte = (uint32_t)(fv >> (8 * (l - fpos))) & 0xFFu;
-    if (write && l < hn) dst[l] = (uint8_t)byte;
-    return hn;
-}
-
-__device__ __forceinline__ int64_t ze_bound(int64_t n) { return n + (n >> 8) + (n < BLK ? (BLK - n) >> 11 : 0); }
-
-// Block-parallel mode (BPAR): one work item = one 128 KiB block of a frame,
-// encoded into its slot dst[hn + k * SLOT] (a block and its literal staging
-// never exceed SLOT bytes); zstd_compact_kernel then moves the blocks down
-// to their frame positions.  The wave's hash table starts from the WARM bytes
-// before the block (every position inserted), the repeat offset starts
-// unknown (no repeat code before the block's first explicit offset): the
-// frames are valid RFC 8878 frames, the window (512 KiB) reaches back into
-// earlier blocks.  Without BPAR one wave encodes a whole frame, block after
-// block.
-constexpr int64_t SLOT = BLK + 16;
-#ifndef JFS_ZE_WARM_KB
-#define JFS_ZE_WARM_KB 256  // 64: ratio 3.032, 128: 3.049, 256: 3.054 (one wave per frame: 3.052)
-#endif
-constexpr int64_t WARM = (int64_t)JFS_ZE_WARM_KB << 10;
-
-template <bool BPAR>
-__global__ __launch_bounds__(64) void zstd_encode_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
-                                                        int32_t *__restrict__ ret, uint64_t *__restrict__ scratch,
-                                                        const int2 *__restrict__ work, int nwork,
-                                                        int32_t *__restrict__ bsize) {
-    __shared__ Smem s;
-    if (!BPAR && (int)blockIdx.x >= nblk) return;
-    const int l = lane_id();
-    // per-wave scratch: sequences and Huffman streams of the current block
-    const int64_t sidx = (int64_t)blockIdx.x;
-    uint64_t *seq = (uint64_t *)((uint8_t *)scratch + sidx * SCR_PER);
-    g_u8 *lscr = (g_u8 *)((uint8_t *)scratch + sidx * SCR_PER + SEQ_CAP * 8);
-    // tables
-    for (int v = l; v < 64; v += 64) {
-        int c = 0;
-        while (c + 1 < 36 && LL_BASE[c + 1] <= (uint32_t)v) c++;
-        s.lut_ll[v] = (uint8_t)c;
-    }
-    for (int v = l; v < 128; v += 64) {
-        int c = 0;
-        while (c + 1 < 53 && ML_BASE[c + 1] - 3 <= (uint32_t)v) c++;
-        s.lut_ml[v] = (uint8_t)c;
-    }
-    for (int t = l; t < 3; t += 64) {
-        s.smode[t] = 0;
-        s.slog[t] = t == 2 ? 5 : 6;
-        s.shsz[t] = 0;
-    }
-    build_ctab(s.q.tsym, s.q.cumul, s.ct[0], LL_DEF, 35, 6);
-    __builtin_amdgcn_wave_barrier();
-    build_ctab(s.q.tsym, s.q.cumul, s.ct[1], ML_DEF, 52, 6);
-    __builtin_amdgcn_wave_barrier();
-    build_ctab(s.q.tsym, s.q.cumul, s.ct[2], OF_DEF, 28, 5);
-    __syncthreads();
-    ZE_DECL
-
-    for (int wi = BPAR ? (int)blockIdx.x : 0; BPAR ? wi < nwork : wi < 1; wi += BPAR ? (int)gridDim.x : 1) {
-    const int b = BPAR ? work[wi].x : (int)blockIdx.x;  // the frame (input)
-    const int kb = BPAR ? work[wi].y : 0;               // its block (BPAR)
-    const jfs_dev_block d = ((const gc_blk *)blocks)[b];
-    const gc_u8 *src = (const gc_u8 *)d.src;
-    g_u8 *dst = (g_u8 *)d.dst;
-    const int64_t n = d.src_len, cap = d.dst_cap;
-    if (n < 0 || cap < ze_bound(n)) {  // compress.go:86-89: cap(dst) < CompressBound -> "buffer too short"
-        if (l == 0) {
-            if (BPAR) bsize[wi] = -1;
-            else ret[b] = -2;
-        }
-        continue;
-    }
-    // ---- frame header (BPAR: written by the frame's first block)
-    const int hn = frame_header(n, !BPAR || kb == 0, dst);
-    const int64_t slot0 = BPAR ? hn + (int64_t)kb * SLOT : hn;
-    int64_t op = slot0;
-    for (int k = l; k < (1 << HBITS); k += 64) s.table[k] = 0;
-    int64_t bs = BPAR ? (int64_t)kb * BLK : 0;
-    if (BPAR && bs > 0) {  // warm-up: the positions of the WARM bytes before the block
-        __builtin_amdgcn_wave_barrier();
-        const int64_t w0 = bs > WARM ? bs - WARM : 0;
-        for (int64_t q0 = w0; q0 + 8 <= bs; q0 += 64) {
-            const int64_t q = q0 + l;
-            if (q + 8 <= bs) {
-                const uint64_t v = ld64u(src + q);
-                s.table[JFS_ZE_HASH == 6 ? hash6(v) : hash4((uint32_t)v)] = (uint32_t)q;
-            }
-        }
-    }
-    __builtin_amdgcn_wave_barrier();
-
-    // ---- blocks (the repeat offsets carry across the frame's blocks, RFC 8878 3.1.1.5)
-    uint32_t rep0 = BPAR && bs > 0 ? 0u : 1u;  // Repeated_Offset1 (0: unknown; only it is reused: Offset_Value 1 with LL > 0)
-    do {
-        const int64_t be = bs + BLK < n ? bs + BLK : n;
-        const bool last = be == n;
-        const int64_t raw = be - bs;
-        const int64_t lit0 = op + 3 + 3;  // block header + largest literals header
-        int64_t L = 0, ns = 0;
-        bool ok = raw > 0;
-        // 1. parse; literals straight to dst[lit0 + L]
-        {
-            int64_t ip = bs, anchor = bs;
-            uint32_t miss = 0;
-            while (ok && ip + 8 <= be) {
-                // zstd_fast: a repeat-offset match one byte ahead first, else the
-                // 6-byte hash candidate (level 1: minMatch 6) within the window
-                int64_t cand;
-                uint32_t ofv = 0;  // Offset_Value: 1 = repeat offset 1, else offset + 3
-#if JFS_ZE_PSEARCH
-                // Lane-parallel search: lane j takes the j-th next position of
-                // the miss schedule and makes both checks of the serial loop
-                // there (repeat offset one byte ahead, then the hash candidate);
-                // the first lane with a match ends the search.  Table entries
-                // are read before any insert of the batch, which is the serial
-                // order while no two positions share a hash: the batch is cut
-                // at the first lane of a shared hash (tagged write + read-back),
-                // so the parse is the serial loop's exactly.
-                {
-                    bool done = false;
-                    for (;;) {
-                        const uint32_t st = 1u + ((miss + (uint32_t)l) >> 6);
-                        const uint32_t inc = dpp_scan_add(st);
-                        const int64_t P = ip + (int64_t)(inc - st);
-                        const uint64_t onm = __ballot(P + 8 <= be);
-                        const int nl = ~onm ? (int)__builtin_ctzll(~onm) : 64;
-                        if (nl == 0) { done = true; break; }
-                        const bool on = l < nl;
-                        bool rep = false;
-                        uint64_t v = 0;
-                        uint32_t h = 0, E = 0;
-                        if (on) {
-                            const int64_t rp = P + 1;
-                            rep = JFS_ZE_REP && rep0 > 0 && rep0 <= rp && ld32u(src + rp) == ld32u(src + rp - rep0);
-                            v = ld64u(src + P);
-                            h = JFS_ZE_HASH == 6 ? hash6(v) : hash4((uint32_t)v);
-                            E = s.table[h];
-                        }
-                        const uint32_t tag = 0xFFFFFF00u | (uint32_t)l;  // never a position (inputs < 2 GiB)
-                        if (on) s.table[h] = tag;
-                        __builtin_amdgcn_wave_barrier();
-                        uint32_t cm = 64u;
-                        if (on) {
-                            const uint32_t t = s.table[h];
-                            if (t != tag) cm = umin32((uint32_t)l, t & 0xFFu);
-                        }
-                        const int ncut = (int)dwave_min(cm) + 1;
-                        const int nb = ncut < nl ? ncut : nl;  // lanes [0, nb) are exact
-                        if (on && l >= nb) s.table[h] = E;
-                        const int64_t hc = (int64_t)E;
-                        bool hit = l < nb && !rep && hc < P && P - hc <= WMAX;
-                        if (__ballot(hit)) {
-                            if (hit) hit = ld32u(src + hc) == (uint32_t)v;
-                        }
-                        const bool got = l < nb && (rep || hit);
-                        const uint64_t gm = __ballot(got);
-                        const int jm = gm ? (int)__builtin_ctzll(gm) : 64;
-                        // inserts: every position before jm, and jm itself unless its repeat check hit
-                        if (l < nb) s.table[h] = (l < jm || (l == jm && !rep)) ? (uint32_t)P : E;
-                        __builtin_amdgcn_wave_barrier();
-                        if (gm) {
-                            const int64_t pj = ip + (int64_t)readlane(inc - st, jm);
-                            if (readlane(rep ? 1u : 0u, jm)) {
-                                ip = pj + 1;
-                                cand = ip - rep0;
-                                ofv = 1;
-                            } else {
-                                ip = pj;
-                                cand = (int64_t)readlane(E, jm);
-                            }
-                            break;
-                        }
-                        ip += (int64_t)readlane(inc, nb - 1);
-                        miss += (uint32_t)nb;
-                    }
-                    if (done) break;
-                }
-                {
-#else
-                const int64_t rp = ip + 1;
-                if (JFS_ZE_REP && rep0 > 0 && rep0 <= rp && ld32u(src + rp) == ld32u(src + rp - rep0)) {
-                    cand = rp - rep0;
-                    ip = rp;
-                    ofv = 1;
-                } else {
-                    const uint64_t v = ld64u(src + ip);
-                    const uint32_t h = JFS_ZE_HASH == 6 ? hash6(v) : hash4((uint32_t)v);
-                    cand = (int64_t)s.table[h];
-                    s.table[h] = (uint32_t)ip;
-                    bool hit = cand < ip && ip - cand <= WMAX;
-                    if (hit) hit = ld32u(src + cand) == (uint32_t)v;
-                    if (!hit) {
-                        ip += 1 + (miss++ >> 6);
-                        continue;
-                    }
-#endif
-                }
-                miss = 0;
-                // forward extension from +4 (64 bytes per step, up to the block
-                // end) and backward catch-up (new offsets only): the first step
-                // of both is loaded in one HBM round trip
-                int64_t ml = 4;
-                int64_t lim = 0;
-                if (ofv == 0) {
-                    lim = ip - anchor;
-                    if (cand < lim) lim = cand;
-                }
-                const int64_t kk = 1 + l, a0 = ip + 4 + l;
-                uint32_t xa = 0, xb = 1, ca = 0, cb = 1;
-                if (a0 < be) { xa = src[a0]; xb = src[cand + 4 + l]; }
-                if (kk <= lim) { ca = src[ip - kk]; cb = src[cand - kk]; }
-                {
-                    const uint64_t ne = ~__ballot(a0 < be && xa == xb);
-                    const int run = ne ? (int)__builtin_ctzll(ne) : 64;
-                    ml += run;
-                    bool more = run == 64;
-                    while (more) {
-                        const int64_t a = ip + ml + l;
-                        const bool eq = a < be && src[a] == src[cand + ml + l];
-                        const uint64_t ne2 = ~__ballot(eq);
-                        const int r2 = ne2 ? (int)__builtin_ctzll(ne2) : 64;
-                        ml += r2;
-                        more = r2 == 64;
-                    }
-                }
-                int64_t m0 = cand;
-                if (ofv == 0) {
-                    const uint64_t cne = ~__ballot(kk <= lim && ca == cb);
-                    int64_t back = cne ? (int)__builtin_ctzll(cne) : 64;
-                    bool cmore = back == 64;
-                    while (cmore && back < lim) {
-                        const int64_t k = back + 1 + l;
-                        const bool eq = k <= lim && src[ip - k] == src[m0 - k];
-                        const uint64_t ne = ~__ballot(eq);
-                        const int run = ne ? (int)__builtin_ctzll(ne) : 64;
-                        back += run;
-                        cmore = run == 64;
-                    }
-                    if (back > lim) back = lim;
-                    ip -= back;
-                    m0 -= back;
-                    ml += back;
-                }
-                const int64_t ll = ip - anchor;
-                copy_bytes(dst, lit0 + L, src, anchor, ll);
-                L += ll;
-                if (ns >= SEQ_CAP) { ok = false; break; }
-                if (ofv == 0) {  // a new offset enters the repeat history
-                    const uint32_t off = (uint32_t)(ip - m0);
-                    ofv = off + 3;
-                    rep0 = off;
-                }
-                if (l == 0) seq[ns] = (uint64_t)ll | ((uint64_t)ml << 17) | ((uint64_t)ofv << 35);
-                ns++;
-                ip += ml;
-                anchor = ip;
-                if (ip - 2 >= bs && ip + 6 <= n) {
-                    const uint64_t v2 = ld64u(src + ip - 2);
-                    s.table[JFS_ZE_HASH == 6 ? hash6(v2) : hash4((uint32_t)v2)] = (uint32_t)(ip - 2);
-                }
-            }
-            if (ok) {  // last literals of the block
-                copy_bytes(dst, lit0 + L, src, anchor, be - anchor);
-                L += be - anchor;
-            }
-        }
-        __threadfence_block();
-        ZE(0);
-        ZEC(8, 1);
-        ZEC(9, ns);
-        // 2./3. headers and the sequences bitstream
-        int64_t end = lit0 + L;
-        if (ok) {
-            // literal section kind: 2 Huffman, 1 RLE, 0 raw -- the smallest
-            const int hsz = L < 32 ? 1 : L < 4096 ? 2 : 3;  // raw / RLE header bytes
-            int kind = 0;
-            int64_t hcs = 0;  // Huffman: Compressed_Size (tree + jump table + streams)
-            int hlh = 0;      // Huffman: literal header bytes
-            if (L >= HUF_MINL) {
-                wait_vm();  // the literals this wave stored are read back
-                for (int k = l; k < 256; k += 64) s.h.cnt[k] = 0;
-                __syncthreads();
-                for (int64_t k = l; k < L; k += 64) atomicAdd(&s.h.cnt[dst[lit0 + k]], 1u);
-                __syncthreads();
-                if (l == 0) {
-                    s.h.maxbits = huf_build(s.h);
-                    s.h.hsize = s.h.maxbits > 0 ? huf_describe(s) : -1;
-                }
-                __syncthreads();
-                ZE(1);
-                if (s.h.nsym == 1) {
-                    kind = 1;
-                } else if (s.h.maxbits > 0 && s.h.hsize > 0) {
-                    const int64_t ss = huf_streams(s, (const gc_u8 *)dst + lit0, L, lscr);
-                    hcs = s.h.hsize + 6 + ss;
-                    const int64_t big = L > hcs ? L : hcs;
-                    hlh = big < 1024 ? 3 : big < 16384 ? 4 : 5;
-                    if (big < (1 << 18) && hlh + hcs < hsz + L) kind = 2;
-                }
-                wait_vm();
-                __syncthreads();
-                ZE(2);
-            }
-            if (kind == 2) {
-                const uint64_t sf = hlh == 3 ? 1 : hlh == 4 ? 2 : 3;
-                const int sb = hlh == 3 ? 10 : hlh == 4 ? 14 : 18;
-                const uint64_t lh = 2u | (sf << 2) | ((uint64_t)L << 4) | ((uint64_t)hcs << (4 + sb));
-                int64_t o = op + 3;
-                if (l < hlh) dst[o + l] = (uint8_t)(lh >> (8 * l));
-                o += hlh;
-                for (int k = l; k < s.h.hsize; k += 64) dst[o + k] = s.h.hdr[k];
-                o += s.h.hsize;
-                if (l < 3) {  // jump table: sizes of streams 1-3
-                    dst[o + 2 * l] = (uint8_t)s.h.ssz[l];
-                    dst[o + 2 * l + 1] = (uint8_t)(s.h.ssz[l] >> 8);
-                }
-                o += 6;
-                for (int k = 0; k < 4; k++) {
-                    copy_bytes(dst, o, (const gc_u8 *)lscr + k * LSTREAM, 0, s.h.ssz[k]);
-                    o += s.h.ssz[k];
-                }
-                end = o;
-            } else if (kind == 1) {
-                const uint32_t lh = hsz == 1   ? ((uint32_t)L << 3) | 1u
-                                    : hsz == 2 ? (1u << 2) | ((uint32_t)L << 4) | 1u
-                                               : (3u << 2) | ((uint32_t)L << 4) | 1u;
-                const uint8_t v = dst[lit0];
-                __builtin_amdgcn_wave_barrier();
-                if (l < hsz) dst[op + 3 + l] = (uint8_t)(lh >> (8 * l));
-                if (l == 0) dst[op + 3 + hsz] = v;
-                end = op + 3 + hsz + 1;
-            }
-            // Raw_Literals_Block with the smallest Size_Format (1, 2 or 3 header
-            // bytes, like libzstd); the literals move down to follow it
-            const uint32_t lh = hsz == 1   ? (uint32_t)L << 3
-                                : hsz == 2 ? (1u << 2) | ((uint32_t)L << 4)
-                                           : (3u << 2) | ((uint32_t)L << 4);
-            if (kind == 0 && hsz < 3) {
-                const int64_t to = op + 3 + hsz;
-                for (int64_t k = 0; k < L; k += 64) {  // dst < src: ascending chunks are safe
-                    uint8_t v = 0;
-                    if (k + l < L) v = dst[lit0 + k + l];
-                    __builtin_amdgcn_wave_barrier();
-                    if (k + l < L) dst[to + k + l] = v;
-                }
-                end = to + L;
-            }
-            if (kind == 0 && l < hsz) dst[op + 3 + l] = (uint8_t)(lh >> (8 * l));
-            __threadfence_block();
-            if (ns < 128) {
-                if (l == 0) dst[end] = (uint8_t)ns;
-                end += 1;
-            } else if (ns < 0x7F00) {
-                if (l == 0) dst[end] = (uint8_t)((ns >> 8) + 128);
-                if (l == 1) dst[end + 1] = (uint8_t)(ns & 255);
-                end += 2;
-            } else {
-                const int64_t r = ns - 0x7F00;
-                if (l == 0) dst[end] = 255;
-                if (l == 1) dst[end + 1] = (uint8_t)(r & 255);
-                if (l == 2) dst[end + 2] = (uint8_t)(r >> 8);
-                end += 3;
-            }
-            ZE(3);
-            if (ns > 0) {
-                choose_seq_tables(s, seq, ns);
-                ZE(4);
-                // Symbol_Compression_Modes: LL bits 7-6, OF 5-4, ML 3-2; then the
-                // table descriptions in the order LL, OF, ML
-                if (l == 0) dst[end] = (uint8_t)((s.smode[0] << 6) | (s.smode[2] << 4) | (s.smode[1] << 2));
-                end += 1;
-                for (int t : {0, 2, 1}) {
-                    for (int k = l; k < s.shsz[t]; k += 64) dst[end + k] = s.q.shdr[t][k];
-                    end += s.shsz[t];
-                }
-                __threadfence_block();
-                BitW w;
-                w.dst = dst;
-                w.wp = end;
-                w.lim = op + 3 + raw;  // not smaller than raw -> stored raw anyway
-                w.bc = 0;
-                w.bp = 0;
-                w.ovf = false;
-                encode_sequences(s, w, seq, ns);
-                end = w.wp;
-                if (w.ovf) ok = false;
-                ZE(5);
-            }
-        }
-        const int64_t csize = end - (op + 3);
-        __threadfence_block();
-        if (ok && csize < raw) {
-            put3(dst, op, (uint32_t)((csize << 3) | (2u << 1) | (last ? 1u : 0u)));
-            op = end;
-        } else {
-            put3(dst, op, (uint32_t)((raw << 3) | (last ? 1u : 0u)));  // Raw_Block
-            copy_bytes(dst, op + 3, src, bs, raw);
-            op += 3 + raw;
-        }
-        __threadfence_block();
-        ZE(6);
-        bs = be;
-    } while (!BPAR && bs < n);
-    if (l == 0) {
-        if (BPAR) bsize[wi] = (int32_t)(op - slot0);
-        else ret[b] = op <= cap ? (int32_t)op : -2;
-    }
-    }
-    ZE_FLUSH();
-}
-
-// BPAR: move every frame's blocks from their slots to their places (ascending:
-// a block only moves down, over bytes already moved or its own) and report
-// the frame size.  One wave per frame; first[f] = index of its first item.
-__global__ __launch_bounds__(64) void zstd_compact_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
-                                                         int32_t *__restrict__ ret, const int32_t *__restrict__ bsize,
-                                                         const int32_t *__restrict__ first) {
-    const int f = blockIdx.x;
-    if (f >= nblk) return;
-    const int l = lane_id();
-    const jfs_dev_block d = ((const gc_blk *)blocks)[f];
-    g_u8 *dst = (g_u8 *)d.dst;
-    const int64_t n = d.src_len, cap = d.dst_cap;
-    const int i0 = first[f], i1 = first[f + 1];
-    bool bad = n < 0 || cap < ze_bound(n);
-    for (int i = i0; i < i1 && !bad; i++) bad = bsize[i] < 0;
-    if (bad) {
-        if (l == 0) ret[f] = -2;
+    const int bid = blist[blockIdx.x];
+    BInfo &B = bi[bid];
+    const FInfo F = fi[B.frame];
+    if (F.status < 0) return;
+    const int32_t flags = B.flags;
+    if (flags & F_NOCOMP) {
+        if (l == 0) B.secsz = 0;
         return;
     }
-    const int hn = frame_header(n, false, dst);
-    int64_t out = hn;
-    for (int i = i0; i < i1; i++) {
-        const int64_t from = hn + (int64_t)(i - i0) * SLOT, sz = bsize[i];
-        if (from != out) {
-            // dst[out, out + sz) <- dst[from, from + sz): 16-byte stores, the
-            // source read as aligned dwords (alignbyte), 1 KiB per wave step
-            int64_t x = 0;
-            const uint32_t hm = (uint32_t)(((uintptr_t)(dst + out)) & 15u), ha = (16u - hm) & 15u;
-            const int64_t head = (int64_t)ha < sz ? (int64_t)ha : sz;
-            uint8_t hb = 0;
-            if (l < head) hb = dst[from + l];
-            __builtin_amdgcn_wave_barrier();
-            if (l < head) dst[out + l] = hb;
-            x = head;
-            for (; x + 16 <= sz; x += 1024) {
-                const int64_t y = x + 16 * l;
-                uint4 o = make_uint4(0, 0, 0, 0);
-                const bool on = y + 16 <= sz;
-                if (on) {
-                    const uintptr_t a = (uintptr_t)(dst + from + y);
-                    const gc_u32 *w = (const gc_u32 *)(a & ~(uintptr_t)3);
-                    const uint32_t sh = (uint32_t)(a & 3u);
-                    const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = sh ? w[4] : 0u;
-                    o.x = __builtin_amdgcn_alignbyte(w1, w0, sh);
-                    o.y = __builtin_amdgcn_alignbyte(w2, w1, sh);
-                    o.z = __builtin_amdgcn_alignbyte(w3, w2, sh);
-                    o.w = __builtin_amdgcn_alignbyte(w4, w3, sh);
-                }
-                if (on) *(g_u4 *)(dst + out + y) = o;
+    const Src S = make_src(F.src, F.n);
+    const int32_t ns = B.ns, nl = B.nl, bs = B.bs, be = B.be, bsz = be - bs;
+    const uint64_t *sq = seqs + B.seq_off;
+    g_u8 *lit = (g_u8 *)(bytes + B.lit_off);
+    g_u8 *sec = (g_u8 *)(bytes + B.lit_off + bsz);
+    // ---- 1. literals: runs in sequence order (+ the last literals), gathered
+    // into lit[], histograms per stream segment
+    for (int k = l; k < 4 * 256; k += 64) (&s.h4[0][0])[k] = 0;
+    __syncthreads();
+    const uint32_t seg = (uint32_t)(nl + 3) / 4;
+    {
+        int32_t lbase = 0, sbase = 0;  // literal / source offsets at the chunk start
+        for (int32_t c0 = 0; c0 <= ns; c0 += 64) {
+            const int32_t i = c0 + l;
+            uint32_t ll = 0, ml = 0;
+            if (i < ns) {
+                const uint64_t r = sq[i];
+                ll = (uint32_t)(r & 0x1FFFFu);
+                ml = (uint32_t)((r >> 17) & 0x1FFFFu) + 3;
             }
-            const int64_t xe = head + ((sz - head) & ~(int64_t)15);
-            uint8_t tb = 0;
-            if (xe + l < sz) tb = dst[from + xe + l];
-            if (xe + l < sz) dst[out + xe + l] = tb;
+            uint32_t tl = 0, ts = 0;
+            const uint32_t lp = wave_scan_excl(ll, &tl);
+            const uint32_t sp = wave_scan_excl(ll + ml, &ts);
+            if (i == ns) ll = (uint32_t)(nl - lbase) - lp;  // the last literals: what the runs leave
+            const uint32_t Lc = (ns < c0 + 64) ? tl + readlane(ll, ns - c0) : tl;
+            // byte t of this chunk's literals -> its run (binary search over
+            // the lanes' run starts; runs past the last one excluded)
+            for (uint32_t t0 = 0; t0 < Lc; t0 += 256) {
+                uint32_t bv[4];
+                int32_t xs[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const uint32_t t = t0 + 64 * u + l;
+                    const uint32_t te = t < Lc ? t : Lc - 1;
+                    int lo = 0;
+#pragma unroll
+                    for (int st = 32; st >= 1; st >>= 1) {
+                        const int c = lo + st;
+                        const uint32_t lpc = (uint32_t)__shfl((int)lp, c < 64 ? c : 63, 64);
+                        if (c < 64 && c0 + c <= ns && lpc <= te) lo = c;
+                    }
+                    const uint32_t lpr = (uint32_t)__shfl((int)lp, lo, 64), spr = (uint32_t)__shfl((int)sp, lo, 64);
+                    const int32_t pos = bs + sbase + (int32_t)spr + (int32_t)(te - lpr);
+                    xs[u] = t < Lc ? lbase + (int32_t)t : -1;
+                    bv[u] = t < Lc ? (uint32_t)S.b[pos] : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    if (xs[u] >= 0) {
+                        lit[xs[u]] = (uint8_t)bv[u];
+                        const uint32_t sg = seg ? umin32((uint32_t)xs[u] / seg, 3u) : 0u;
+                        atomicAdd(&s.h4[sg][bv[u]], 1u);
+                    }
+                }
+            }
+            lbase += (int32_t)Lc;
+            sbase += (int32_t)ts;
         }
-        out += sz;
     }
-    if (l == 0) ret[f] = out <= cap ? (int32_t)out : -2;
+    __syncthreads();
+    for (int k = l; k < 4 * 256; k += 64) hist[(int64_t)bid * 1024 + k] = (&s.h4[0][0])[k];
+    // ---- 2. sequences section (ZSTD_entropyCompressSequences_internal after the literals)
+    const int64_t cap = bsz + SEC_EXTRA;
+    int64_t o = 0;
+    if (ns < 128) {
+        if (l == 0) sec[0] = (uint8_t)ns;
+        o = 1;
+    } else if (ns < 0x7F00) {
+        if (l == 0) sec[0] = (uint8_t)((ns >> 8) + 0x80);
+        if (l == 1) sec[1] = (uint8_t)ns;
+        o = 2;
+    } else {
+        if (l == 0) sec[0] = 0xFF;
+        if (l == 1) sec[1] = (uint8_t)(ns - 0x7F00);
+        if (l == 2) sec[2] = (uint8_t)((ns - 0x7F00) >> 8);
+        o = 3;
+    }
+    if (ns == 0) {
+        if (l == 0) {
+            B.secsz = (int32_t)o;
+            B.flags = flags & ~F_LASTNC;
+        }
+        return;
+    }
+    for (int k = l; k < 3 * 64; k += 64) (&s.cnt[0][0])[k] = 0;
+    __syncthreads();
+    for (int32_t i = l; i < ns; i += 64) {
+        const uint64_t r = sq[i];
+        const uint32_t ll = (uint32_t)(r & 0x1FFFFu), mlb = (uint32_t)((r >> 17) & 0x1FFFFu), ofv = (uint32_t)(r >> 34);
+        const uint32_t lc = ll_code(ll), oc = hbit(ofv), mc = ml_code(mlb);
+        atomicAdd(&s.cnt[0][lc], 1u);
+        atomicAdd(&s.cnt[1][oc], 1u);
+        atomicAdd(&s.cnt[2][mc], 1u);
+        if (i == ns - 1) {
+            s.lastc[0] = lc;
+            s.lastc[1] = oc;
+            s.lastc[2] = mc;
+        }
+    }
+    __syncthreads();
+    if (l == 0) {
+        // ZSTD_selectEncodingType (strategy fast) + ZSTD_buildCTable, LL, OF, ML
+        const uint32_t maxs[3] = {35, 31, 52}, flog[3] = {9, 8, 9}, dlog[3] = {6, 5, 6};
+        for (int t = 0; t < 3; t++) {
+            uint32_t *cnt = s.cnt[t];
+            uint32_t max = maxs[t];
+            while (!cnt[max]) max--;
+            uint32_t mf = 0;
+            for (uint32_t v = 0; v <= max; v++) mf = cnt[v] > mf ? cnt[v] : mf;
+            const bool defOK = t != 1 || max <= 28;
+            int type;
+            if (mf == (uint32_t)ns) {
+                type = (defOK && ns <= 2) ? 0 : 1;
+            } else {
+                type = 2;
+                if (defOK) {
+                    const uint32_t dynMin = ((1u << dlog[t]) * 9u) >> 3;
+                    if ((uint32_t)ns < dynMin || mf < ((uint32_t)ns >> (dlog[t] - 1))) type = 0;
+                }
+            }
+            s.type[t] = type;
+            s.hsz[t] = 0;
+            if (type == 1) {  // set_rle
+                s.hdr[t][0] = (uint8_t)max;
+                s.hsz[t] = 1;
+                if (t == 0) build_rle(s.tLL, max);
+                else if (t == 1) build_rle(s.tOF, max);
+                else build_rle(s.tML, max);
+            } else if (type == 0) {  // set_basic
+                if (t == 0) build_ctab(s.tsym, s.tLL, LL_DEF, 35, 6);
+                else if (t == 1) build_ctab(s.tsym, s.tOF, OF_DEF, 28, 5);
+                else build_ctab(s.tsym, s.tML, ML_DEF, 52, 6);
+            } else {  // set_compressed
+                uint32_t nb1 = (uint32_t)ns;
+                const uint32_t tlog = fse_opt_tlog(flog[t], (uint32_t)ns, max, 2);
+                if (cnt[s.lastc[t]] > 1) {
+                    cnt[s.lastc[t]]--;
+                    nb1--;
+                }
+                fse_normalize(s.norm, tlog, cnt, nb1, max, nb1 >= 2048);
+                s.hsz[t] = write_ncount(s.hdr[t], s.norm, max, tlog);
+                if (t == 0) build_ctab(s.tsym, s.tLL, s.norm, max, tlog);
+                else if (t == 1) build_ctab(s.tsym, s.tOF, s.norm, max, tlog);
+                else build_ctab(s.tsym, s.tML, s.norm, max, tlog);
+            }
+        }
+    }
+    __syncthreads();
+    // header: Symbol_Compression_Modes, then LL, OF, ML table descriptions
+    if (l == 0) sec[o] = (uint8_t)((s.type[0] << 6) + (s.type[1] << 4) + (s.type[2] << 2));
+    o += 1;
+    int64_t lastnc = -1;
+    for (int t = 0; t < 3; t++) {
+        if (s.type[t] == 2) lastnc = o;
+        for (int k = l; k < s.hsz[t]; k += 64) sec[o + k] = s.hdr[t][k];
+        o += s.hsz[t];
+    }
+    // ZSTD_encodeSequences: last sequence first; per 64 sequences the lanes
+    // look up everything that does not depend on the states, the serial loop
+    // steps the three states and packs the bits
+    BitW w;
+    w.dst = sec;
+    w.wp = o;
+    w.lim = cap;
+    w.bc = 0;
+    w.bp = 0;
+    w.ovf = false;
+    uint32_t sML = 0, sOF = 0, sLL = 0;
+    for (int64_t c0 = ns - 1; c0 >= 0; c0 -= 64) {
+        const int64_t i = c0 - l;
+        uint32_t ll = 0, mlb = 0, ofv = 1;
+        if (i >= 0) {
+            const uint64_t r = sq[i];
+            ll = (uint32_t)(r & 0x1FFFFu);
+            mlb = (uint32_t)((r >> 17) & 0x1FFFFu);
+            ofv = (uint32_t)(r >> 34);
+        }
+        const uint32_t lc = ll_code(ll), mc = ml_code(mlb), oc = hbit(ofv);
+        const int32_t dO = s.tOF.dnb[oc], dM = s.tML.dnb[mc], dL = s.tLL.dnb[lc];
+        const int32_t fO = s.tOF.dfs[oc], fM = s.tML.dfs[mc], fL = s.tLL.dfs[lc];
+        const uint32_t nbits = (uint32_t)LL_BITS[lc] | ((uint32_t)ML_BITS[mc] << 8) | (oc << 16);
+        const int nj = c0 + 1 < 64 ? (int)(c0 + 1) : 64;
+        for (int jj = 0; jj < nj; ++jj) {
+            const int32_t jdO = (int32_t)readlane((uint32_t)dO, jj), jdM = (int32_t)readlane((uint32_t)dM, jj),
+                          jdL = (int32_t)readlane((uint32_t)dL, jj);
+            const int32_t jfO = (int32_t)readlane((uint32_t)fO, jj), jfM = (int32_t)readlane((uint32_t)fM, jj),
+                          jfL = (int32_t)readlane((uint32_t)fL, jj);
+            const uint32_t jnb = readlane(nbits, jj);
+            const uint32_t jll = readlane(ll, jj), jml = readlane(mlb, jj), jof = readlane(ofv, jj);
+            if (c0 == ns - 1 && jj == 0) {  // FSE_initCState2 with the last sequence
+                const uint32_t nM = (uint32_t)((jdM + (1 << 15)) >> 16), nO = (uint32_t)((jdO + (1 << 15)) >> 16),
+                               nL = (uint32_t)((jdL + (1 << 15)) >> 16);
+                sML = s.tML.st[(((nM << 16) - (uint32_t)jdM) >> nM) + (uint32_t)jfM];
+                sOF = s.tOF.st[(((nO << 16) - (uint32_t)jdO) >> nO) + (uint32_t)jfO];
+                sLL = s.tLL.st[(((nL << 16) - (uint32_t)jdL) >> nL) + (uint32_t)jfL];
+            } else {
+                const uint32_t nO = (uint32_t)(((int32_t)sOF + jdO) >> 16), nM = (uint32_t)(((int32_t)sML + jdM) >> 16),
+                               nL = (uint32_t)(((int32_t)sLL + jdL) >> 16);
+                bw_add(w, sOF, (int)nO);
+                bw_add(w, sML, (int)nM);
+                bw_add(w, sLL, (int)nL);
+                const uint32_t tO = s.tOF.st[(sOF >> nO) + (uint32_t)jfO], tM = s.tML.st[(sML >> nM) + (uint32_t)jfM],
+                               tL = s.tLL.st[(sLL >> nL) + (uint32_t)jfL];
+                sOF = tO;
+                sML = tM;
+                sLL = tL;
+                bw_flush(w);
+            }
+            bw_add(w, jll, (int)(jnb & 0xFFu));
+            bw_add(w, jml, (int)((jnb >> 8) & 0xFFu));
+            bw_flush(w);
+            bw_add(w, jof, (int)(jnb >> 16));
+            bw_flush(w);
+        }
+    }
+    bw_add(w, sML, s.tML.tlog);
+    bw_flush(w);
+    bw_add(w, sOF, s.tOF.tlog);
+    bw_flush(w);
+    bw_add(w, sLL, s.tLL.tlog);
+    bw_flush(w);
+    bw_add(w, 1, 1);  // end mark
+    bw_flush(w);
+    if (w.bp > 0) {
+        if (w.wp + 1 > w.lim) w.ovf = true;
+        if (!w.ovf && l == 0) w.dst[w.wp] = (uint8_t)w.bc;
+        w.wp++;
+    }
+    if (l == 0) {
+        B.secsz = w.ovf ? -1 : (int32_t)w.wp;
+        // zstd <= 1.3.4 decoder workaround: a last FSE_Compressed table
+        // description closer than 4 bytes to the end -> raw block
+        B.flags = (lastnc >= 0 && w.wp - lastnc < 4) ? (flags | F_LASTNC) : (flags & ~F_LASTNC);
+    }
 }
 
-}  // namespace zstde
+// ---------------------------------------------------------------------------
+// kernel 3: literal sections, block decisions and the frame bytes (one wave
+// per frame, blocks in order)
+// ---------------------------------------------------------------------------
+struct HNode {
+    uint32_t count;
+    uint16_t parent;
+    uint8_t byte, nbBits;
+};
+struct LitSmem {
+    uint8_t pnb[256];   // previous (confirmed) Huffman table: code lengths
+    uint16_t pval[256]; //                                      codes
+    uint8_t nnb[256];   // this block's new table
+    uint16_t nval[256];
+    uint32_t cnt[4][256];
+    uint32_t tot[256];
+    HNode node[2 * 256 + 2];
+    uint8_t hdr[160];
+    uint8_t wt[256];
+    int16_t wnorm[16];
+    uint32_t wcnt[16];
+    uint8_t wtsym[64];
+    CTab<64, 16> wct;
+    uint32_t ring[256];  // Huffman stream staging (8,192 bits)
+    int32_t hs, maxbits;
+};
+
+// HUF_setMaxHeight
+__device__ uint32_t huf_set_max_height(HNode *huffNode, uint32_t lastNonNull, uint32_t maxNbBits) {
+    const uint32_t largestBits = huffNode[lastNonNull].nbBits;
+    if (largestBits <= maxNbBits) return largestBits;
+    int totalCost = 0;
+    const uint32_t baseCost = 1u << (largestBits - maxNbBits);
+    int n = (int)lastNonNull;
+    while (huffNode[n].nbBits > maxNbBits) {
+        totalCost += (int)(baseCost - (1u << (largestBits - huffNode[n].nbBits)));
+        huffNode[n].nbBits = (uint8_t)maxNbBits;
+        n--;
+    }
+    while (huffNode[n].nbBits == maxNbBits) n--;
+    totalCost >>= (largestBits - maxNbBits);
+    const uint32_t noSymbol = 0xF0F0F0F0u;
+    uint32_t rankLast[14];
+    for (int i = 0; i < 14; i++) rankLast[i] = noSymbol;
+    {
+        uint32_t currentNbBits = maxNbBits;
+        for (int pos = n; pos >= 0; pos--) {
+            if (huffNode[pos].nbBits >= currentNbBits) continue;
+            currentNbBits = huffNode[pos].nbBits;
+            rankLast[maxNbBits - currentNbBits] = (uint32_t)pos;
+        }
+    }
+    for (int guard = 0; totalCost > 0 && guard < 100000; guard++) {
+        uint32_t nBitsToDecrease = hbit((uint32_t)totalCost) + 1;
+        for (; nBitsToDecrease > 1; nBitsToDecrease--) {
+            const uint32_t highPos = rankLast[nBitsToDecrease], lowPos = rankLast[nBitsToDecrease - 1];
+            if (highPos == noSymbol) continue;
+            if (lowPos == noSymbol) break;
+            const uint32_t highTotal = huffNode[highPos].count, lowTotal = 2 * huffNode[lowPos].count;
+            if (highTotal <= lowTotal) break;
+        }
+        while (nBitsToDecrease <= 12 && rankLast[nBitsToDecrease] == noSymbol) nBitsToDecrease++;
+        totalCost -= 1 << (nBitsToDecrease - 1);
+        if (rankLast[nBitsToDecrease - 1] == noSymbol) rankLast[nBitsToDecrease - 1] = rankLast[nBitsToDecrease];
+        huffNode[rankLast[nBitsToDecrease]].nbBits++;
+        if (rankLast[nBitsToDecrease] == 0)
+            rankLast[nBitsToDecrease] = noSymbol;
+        else {
+            rankLast[nBitsToDecrease]--;
+            if (huffNode[rankLast[nBitsToDecrease]].nbBits != maxNbBits - nBitsToDecrease)
+                rankLast[nBitsToDecrease] = noSymbol;
+        }
+    }
+    for (int guard = 0; totalCost < 0 && guard < 100000; guard++) {
+        if (rankLast[1] == noSymbol) {
+            while (huffNode[n].nbBits == maxNbBits) n--;
+            huffNode[n + 1].nbBits--;
+            rankLast[1] = (uint32_t)(n + 1);
+            totalCost++;
+            continue;
+        }
+        huffNode[rankLast[1] + 1].nbBits--;
+        rankLast[1]++;
+        totalCost++;
+    }
+    return maxNbBits;
+}
+
+// HUF_buildCTable_wksp into (nnb, nval); lane 0; returns the max code length
+__device__ uint32_t huf_build(LitSmem &s, uint32_t maxsv, uint32_t maxNbBits) {
+    HNode *const huffNode = s.node + 1;
+    const int STARTNODE = 256;
+    for (int i = 0; i < 2 * 256 + 2; i++) {
+        s.node[i].count = 0;
+        s.node[i].parent = 0;
+        s.node[i].byte = 0;
+        s.node[i].nbBits = 0;
+    }
+    int m = 0;
+    for (uint32_t i = 0; i <= maxsv; i++) {  // stable sort, decreasing count
+        const uint32_t c = s.tot[i];
+        int pos = m++;
+        while (pos > 0 && c > huffNode[pos - 1].count) {
+            huffNode[pos] = huffNode[pos - 1];
+            pos--;
+        }
+        huffNode[pos].count = c;
+        huffNode[pos].byte = (uint8_t)i;
+        huffNode[pos].parent = 0;
+        huffNode[pos].nbBits = 0;
+    }
+    int nonNullRank = (int)maxsv;
+    while (huffNode[nonNullRank].count == 0) nonNullRank--;
+    int lowS = nonNullRank, nodeNb = STARTNODE;
+    const int nodeRoot = nodeNb + lowS - 1;
+    int lowN = nodeNb;
+    huffNode[nodeNb].count = huffNode[lowS].count + huffNode[lowS - 1].count;
+    huffNode[lowS].parent = huffNode[lowS - 1].parent = (uint16_t)nodeNb;
+    nodeNb++;
+    lowS -= 2;
+    for (int n = nodeNb; n <= nodeRoot; n++) huffNode[n].count = 1u << 30;
+    s.node[0].count = 1u << 31;
+    while (nodeNb <= nodeRoot) {
+        const int n1 = (huffNode[lowS].count < huffNode[lowN].count) ? lowS-- : lowN++;
+        const int n2 = (huffNode[lowS].count < huffNode[lowN].count) ? lowS-- : lowN++;
+        huffNode[nodeNb].count = huffNode[n1].count + huffNode[n2].count;
+        huffNode[n1].parent = huffNode[n2].parent = (uint16_t)nodeNb;
+        nodeNb++;
+    }
+    huffNode[nodeRoot].nbBits = 0;
+    for (int n = nodeRoot - 1; n >= STARTNODE; n--) huffNode[n].nbBits = huffNode[huffNode[n].parent].nbBits + 1;
+    for (int n = 0; n <= nonNullRank; n++) huffNode[n].nbBits = huffNode[huffNode[n].parent].nbBits + 1;
+    maxNbBits = huf_set_max_height(huffNode, (uint32_t)nonNullRank, maxNbBits);
+    uint16_t nbPerRank[13], valPerRank[13];
+    for (int i = 0; i < 13; i++) nbPerRank[i] = valPerRank[i] = 0;
+    for (int n = 0; n <= nonNullRank; n++) nbPerRank[huffNode[n].nbBits]++;
+    {
+        uint16_t mn = 0;
+        for (int n = (int)maxNbBits; n > 0; n--) {
+            valPerRank[n] = mn;
+            mn += nbPerRank[n];
+            mn >>= 1;
+        }
+    }
+    for (int i = 0; i < 256; i++) {
+        s.nnb[i] = 0;
+        s.nval[i] = 0;
+    }
+    for (int n = 0; n <= (int)maxsv; n++) s.nnb[huffNode[n].byte] = huffNode[n].nbBits;
+    for (int n = 0; n <= (int)maxsv; n++) s.nval[n] = valPerRank[s.nnb[n]]++;
+    return maxNbBits;
+}
+
+// HUF_writeCTable (weights FSE-compressed when that is smaller) into s.hdr; lane 0; 0 = impossible
+__device__ int huf_write_ctable(LitSmem &s, uint32_t maxsv, uint32_t huffLog) {
+    uint8_t b2w[13];
+    b2w[0] = 0;
+    for (uint32_t n = 1; n < huffLog + 1; n++) b2w[n] = (uint8_t)(huffLog + 1 - n);
+    for (uint32_t n = 0; n < maxsv; n++) s.wt[n] = b2w[s.nnb[n]];
+    // HUF_compressWeights
+    const uint32_t wtSize = maxsv;
+    int hsz = 0;
+    if (wtSize > 1) {
+        for (int i = 0; i < 16; i++) s.wcnt[i] = 0;
+        for (uint32_t i = 0; i < wtSize; i++) s.wcnt[s.wt[i]]++;
+        uint32_t wmax = 12;
+        while (!s.wcnt[wmax]) wmax--;
+        uint32_t maxc = 0;
+        for (uint32_t i = 0; i <= wmax; i++) maxc = s.wcnt[i] > maxc ? s.wcnt[i] : maxc;
+        if (maxc == wtSize) {
+            hsz = 1;
+        } else if (maxc == 1) {
+            hsz = 0;
+        } else {
+            const uint32_t tlog = fse_opt_tlog(6, wtSize, wmax, 2);
+            if (fse_normalize(s.wnorm, tlog, s.wcnt, wtSize, wmax, false) >= 0) {
+                int o = 1 + write_ncount(s.hdr + 1, s.wnorm, wmax, tlog);
+                build_ctab(s.wtsym, s.wct, s.wnorm, wmax, tlog);
+                // FSE_compress_usingCTable: two states, last symbols first
+                uint64_t bc = 0;
+                int bp = 0;
+                const int lim = 159;
+                auto flush = [&]() {
+                    while (bp >= 8) {
+                        if (o < lim) s.hdr[o] = (uint8_t)bc;
+                        o++;
+                        bc >>= 8;
+                        bp -= 8;
+                    }
+                };
+                auto add = [&](uint32_t v, int nb) {
+                    bc |= ((uint64_t)v & ((1ull << nb) - 1ull)) << bp;
+                    bp += nb;
+                };
+                auto init = [&](uint32_t sym) -> uint32_t {
+                    const int32_t dnb = s.wct.dnb[sym];
+                    const uint32_t nbo = (uint32_t)((dnb + (1 << 15)) >> 16);
+                    return s.wct.st[(((nbo << 16) - (uint32_t)dnb) >> nbo) + (uint32_t)s.wct.dfs[sym]];
+                };
+                auto enc = [&](uint32_t &st, uint32_t sym) {
+                    const uint32_t nbo = (uint32_t)(((int32_t)st + s.wct.dnb[sym]) >> 16);
+                    add(st, (int)nbo);
+                    st = s.wct.st[(st >> nbo) + (uint32_t)s.wct.dfs[sym]];
+                };
+                int ip = (int)wtSize;
+                uint32_t s1, s2;
+                if (wtSize > 2) {
+                    if (wtSize & 1) {
+                        s1 = init(s.wt[--ip]);
+                        s2 = init(s.wt[--ip]);
+                        enc(s1, s.wt[--ip]);
+                        flush();
+                    } else {
+                        s2 = init(s.wt[--ip]);
+                        s1 = init(s.wt[--ip]);
+                    }
+                    if ((wtSize - 2) & 2) {
+                        enc(s2, s.wt[--ip]);
+                        enc(s1, s.wt[--ip]);
+                        flush();
+                    }
+                    while (ip > 0) {
+                        enc(s2, s.wt[--ip]);
+                        enc(s1, s.wt[--ip]);
+                        enc(s2, s.wt[--ip]);
+                        enc(s1, s.wt[--ip]);
+                        flush();
+                    }
+                    add(s2, (int)tlog);
+                    flush();
+                    add(s1, (int)tlog);
+                    flush();
+                    add(1, 1);
+                    flush();
+                    if (bp > 0) {
+                        if (o < lim) s.hdr[o] = (uint8_t)bc;
+                        o++;
+                    }
+                    hsz = o - 1;
+                } else {
+                    hsz = 0;
+                }
+            }
+        }
+    }
+    if (hsz > 1 && hsz < (int)(maxsv / 2)) {
+        s.hdr[0] = (uint8_t)hsz;
+        return hsz + 1;
+    }
+    if (maxsv > 128) return 0;
+    s.hdr[0] = (uint8_t)(128 + (maxsv - 1));
+    s.wt[maxsv] = 0;
+    for (uint32_t n = 0; n < maxsv; n += 2) s.hdr[n / 2 + 1] = (uint8_t)((s.wt[n] << 4) + s.wt[n + 1]);
+    return (int)((maxsv + 1) / 2 + 1);
+}
+
+// wave copy dst[0, len) <- src[0, len): 16-byte aligned stores, dword loads
+// of the source that never touch a dword without a source byte
+__device__ void wave_copy(g_u8 *dst, const uint8_t *srcp, int64_t len) {
+    const int l = lane_id();
+    if (len <= 0) return;
+    const int64_t h16 = (int64_t)((16u - (uint32_t)((uintptr_t)dst & 15u)) & 15u);
+    const int64_t head = len < h16 ? len : h16;
+    const gc_u8 *sb = (const gc_u8 *)srcp;
+    if (l < head) dst[l] = sb[l];
+    const Src S = make_src(srcp, (int32_t)(len < 0x7FFFFFFF ? len : 0x7FFFFFFF));
+    int64_t x = head;
+    for (; x + 16 <= len; x += 1024) {
+        const int64_t y = x + 16 * l;
+        if (y + 16 <= len) *(g_u4 *)(dst + y) = ld128(S, (int32_t)y);
+    }
+    const int64_t xe = head + ((len - head) & ~(int64_t)15);
+    if (xe + l < len) dst[xe + l] = sb[xe + l];
+}
+
+__device__ __forceinline__ void put_bytes(g_u8 *dst, int64_t o, uint64_t v, int n) {
+    const int l = lane_id();
+    if (l < n) dst[o + l] = (uint8_t)(v >> (8 * l));
+}
+
+// encode literals lit[a, b) with table (nb, val), last symbol first, into dst
+// at byte o; returns the stream bytes (end mark included)
+__device__ int64_t huf_stream(LitSmem &s, const uint8_t *tnb, const uint16_t *tval, const gc_u8 *lit, int32_t a,
+                              int32_t b, g_u8 *dst, int64_t o) {
+    const int l = lane_id();
+    // ring bit 0 = bit 0 of the dword at (dst + o) & ~3
+    const uint32_t boff = (uint32_t)((uintptr_t)(dst + o) & 3u) * 8u;
+    g_u8 *base = (g_u8 *)((uintptr_t)(dst + o) & ~(uintptr_t)3);
+    g_u32 *wbase = (g_u32 *)base;
+    const int64_t first_byte = (int64_t)(boff >> 3);  // bytes of dword 0 before the stream: keep
+    for (int k = l; k < 256; k += 64) s.ring[k] = 0;
+    __syncthreads();
+    uint64_t bitpos = boff;  // absolute bit position from base
+    uint64_t flushed = 0;    // dwords stored
+    for (int32_t c0 = b - 1; c0 >= a; c0 -= 64) {
+        const int32_t i = c0 - l;
+        uint32_t len = 0, code = 0;
+        if (i >= a) {
+            const uint32_t sym = lit[i];
+            len = tnb[sym];
+            code = tval[sym];
+        }
+        uint32_t tot = 0;
+        const uint32_t ex = wave_scan_excl(len, &tot);
+        if (len) {
+            const uint64_t p = bitpos + ex;
+            const uint32_t d = (uint32_t)(p >> 5) & 255u, sh = (uint32_t)(p & 31u);
+            atomicOr(&s.ring[d], code << sh);
+            if (sh + len > 32) atomicOr(&s.ring[(d + 1) & 255u], code >> (32 - sh));
+        }
+        __syncthreads();
+        bitpos += tot;
+        // store the complete dwords
+        const uint64_t full = bitpos >> 5;
+        for (uint64_t dw = flushed + l; dw < full; dw += 64) {
+            const uint32_t v = s.ring[dw & 255u];
+            if (dw == 0 && first_byte > 0) {
+                for (int k = (int)first_byte; k < 4; k++) base[k] = (uint8_t)(v >> (8 * k));
+            } else {
+                wbase[dw] = v;
+            }
+            s.ring[dw & 255u] = 0;
+        }
+        __syncthreads();
+        flushed = full;
+    }
+    // end mark, last partial dword (bytes up to the end only)
+    if (l == 0) {
+        const uint32_t d = (uint32_t)(bitpos >> 5) & 255u, sh = (uint32_t)(bitpos & 31u);
+        s.ring[d] |= 1u << sh;
+    }
+    __syncthreads();
+    bitpos += 1;
+    const uint64_t endbyte = (bitpos + 7) >> 3;  // bytes from base
+    const uint64_t lastdw = (endbyte + 3) >> 2;
+    for (uint64_t dw = flushed + l; dw < lastdw; dw += 64) {
+        const uint32_t v = s.ring[dw & 255u];
+        const int64_t b0 = (int64_t)dw * 4;
+        for (int k = 0; k < 4; k++) {
+            const int64_t by = b0 + k;
+            if (by >= first_byte && by < (int64_t)endbyte) base[by] = (uint8_t)(v >> (8 * k));
+        }
+    }
+    __syncthreads();
+    return (int64_t)endbyte - first_byte;
+}
+
+__global__ __launch_bounds__(64) void zl1_lit_kernel(FInfo *__restrict__ fi, const int32_t *__restrict__ flist,
+                                                     BInfo *__restrict__ bi, const uint8_t *__restrict__ bytes,
+                                                     const uint32_t *__restrict__ hist, int32_t *__restrict__ ret) {
+    __shared__ LitSmem s;
+    const int l = lane_id();
+    const int fidx = flist[blockIdx.x];
+    FInfo &FR = fi[fidx];
+    const FInfo F = FR;
+    if (F.status < 0) return;
+    g_u8 *dst = (g_u8 *)F.dst;
+    const Src S = make_src(F.src, F.n);
+    // frame header (ZSTD_writeFrameHeader: no checksum, no dictionary, FCS)
+    const uint32_t n = (uint32_t)F.n;
+    const bool single = (1u << F.wlog) >= n;
+    const uint32_t fcs = (n >= 256) + (n >= 65536 + 256);
+    int64_t op = 0;
+    {
+        uint64_t hv = 0xFD2FB528ull | ((uint64_t)((single ? 0x20 : 0) | (fcs << 6)) << 32);
+        int hn = 5;
+        if (!single) {
+            hv |= (uint64_t)((F.wlog - 10) << 3) << 40;
+            hn = 6;
+        }
+        put_bytes(dst, 0, hv, hn);
+        op = hn;
+        if (fcs == 0) {
+            if (single) {
+                put_bytes(dst, op, n, 1);
+                op += 1;
+            }
+        } else if (fcs == 1) {
+            put_bytes(dst, op, n - 256, 2);
+            op += 2;
+        } else {
+            put_bytes(dst, op, n, 4);
+            op += 4;
+        }
+    }
+    if (F.nb == 0) {  // empty input: one last empty raw block
+        put_bytes(dst, op, 1, 3);
+        op += 3;
+    }
+    for (int k = l; k < 256; k += 64) {
+        s.pnb[k] = 0;
+        s.pval[k] = 0;
+    }
+    int prep = 0;  // HUF repeat mode of the previous confirmed table: 0 none, 1 check
+    __syncthreads();
+    for (int32_t k = 0; k < F.nb; k++) {
+        BInfo &B = bi[F.b0 + k];
+        const int32_t bs = B.bs, be = B.be, bsz = be - bs, flags = B.flags;
+        const bool last = k == F.nb - 1;
+        const uint8_t *lit8 = bytes + B.lit_off;
+        const gc_u8 *lit = (const gc_u8 *)lit8;
+        int64_t cS = 0;
+        int lkind = 0;  // literal section: 0 raw, 1 RLE, 2 Huffman new table, 3 Huffman previous table
+        int64_t litsz = 0, clit = 0;
+        bool single = false;
+        int32_t L = 0;
+        if (!(flags & F_NOCOMP)) {
+            L = B.nl;
+            for (int i = l; i < 1024; i += 64) (&s.cnt[0][0])[i] = hist[(int64_t)(F.b0 + k) * 1024 + i];
+            __syncthreads();
+            for (int i = l; i < 256; i += 64) s.tot[i] = s.cnt[0][i] + s.cnt[1][i] + s.cnt[2][i] + s.cnt[3][i];
+            __syncthreads();
+            // ---- ZSTD_compressLiterals + HUF_compress_internal
+            const int64_t fl = 1 + (L > 31) + (L > 4095);
+            const int32_t minGain = (L >> 6) + 2;
+            const int lh = 3 + (L >= 1024) + (L >= 16384);
+            single = L < 256;
+            lkind = 0;
+            if (L > 63) {
+                uint32_t mx = 0, largest = 0;
+                for (int i = l; i < 256; i += 64)
+                    if (s.tot[i]) mx = umax32(mx, (uint32_t)i);
+                for (int i = l; i < 256; i += 64) largest = umax32(largest, s.tot[i]);
+                const uint32_t maxsv = dwave_max(mx);
+                largest = dwave_max(largest);
+                int repeat = prep;
+                const bool prefer = L <= 1024;
+                if (largest == (uint32_t)L) {
+                    clit = 1;
+                } else if (largest <= (uint32_t)(L >> 7) + 4) {
+                    clit = 0;
+                } else {
+                    if (repeat == 1) {
+                        bool bad = false;
+                        for (int i = l; i < 256; i += 64) bad |= (s.tot[i] != 0) && (s.pnb[i] == 0);
+                        if (ballot(bad)) repeat = 0;
+                    }
+                    // exact stream sizes of a table: sum of code bits per segment
+                    auto streams = [&](const uint8_t *tnb) -> int64_t {
+                        uint32_t b0 = 0, b1 = 0, b2 = 0, b3 = 0;
+                        for (int i = l; i < 256; i += 64) {
+                            b0 += s.cnt[0][i] * tnb[i];
+                            b1 += s.cnt[1][i] * tnb[i];
+                            b2 += s.cnt[2][i] * tnb[i];
+                            b3 += s.cnt[3][i] * tnb[i];
+                        }
+                        b0 = dwave_sum(b0); b1 = dwave_sum(b1); b2 = dwave_sum(b2); b3 = dwave_sum(b3);
+                        if (single) return (int64_t)((b0 + b1 + b2 + b3 + 1 + 7) >> 3);
+                        return 6 + (int64_t)((b0 + 8) >> 3) + ((b1 + 8) >> 3) + ((b2 + 8) >> 3) + ((b3 + 8) >> 3);
+                    };
+                    auto estimate = [&](const uint8_t *tnb) -> int64_t {
+                        uint32_t a = 0;
+                        for (int i = l; i < 256; i += 64) a += s.tot[i] * tnb[i];
+                        return (int64_t)(dwave_sum(a) >> 3);
+                    };
+                    auto ct_internal = [&](const uint8_t *tnb, int64_t hs) -> int64_t {
+                        const int64_t t = hs + streams(tnb);
+                        return t >= L - 1 ? 0 : t;
+                    };
+                    if (prefer && repeat != 0) {
+                        clit = ct_internal(s.pnb, 0);
+                        lkind = 3;
+                    } else {
+                        const uint32_t hlog0 = fse_opt_tlog(11, (uint32_t)L, maxsv, 1);
+                        if (l == 0) {
+                            s.maxbits = (int32_t)huf_build(s, maxsv, hlog0);
+                            s.hs = huf_write_ctable(s, maxsv, (uint32_t)s.maxbits);
+                        }
+                        __syncthreads();
+                        const int64_t hs = s.hs;
+                        bool decided = false;
+                        if (hs == 0) {
+                            clit = 0;
+                            decided = true;
+                        } else if (repeat != 0) {
+                            const int64_t oldSize = estimate(s.pnb), newSize = estimate(s.nnb);
+                            if (oldSize <= hs + newSize || hs + 12 >= L) {
+                                clit = ct_internal(s.pnb, 0);
+                                lkind = 3;
+                                decided = true;
+                            }
+                        }
+                        if (!decided) {
+                            if (hs + 12 >= L) {
+                                clit = 0;
+                            } else {
+                                clit = ct_internal(s.nnb, hs);
+                                lkind = 2;
+                            }
+                        }
+                    }
+                }
+                if (clit == 0 || clit >= L - minGain) {
+                    lkind = 0;
+                } else if (clit == 1) {
+                    lkind = 1;
+                }
+            }
+            litsz = lkind == 0 ? fl + L : lkind == 1 ? fl + 1 : lh + clit;
+            // ---- the block: ZSTD_entropyCompressSequences + ZSTD_compressBlock_internal
+            const int32_t secsz = B.secsz;
+            if (secsz < 0 || (flags & F_LASTNC)) {
+                cS = 0;
+            } else {
+                const int64_t c = litsz + secsz;
+                cS = c >= (int64_t)bsz - ((bsz >> 6) + 2) ? 0 : c;
+            }
+            if (k > 0 && cS < 25 && (flags & F_RLE)) cS = 1;
+        }
+        const bool confirmed = cS > 1;
+        const bool assumed = (flags & F_ASSUMED) != 0;
+        if (confirmed != assumed && !last && (B.rout0 != B.rin0 || B.rout1 != B.rin1)) {
+            // the parse handed the wrong offsets to block k + 1: parse again
+            // with this block's outcome known
+            for (int32_t i = l; i <= k; i += 64) {
+                BInfo &Bi = bi[F.b0 + i];
+                if (i < k) Bi.conf = (Bi.flags & F_ASSUMED) ? 1 : 2;
+            }
+            if (l == 0) {
+                B.conf = confirmed ? 1 : 2;
+                FR.status = 1;
+            }
+            return;
+        }
+        // ---- write the block
+        if (cS == 0) {
+            put_bytes(dst, op, (uint32_t)(last ? 1 : 0) | ((uint32_t)bsz << 3), 3);
+            wave_copy(dst + op + 3, F.src + bs, bsz);
+            op += 3 + bsz;
+        } else if (cS == 1) {
+            put_bytes(dst, op, (uint32_t)(last ? 1 : 0) | (1u << 1) | ((uint32_t)bsz << 3), 3);
+            if (l == 0) dst[op + 3] = S.b[bs];
+            op += 4;
+        } else {
+            put_bytes(dst, op, (uint32_t)(last ? 1 : 0) | (2u << 1) | ((uint32_t)cS << 3), 3);
+            int64_t o = op + 3;
+            const int64_t fl = 1 + (L > 31) + (L > 4095);
+            if (lkind == 0 || lkind == 1) {
+                const uint32_t t = lkind;
+                const uint64_t hv = fl == 1 ? (t | ((uint64_t)L << 3))
+                                            : fl == 2 ? (t | (1u << 2) | ((uint64_t)L << 4)) : (t | (3u << 2) | ((uint64_t)L << 4));
+                put_bytes(dst, o, hv, (int)fl);
+                o += fl;
+                if (lkind == 0) {
+                    wave_copy(dst + o, lit8, L);
+                    o += L;
+                } else {
+                    if (l == 0) dst[o] = lit[0];
+                    o += 1;
+                }
+            } else {
+                const int lh = 3 + (L >= 1024) + (L >= 16384);
+                const uint64_t ht = lkind == 2 ? 2 : 3;
+                uint64_t hv;
+                if (lh == 3) hv = ht | ((uint64_t)(single ? 0 : 1) << 2) | ((uint64_t)L << 4) | ((uint64_t)clit << 14);
+                else if (lh == 4) hv = ht | (2ull << 2) | ((uint64_t)L << 4) | ((uint64_t)clit << 18);
+                else hv = ht | (3ull << 2) | ((uint64_t)L << 4) | ((uint64_t)clit << 22);
+                put_bytes(dst, o, hv, lh);
+                o += lh;
+                const uint8_t *tnb = lkind == 2 ? s.nnb : s.pnb;
+                const uint16_t *tval = lkind == 2 ? s.nval : s.pval;
+                if (lkind == 2) {
+                    for (int i = l; i < s.hs; i += 64) dst[o + i] = s.hdr[i];
+                    o += s.hs;
+                }
+                if (single) {
+                    o += huf_stream(s, tnb, tval, lit, 0, L, dst, o);
+                } else {
+                    const int32_t sg = (L + 3) / 4;
+                    const int64_t jt = o;
+                    o += 6;
+                    int64_t sz[4];
+                    for (int q = 0; q < 4; q++) {
+                        const int32_t a = q * sg, b = q < 3 ? a + sg : L;
+                        sz[q] = huf_stream(s, tnb, tval, lit, a, b, dst, o);
+                        o += sz[q];
+                    }
+                    put_bytes(dst, jt, (uint64_t)sz[0] | ((uint64_t)sz[1] << 16) | ((uint64_t)sz[2] << 32), 6);
+                }
+            }
+            // the sequences section
+            wave_copy(dst + o, bytes + B.lit_off + bsz, B.secsz);
+            o += B.secsz;
+            op = o;
+        }
+        __syncthreads();
+        if (confirmed && lkind == 2) {  // this block's new table becomes the previous table
+            for (int i = l; i < 256; i += 64) {
+                s.pnb[i] = s.nnb[i];
+                s.pval[i] = s.nval[i];
+            }
+            prep = 1;
+        }
+        __syncthreads();
+    }
+    if (l == 0) {
+        ret[fidx] = op <= F.cap ? (int32_t)op : -2;
+        FR.status = 0;
+    }
+}
+
+}  // namespace zl1
 }  // namespace jfs
 
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
 namespace {
-struct ZEScratch {
+using namespace jfs::zl1;
+struct ZL1Scratch {
     std::mutex mu;
-    uint64_t *d = nullptr;
-    size_t cap = 0;  // waves
-    uint8_t *aux = nullptr;  // BPAR work list, frame starts, block sizes
-    size_t aux_cap = 0;
-    int waves = 0;   // resident encoder waves on this device (BPAR grid)
-    bool grow(size_t w) {
-        if (d) (void)hipFree(d);  // hipFree synchronises with work still using it
+    uint8_t *d = nullptr;
+    size_t cap = 0;
+    bool grow(size_t need) {
+        if (cap >= need) return true;
+        if (d) (void)hipFree(d);  // hipFree waits for work still using it
         d = nullptr;
         cap = 0;
-        if (hipMalloc((void **)&d, (size_t)jfs::zstde::SCR_PER * w) != hipSuccess) return false;
-        cap = w;
+        size_t want = (size_t)64 << 20;
+        while (want < need) want <<= 1;
+        if (hipMalloc((void **)&d, want) != hipSuccess) return false;
+        cap = want;
         return true;
     }
 };
-// JFS_ZSTD_BPAR=0: one wave per frame (blocks in order) instead of one work
-// item per 128 KiB block
-bool zstd_bpar() {
-    static const bool v = [] {
-        const char *e = getenv("JFS_ZSTD_BPAR");
-        return !(e && atoi(e) == 0);
-    }();
-    return v;
-}
-ZEScratch g_zes[16];
+ZL1Scratch g_zl1[16];
+inline size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
 }  // namespace
 
-#ifdef JFS_PROF
-extern "C" int jfs_zeprof_read(unsigned long long *out) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(jfs::zstde::g_zeprof), sizeof(unsigned long long) * 12) == hipSuccess ? 0 : -1;
-}
-extern "C" int jfs_zeprof_reset() {
-    unsigned long long z[12] = {0};
-    return hipMemcpyToSymbol(HIP_SYMBOL(jfs::zstde::g_zeprof), z, sizeof(z)) == hipSuccess ? 0 : -1;
-}
-#endif
-
 extern "C" int jfs_launch_zstd_encode(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, hipStream_t stream) {
-    using namespace jfs::zstde;
     if (nblk <= 0) return 0;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return -1;
-    ZEScratch &z = g_zes[dev];
+    ZL1Scratch &z = g_zl1[dev];
     std::lock_guard<std::mutex> lk(z.mu);
-    if (!zstd_bpar()) {
-        if (z.cap < (size_t)nblk && !z.grow((size_t)nblk)) return -1;
-        hipLaunchKernelGGL(zstd_encode_kernel<false>, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, d_ret, z.d,
-                           (const int2 *)nullptr, 0, (int32_t *)nullptr);
-        if (hipGetLastError() != hipSuccess) return -1;
-        // the scratch is shared by every launch on this device: finish before it is reused
-        return hipStreamSynchronize(stream) == hipSuccess ? 0 : -1;
-    }
-    // block-parallel: one work item per 128 KiB block (the descriptors may
-    // have been written on this stream: read them after it drains)
+    // the descriptors may have been written on this stream: read them after it drains
     std::vector<jfs_dev_block> h(nblk);
     if (hipMemcpyAsync(h.data(), d_blocks, sizeof(jfs_dev_block) * nblk, hipMemcpyDeviceToHost, stream) != hipSuccess ||
         hipStreamSynchronize(stream) != hipSuccess)
         return -1;
-    std::vector<int2> work;
-    std::vector<int32_t> first(nblk + 1);
+    std::vector<FInfo> fi(nblk);
+    std::vector<BInfo> bi;
+    std::vector<int32_t> hret(nblk, -2);
+    int64_t seq_total = 0, byte_total = 0;
     for (int f = 0; f < nblk; f++) {
-        first[f] = (int32_t)work.size();
-        const int64_t n = h[f].src_len;
-        const int64_t nb = n <= 0 ? 1 : (n + BLK - 1) / BLK;
-        for (int64_t k = 0; k < nb; k++) work.push_back(make_int2(f, (int)k));
+        FInfo &F = fi[f];
+        const int64_t n = h[f].src_len, cap = h[f].dst_cap;
+        F.src = (const uint8_t *)h[f].src;
+        F.dst = (uint8_t *)h[f].dst;
+        F.n = (int32_t)std::max<int64_t>(0, std::min<int64_t>(n, 0x7FFFFFFF));
+        F.cap = (int32_t)std::max<int64_t>(0, std::min<int64_t>(cap, 0x7FFFFFFF));
+        const Params p = params_of(F.n);
+        F.wlog = p.wlog;
+        F.hlog = p.hlog;
+        F.mls = p.mls;
+        F.b0 = (int32_t)bi.size();
+        F.nb = 0;
+        // compress.go:86-89: cap(dst) < CompressBound -> "buffer too short"
+        F.status = (n < 0 || n > 0x7FFFFF00ll || cap < zbound(n)) ? -2 : 0;
+        if (F.status < 0) continue;
+        for (int64_t bs = 0; bs < n; bs += BLK) {
+            BInfo B;
+            memset(&B, 0, sizeof(B));
+            B.frame = f;
+            B.bs = (int32_t)bs;
+            B.be = (int32_t)std::min<int64_t>(n, bs + BLK);
+            const int32_t bsz = B.be - B.bs;
+            B.seq_off = seq_total;
+            B.lit_off = byte_total;
+            seq_total += seq_cap(bsz);
+            byte_total += (int64_t)a256((size_t)(2 * (int64_t)bsz + SEC_EXTRA));
+            bi.push_back(B);
+            F.nb++;
+        }
     }
-    first[nblk] = (int32_t)work.size();
-    const int nwork = (int)work.size();
-    if (z.waves == 0) {
-        int per_cu = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, zstd_encode_kernel<true>, 64, 0) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            return -1;
-        z.waves = std::max(1, per_cu) * std::max(1, cus);
-    }
-    const int grid = std::min(nwork, z.waves);
-    if (z.cap < (size_t)grid && !z.grow((size_t)grid)) return -1;
-    const size_t wb = sizeof(int2) * nwork, fb = sizeof(int32_t) * (nblk + 1), sb = sizeof(int32_t) * nwork;
-    if (z.aux_cap < wb + fb + sb) {
-        if (z.aux) (void)hipFree(z.aux);
-        z.aux = nullptr;
-        z.aux_cap = 0;
-        if (hipMalloc((void **)&z.aux, wb + fb + sb) != hipSuccess) return -1;
-        z.aux_cap = wb + fb + sb;
-    }
-    int2 *d_work = (int2 *)z.aux;
-    int32_t *d_first = (int32_t *)(z.aux + wb), *d_bsize = (int32_t *)(z.aux + wb + fb);
-    if (hipMemcpyAsync(d_work, work.data(), wb, hipMemcpyHostToDevice, stream) != hipSuccess ||
-        hipMemcpyAsync(d_first, first.data(), fb, hipMemcpyHostToDevice, stream) != hipSuccess)
+    const int nbk = (int)bi.size();
+    const size_t fb = a256(sizeof(FInfo) * nblk), bb = a256(sizeof(BInfo) * std::max(nbk, 1)),
+                 lb = a256(sizeof(int32_t) * (2 * (size_t)nblk + (size_t)nbk + 16)), sb = a256(sizeof(uint64_t) * (size_t)std::max<int64_t>(seq_total, 1)),
+                 yb = a256((size_t)std::max<int64_t>(byte_total, 1)), hb = a256(sizeof(uint32_t) * 1024 * (size_t)std::max(nbk, 1));
+    if (!z.grow(fb + bb + lb + sb + yb + hb)) return -1;
+    uint8_t *p = z.d;
+    FInfo *d_fi = (FInfo *)p;
+    p += fb;
+    BInfo *d_bi = (BInfo *)p;
+    p += bb;
+    int32_t *d_list = (int32_t *)p;
+    p += lb;
+    uint64_t *d_seq = (uint64_t *)p;
+    p += sb;
+    uint8_t *d_bytes = p;
+    p += yb;
+    uint32_t *d_hist = (uint32_t *)p;
+    if (hipMemcpyAsync(d_fi, fi.data(), sizeof(FInfo) * nblk, hipMemcpyHostToDevice, stream) != hipSuccess) return -1;
+    if (nbk > 0 && hipMemcpyAsync(d_bi, bi.data(), sizeof(BInfo) * nbk, hipMemcpyHostToDevice, stream) != hipSuccess)
         return -1;
-    hipLaunchKernelGGL(zstd_encode_kernel<true>, dim3(grid), dim3(64), 0, stream, d_blocks, nblk, d_ret, z.d,
-                       (const int2 *)d_work, nwork, d_bsize);
-    if (hipGetLastError() != hipSuccess) return -1;
-    hipLaunchKernelGGL(zstd_compact_kernel, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, d_ret,
-                       (const int32_t *)d_bsize, (const int32_t *)d_first);
-    if (hipGetLastError() != hipSuccess) return -1;
-    // the scratch and the host work list are shared / local: finish first
+    std::vector<int32_t> todo;
+    for (int f = 0; f < nblk; f++)
+        if (fi[f].status == 0) todo.push_back(f);
+    // frames that cannot be encoded report -2 now; the others are written by zl1_lit_kernel
+    for (int f = 0; f < nblk; f++)
+        if (fi[f].status < 0) hret[f] = -2;
+    if (hipMemcpyAsync(d_ret, hret.data(), sizeof(int32_t) * nblk, hipMemcpyHostToDevice, stream) != hipSuccess) return -1;
+    for (int pass = 0; pass <= nbk + 1 && !todo.empty(); pass++) {
+        // parse launches: one per (table width, hashLog) so each gets exactly its LDS
+        std::vector<int32_t> lists, blist;
+        struct Grp { bool wide; uint32_t hlog; int off, cnt; };
+        std::vector<Grp> grps;
+        for (int wide = 0; wide < 2; wide++)
+            for (uint32_t hl = 6; hl <= 15; hl++) {
+                Grp g{wide != 0, hl, (int)lists.size(), 0};
+                for (int f : todo) {
+                    const bool w = fi[f].n >= 65536;
+                    if (w == (wide != 0) && fi[f].hlog == hl && fi[f].nb > 0) {
+                        lists.push_back(f);
+                        g.cnt++;
+                    }
+                }
+                if (g.cnt) grps.push_back(g);
+            }
+        const int flist_off = (int)lists.size();
+        for (int f : todo) lists.push_back(f);
+        for (int f : todo)
+            for (int k = 0; k < fi[f].nb; k++) blist.push_back(fi[f].b0 + k);
+        const int blist_off = (int)lists.size();
+        lists.insert(lists.end(), blist.begin(), blist.end());
+        if ((size_t)lists.size() * sizeof(int32_t) > lb) {
+            // (cannot happen: a pass lists each frame twice at most and each block once)
+            return -1;
+        }
+        if (hipMemcpyAsync(d_list, lists.data(), sizeof(int32_t) * lists.size(), hipMemcpyHostToDevice, stream) !=
+            hipSuccess)
+            return -1;
+        for (const Grp &g : grps) {
+            const size_t tsz = (size_t)1 << g.hlog;
+            if (g.wide) {
+                hipLaunchKernelGGL(zl1_parse_kernel<true>, dim3(g.cnt), dim3(64), tsz * 2 + tsz / 2, stream, d_fi,
+                                   d_list + g.off, d_bi, d_seq);
+            } else {
+                hipLaunchKernelGGL(zl1_parse_kernel<false>, dim3(g.cnt), dim3(64), tsz * 2, stream, d_fi,
+                                   d_list + g.off, d_bi, d_seq);
+            }
+            if (hipGetLastError() != hipSuccess) return -1;
+        }
+        if (!blist.empty()) {
+            hipLaunchKernelGGL(zl1_seq_kernel, dim3((unsigned)blist.size()), dim3(64), 0, stream, d_fi,
+                               d_list + blist_off, d_bi, d_seq, d_bytes, d_hist);
+            if (hipGetLastError() != hipSuccess) return -1;
+        }
+        hipLaunchKernelGGL(zl1_lit_kernel, dim3((unsigned)todo.size()), dim3(64), 0, stream, d_fi, d_list + flist_off,
+                           d_bi, d_bytes, d_hist, d_ret);
+        if (hipGetLastError() != hipSuccess) return -1;
+        // frames whose confirmation guess was wrong go again
+        std::vector<FInfo> chk(nblk);
+        if (hipMemcpyAsync(chk.data(), d_fi, sizeof(FInfo) * nblk, hipMemcpyDeviceToHost, stream) != hipSuccess ||
+            hipStreamSynchronize(stream) != hipSuccess)
+            return -1;
+        std::vector<int32_t> again;
+        for (int f : todo)
+            if (chk[f].status == 1) again.push_back(f);
+        todo.swap(again);
+    }
+    if (!todo.empty()) return -1;
     return hipStreamSynchronize(stream) == hipSuccess ? 0 : -1;
 }

@@ -34,6 +34,10 @@ class Oracle:
         lib.oracle_envelope_write.restype = i64
         lib.oracle_envelope_parse.argtypes = [vp, i64, ctypes.POINTER(i64), ctypes.POINTER(i64)]
         lib.oracle_envelope_parse.restype = i64
+        if hasattr(lib, "oracle_zstd_compress_l1_ex"):
+            lib.oracle_zstd_compress_l1_ex.argtypes = [vp, i64, vp, i64, vp]
+            lib.oracle_zstd_compress_l1_ex.restype = i64
+            lib.oracle_zstd_l1_params.argtypes = [i64, vp]
         self.has_zstd = hasattr(lib, "oracle_zstd_decompress")
         if self.has_zstd:
             lib.oracle_zstd_decompress.argtypes = [vp, i64, vp, i64]
@@ -43,6 +47,15 @@ class Oracle:
             lib.oracle_zstd_frame_content_size.restype = i64
             lib.oracle_xxh64.argtypes = [vp, ctypes.c_size_t, ctypes.c_uint64]
             lib.oracle_xxh64.restype = ctypes.c_uint64
+
+    def zstd_compress_l1(self, src: bytes) -> bytes:
+        """libzstd 1.4.9 ZSTD_compress(level 1), restated (oracle/zstd_l1_oracle.c)."""
+        n = len(src)
+        cap = n + (n >> 8) + (((128 << 10) - n) >> 11 if n < (128 << 10) else 0) + 64
+        dst = ctypes.create_string_buffer(cap)
+        r = self.lib.oracle_zstd_compress_l1_ex(src, n, dst, cap, None)
+        assert r > 0
+        return dst.raw[:r]
 
     def lz4_bound(self, n: int) -> int:
         return self.lib.oracle_lz4_bound(n)

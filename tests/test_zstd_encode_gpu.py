@@ -1,14 +1,15 @@
-"""GPU Zstd encoder (SURVEY.md 8a row a8, compress.go:82-91).
+"""GPU Zstd encoder (SURVEY.md 8a row a8 / 8f row f2, compress.go:82-91).
 
-Byte parity with the encoder the reference pins (DataDog/zstd v1.5.6) is
-unpinnable offline, so the bar here is:
-  * the frames libzstd 1.4.9 writes for the known-answer inputs are
-    reproduced byte for byte where the encoder makes the same choices (raw
-    blocks for tiny inputs, one predefined-FSE sequence for "hello world"x8);
-  * every frame decodes back to the input through the CPU oracle
-    (oracle/zstd_oracle.c, pinned to libzstd fixtures) and through the GPU
-    decoder, and is never larger than CompressBound;
-  * the ZStandard.Compress contract (short destination -> error)."""
+The encoder restates libzstd's ZSTD_compress(.., level 1); the bar is byte
+identity with libzstd 1.4.9's level-1 frames (the library of this image; the
+reference pins DataDog/zstd v1.5.6, not available offline):
+  * the committed fixtures: KATs, every level-1 frame of
+    tests/golden/zstd_golden.json, the 4 MiB / tier-edge / mixed cases of
+    tests/golden/zstd_l1_golden.json (sha256 of libzstd's frames);
+  * the CPU oracle oracle/zstd_l1_oracle.c (itself pinned to those fixtures
+    and to libzstd) on seeded inputs of every class, misaligned buffers;
+  * every frame also decodes back through the oracle, libzstd and the GPU
+    decoder, and the ZStandard.Compress contract holds (short dst -> error)."""
 import os
 
 import numpy as np
@@ -67,8 +68,8 @@ def _libzstd():
 
 
 def test_zstd_encode_kats(gpu, golden):
-    """Tiny inputs: raw blocks, identical to libzstd 1.4.9 level 1; "hello
-    world"x8: one sequence with predefined FSE tables, also identical."""
+    """Tiny inputs: raw blocks; "hello world"x8: one sequence with predefined
+    FSE tables -- identical to libzstd 1.4.9 level 1."""
     kats = golden["zstd"]["kat"]
     srcs = [bytes.fromhex(k["src"]) for k in kats]
     r, frames = encode_device(srcs, gpu)
@@ -141,23 +142,65 @@ def test_zstandard_compress_contract(gpu):
 
 
 def test_zstd_encode_ratio_floor(gpu):
-    """Huffman literals + FSE sequences: the GPU frames of 4 MiB text blocks
-    reach a level-1-class ratio (floor guards regressions; libzstd level 1
-    reaches ~3.2 on this generator)."""
+    """4 MiB text blocks: level-1 ratio (libzstd 1.4.9 level 1: 3.17 on this
+    generator; the frames are libzstd's own, so the floor is its ratio)."""
     srcs = [gen_block("T", 900 + i, 4 << 20) for i in range(2)]
     r, frames = encode_device(srcs, gpu)
     ratio = sum(len(s) for s in srcs) / sum(r)
     print("zstd GPU ratio", ratio)
-    assert ratio >= 3.0, ratio
+    assert ratio >= 3.15, ratio
 
 
-def test_zstd_encode_many_frames_block_parallel(gpu, oracle):
-    """Block-parallel encoding (zstd_encode.hip BPAR): one work item per 128 KiB
-    block, blocks moved into place per frame.  Many frames of 1..33 blocks in
-    one launch, repeat-offset-heavy periodic data across block starts (the
-    first sequence of a block must not use a repeat code it cannot know),
-    sizes at block boundaries; every frame decodes through the oracle and the
-    GPU decoder."""
+def _sha(b):
+    import hashlib
+    return hashlib.sha256(b).hexdigest()
+
+
+def test_zstd_encode_golden_level1_frames(gpu, golden):
+    """Every level-1 frame of zstd_golden.json (libzstd 1.4.9, 1 B .. 1 MiB,
+    classes T/Z/R), encoded in one launch: byte-identical."""
+    fr = [f for f in golden["zstd"]["frames"] if f["level"] == 1]
+    srcs = [gen_block(f["cls"], f["seed"], f["size"]) for f in fr]
+    r, frames = encode_device(srcs, gpu, src_mis=1, dst_mis=2)
+    for f, x, c in zip(fr, r, frames):
+        assert x == f["csize"] and _sha(c) == f["comp_sha"], (f["cls"], f["size"], x, f["csize"])
+
+
+def test_zstd_encode_golden_l1_cases(gpu):
+    """zstd_l1_golden.json: 4 MiB text / zeros / random / mixed / skewed frames
+    (raw, RLE and compressed blocks in one frame, Huffman-table reuse across
+    blocks, repeat offsets across blocks), tier edges: byte-identical."""
+    import json
+    from tests.zstd_l1_cases import make_case
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "zstd_l1_golden.json")))
+    cs = g["cases"]
+    srcs = [make_case(c["kind"], c["seed"], c["size"]) for c in cs]
+    r, frames = encode_device(srcs, gpu, src_mis=3, dst_mis=5)
+    for c, x, f in zip(cs, r, frames):
+        assert x == c["csize"] and _sha(f) == c["comp_sha"], (c["kind"], c["size"], x, c["csize"])
+
+
+def test_zstd_encode_matches_oracle_seeded(gpu, oracle):
+    """Seeded inputs of every kind and size class (many frames per launch, every
+    (table width, hashLog) parse group): identical to the CPU oracle."""
+    import random
+    from tests.zstd_l1_cases import make_case
+    rng = random.Random(4242)
+    srcs = []
+    for i in range(60):
+        n = rng.choice([rng.randrange(0, 300), rng.randrange(0, 20000), rng.randrange(16000, 140000),
+                        rng.randrange(100000, 700000), rng.choice([65535, 65536, 131072, 262145, 1 << 20])])
+        srcs.append(make_case("TZRSM"[i % 5], 7000 + i, n))
+    r, frames = encode_device(srcs, gpu, src_mis=7, dst_mis=9)
+    for i, (s, x, f) in enumerate(zip(srcs, r, frames)):
+        want = oracle.zstd_compress_l1(s)
+        assert x == len(want) and f == want, (i, "TZRSM"[i % 5], len(s), x, len(want))
+
+
+def test_zstd_encode_many_frames_roundtrip(gpu, oracle):
+    """Many frames of 1..33 blocks in one launch, repeat-offset-heavy periodic
+    data across block starts, sizes at block boundaries: identical to the
+    oracle, and every frame decodes through the oracle and the GPU decoder."""
     rng = np.random.default_rng(17)
     srcs = []
     for i in range(40):
@@ -173,6 +216,7 @@ def test_zstd_encode_many_frames_block_parallel(gpu, oracle):
     r, frames = encode_device(srcs, gpu, dst_mis=5)
     for s, x, f in zip(srcs, r, frames):
         assert 0 < x <= _bound(len(s)), (len(s), x)
+        assert f == oracle.zstd_compress_l1(s), len(s)
         n, out = oracle.zstd_decompress(f, len(s))
         assert n == len(s) and out == s, (len(s), n)
     from tests.test_zstd_gpu import run_device
