@@ -103,6 +103,20 @@ int64_t jfs_compress_batch(int algo, int nblk, const jfs_iov *iov, int64_t *out_
 int64_t jfs_compress_batch_crc(int algo, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t *crc,
                                uint32_t device_mask);
 int64_t jfs_decompress_batch(int algo, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t device_mask);
+/* jfs_decompress_batch plus, for each block with csum[i] != NULL, the disk-cache
+ * checksum of the decoded block -- what cacheStore.add writes beside it
+ * (pkg/chunk/disk_cache.go:536-537, checksum() of disk_cache_file.go:139-152):
+ * the big-endian CRC-32C of every 32 KiB piece, ((n-1)/32768+1)*4 bytes for
+ * n = out_n[i] decoded bytes (4 zero bytes for n = 0), computed on the GPU
+ * before the block leaves HBM.  csum[i] must hold ((dst_cap-1)/32768+1)*4
+ * bytes; nothing is written for a block that fails. */
+int64_t jfs_decompress_batch_csum(int algo, int nblk, const jfs_iov *iov, int64_t *out_n, uint8_t *const *csum,
+                                  uint32_t device_mask);
+/* The batch calls' device dealing policy, exposed for
+ * schedulers and tests: out_dev[i] in [0, ndev) for blocks of cost[i] (the
+ * library uses src_len + dst_cap + 4096): longest-first greedy onto the least
+ * loaded device, so no device ends more than one block above another. */
+void jfs_deal_plan(const int64_t *cost, int n, int ndev, int32_t *out_dev);
 
 /* ---- Encrypted objects (host buffers): compress + seal, open + decompress --
  * The PUT path of an encrypted volume is Compress (cached_store.go:372) and

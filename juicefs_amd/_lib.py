@@ -36,7 +36,7 @@ EXPORTS = [
     "jfs_gpu_mode", "jfs_stats", "jfs_stats_reset", "jfs_device_stats", "jfs_lz4_decompress_device_small",
     "jfs_lz4_split_counts", "jfs_lz4_compress_device_small", "jfs_lz4_eseg_counts", "jfs_cipher_from_name", "jfs_cipher_key_size", "jfs_aead_seal_device",
     "jfs_aead_open_device", "jfs_envelope_bound", "jfs_envelope_parse", "jfs_compress_seal_batch",
-    "jfs_open_decompress_batch", "jfs_compress_batch_crc",
+    "jfs_open_decompress_batch", "jfs_compress_batch_crc", "jfs_decompress_batch_csum", "jfs_deal_plan",
 ]
 
 MODE_OFF, MODE_AUTO, MODE_FORCE = 0, 1, 2
@@ -121,6 +121,11 @@ def load() -> ctypes.CDLL:
     lib.jfs_compress_batch_crc.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(JfsIov), ctypes.POINTER(i64),
                                            vp, u32]
     lib.jfs_compress_batch_crc.restype = i64
+    lib.jfs_decompress_batch_csum.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(JfsIov), ctypes.POINTER(i64),
+                                              ctypes.POINTER(ctypes.c_void_p), u32]
+    lib.jfs_decompress_batch_csum.restype = i64
+    lib.jfs_deal_plan.argtypes = [ctypes.POINTER(i64), ctypes.c_int, ctypes.c_int, ctypes.POINTER(i32)]
+    lib.jfs_deal_plan.restype = None
     lib.jfs_compress_seal_batch.restype = i64
     lib.jfs_open_decompress_batch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(JfsIov),
                                               ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(i64), u32]

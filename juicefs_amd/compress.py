@@ -108,6 +108,12 @@ class Compressor:
     def DecompressBatch(self, pairs, device_mask: int = 0):
         return _batch(self.algo, pairs, device_mask, compress=False)
 
+    def DecompressBatchChecksum(self, pairs, device_mask: int = 0):
+        """DecompressBatch plus each decoded block's disk-cache checksum
+        (checksum() of pkg/chunk/disk_cache_file.go:139-152, written beside the
+        block by disk_cache.go:536-537), computed on the GPU: [(n, err, csum)]"""
+        return _batch(self.algo, pairs, device_mask, compress=False, with_csum=True)
+
     def CompressBatchChecksum(self, pairs, device_mask: int = 0):
         """CompressBatch plus each payload's CRC-32C (generateChecksum,
         pkg/object/checksum.go:30-45): [(n, err, crc)]"""
@@ -145,7 +151,15 @@ def NewCompressor(algr: str):
     return None
 
 
-def _batch(algo: int, pairs, device_mask: int, compress: bool, with_crc: bool = False):
+CSUM_BLOCK = 32 << 10  # disk_cache_file.go csBlock
+
+
+def csum_bytes(n: int) -> int:
+    """Length of checksum() for n data bytes: ((n-1)/32768+1)*4 (Go integer division)."""
+    return (int((n - 1) / CSUM_BLOCK) + 1) * 4
+
+
+def _batch(algo: int, pairs, device_mask: int, compress: bool, with_crc: bool = False, with_csum: bool = False):
     """pairs: list of (dst, src).  Returns list of (n, err)."""
     lib = L.load()
     nb = len(pairs)
@@ -158,8 +172,14 @@ def _batch(algo: int, pairs, device_mask: int, compress: bool, with_crc: bool = 
         iov[i].src, iov[i].src_len, iov[i].dst, iov[i].dst_cap = s, sn, d, dn
     out = (ctypes.c_int64 * max(nb, 1))()
     crc = (ctypes.c_uint32 * max(nb, 1))()
+    cs_bufs = []
+    if with_csum:
+        cs_bufs = [ctypes.create_string_buffer(csum_bytes(max(iov[i].dst_cap, 0))) for i in range(nb)]
+        cs_ptrs = (ctypes.c_void_p * max(nb, 1))(*[ctypes.cast(b, ctypes.c_void_p) for b in cs_bufs])
     if with_crc:
         rc = lib.jfs_compress_batch_crc(algo, nb, iov, out, crc, device_mask)
+    elif with_csum:
+        rc = lib.jfs_decompress_batch_csum(algo, nb, iov, out, cs_ptrs, device_mask)
     else:
         fn = lib.jfs_compress_batch if compress else lib.jfs_decompress_batch
         rc = fn(algo, nb, iov, out, device_mask)
@@ -175,4 +195,6 @@ def _batch(algo: int, pairs, device_mask: int, compress: bool, with_crc: bool = 
             res.append((r, None))
     if with_crc:
         return [(n, e, int(crc[i])) for i, (n, e) in enumerate(res)]
+    if with_csum:
+        return [(n, e, cs_bufs[i].raw[:csum_bytes(n)] if e is None else None) for i, (n, e) in enumerate(res)]
     return res

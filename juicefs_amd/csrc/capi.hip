@@ -46,6 +46,8 @@ inline int64_t align16(int64_t x) { return (x + 15) & ~(int64_t)15; }
 // k % NSLOT, so chunk k+1's H2D and chunk k-1's D2H run while chunk k's
 // kernel runs.
 constexpr int NSLOT = 3;
+// disk-cache checksum piece (pkg/chunk/disk_cache_file.go:139-152: csBlock)
+constexpr int64_t CSUM_SEG = 32 << 10;
 
 // Upper bound on one slot's staging (JFS_STAGING_MAX_MB; default none): a
 // request that needs more fails alone with JFS_ERR_NO_MEMORY.
@@ -645,7 +647,7 @@ struct Aead {
 // (the coalescer releases their callers there, before later chunks finish).
 int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_iov *iov, int64_t *out,
                   const Aead *ae = nullptr, uint32_t *crc_out = nullptr, int max_chunk_blocks = 0,
-                  const std::function<void(int, int)> *on_chunk = nullptr) {
+                  const std::function<void(int, int)> *on_chunk = nullptr, uint8_t *const *csum_out = nullptr) {
     if (nblk <= 0) return JFS_OK;
     DevGuard guard;
     (void)hipSetDevice(dev->id);
@@ -732,10 +734,68 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
         p += align16(nb * 4);
         *crc = (uint32_t *)p;
     };
+    // decode-side disk-cache checksums (csum_out): descriptors, then every
+    // block's ((cap-1)/32 KiB+1)*4 checksum bytes (after the crc area)
+    const bool want_csum = csum_out && dir == DECOMPRESS && !ae;
+    auto csum_words = [&](int i) { return cap[i] > 0 ? (cap[i] - 1) / CSUM_SEG + 1 : 1; };
+    auto crc_bytes = [&](int64_t nb) {
+        return crc_out ? align16(nb * (int64_t)sizeof(jfs_dev_block)) + 2 * align16(nb * 4) : 0;
+    };
+    auto csum_layout = [&](const Chunk &c, uint8_t *base, jfs_dev_block **cd, uint8_t **area) {
+        const int64_t nb = c.e - c.s;
+        uint8_t *p = base + c.tin + c.tout + align16(nb * (int64_t)sizeof(jfs_dev_block)) + align16(nb * 4) +
+                     align16(nb * zib) + aead_bytes(nb) + crc_bytes(nb);
+        *cd = (jfs_dev_block *)p;
+        *area = p + align16(nb * (int64_t)sizeof(jfs_dev_block));
+    };
+    auto csum_area_bytes = [&](const Chunk &c) {
+        int64_t t = 0;
+        for (int i = c.s; i < c.e; i++) t += align16(4 * csum_words(i));
+        return t;
+    };
     auto chunk_bytes = [&](const Chunk &c) {
         const int64_t nb = c.e - c.s;
         return c.tin + c.tout + align16(nb * (int64_t)sizeof(jfs_dev_block)) + align16(nb * 4) + align16(nb * zib) +
-               aead_bytes(nb) + (crc_out ? align16(nb * (int64_t)sizeof(jfs_dev_block)) + 2 * align16(nb * 4) : 0);
+               aead_bytes(nb) + crc_bytes(nb) +
+               (want_csum ? align16(nb * (int64_t)sizeof(jfs_dev_block)) + csum_area_bytes(c) : 0);
+    };
+    // stage the checksum descriptors: the decoded output is the data, the
+    // checksum bytes go to the chunk's checksum area
+    auto stage_csum = [&](const Chunk &c, Slot &sl, uint8_t *d_out) -> int64_t {
+        if (!want_csum) return JFS_OK;
+        const int n = c.e - c.s;
+        jfs_dev_block *h_cd, *d_cd;
+        uint8_t *h_area, *d_area;
+        csum_layout(c, sl.h, &h_cd, &h_area);
+        csum_layout(c, sl.d, &d_cd, &d_area);
+        int64_t o = 0;
+        for (int k = 0; k < n; k++) {
+            const int i = c.s + k;
+            h_cd[k] = jfs_dev_block{d_out + out_off[i], d_area + o, 0, (int32_t)(4 * csum_words(i))};
+            o += align16(4 * csum_words(i));
+        }
+        return hipMemcpyAsync(d_cd, h_cd, (size_t)n * sizeof(jfs_dev_block), hipMemcpyHostToDevice, dev->s_in) ==
+                       hipSuccess
+                   ? JFS_OK
+                   : JFS_ERR_HIP;
+    };
+    auto run_csum = [&](const Chunk &c, Slot &sl, const int32_t *d_lens) -> int64_t {
+        if (!want_csum) return JFS_OK;
+        jfs_dev_block *d_cd;
+        uint8_t *d_area;
+        csum_layout(c, sl.d, &d_cd, &d_area);
+        return jfs_launch_crc32c_segs_lens(d_cd, c.e - c.s, CSUM_SEG, d_lens, c.ks) == 0 ? JFS_OK : JFS_ERR_HIP;
+    };
+    auto fetch_csum = [&](const Chunk &c, Slot &sl) -> int64_t {
+        if (!want_csum) return JFS_OK;
+        jfs_dev_block *h_cd, *d_cd;
+        uint8_t *h_area, *d_area;
+        csum_layout(c, sl.h, &h_cd, &h_area);
+        csum_layout(c, sl.d, &d_cd, &d_area);
+        return hipMemcpyAsync(h_area, d_area, (size_t)csum_area_bytes(c), hipMemcpyDeviceToHost, dev->s_out) ==
+                       hipSuccess
+                   ? JFS_OK
+                   : JFS_ERR_HIP;
     };
     // stage the checksum descriptors (payload = the codec's output area) and
     // queue their H2D on s_in; seeds: the envelope header's CRC for a seal
@@ -929,6 +989,7 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
         if (zplan && hipMemcpyAsync(d_zi, h_zi, (size_t)(n * zib), hipMemcpyHostToDevice, dev->s_in) != hipSuccess)
             return JFS_ERR_HIP;
         if (dir == COMPRESS && stage_crc(c, sl, d_out) != JFS_OK) return JFS_ERR_HIP;
+        if (stage_csum(c, sl, d_out) != JFS_OK) return JFS_ERR_HIP;
         if (hipEventRecord(sl.ev_in, dev->s_in) != hipSuccess) return JFS_ERR_HIP;
         if (hipStreamWaitEvent(c.ks, sl.ev_in, 0) != hipSuccess) return JFS_ERR_HIP;
         int lk;
@@ -955,11 +1016,13 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
         }
         if (lk != 0) return JFS_ERR_HIP;
         if (dir == COMPRESS && run_crc(c, sl, d_ret) != JFS_OK) return JFS_ERR_HIP;
+        if (run_csum(c, sl, d_ret) != JFS_OK) return JFS_ERR_HIP;
         if (hipEventRecord(sl.ev_k, c.ks) != hipSuccess) return JFS_ERR_HIP;
         if (hipStreamWaitEvent(dev->s_out, sl.ev_k, 0) != hipSuccess) return JFS_ERR_HIP;
         if (hipMemcpyAsync(h_ret, d_ret, (size_t)n * 4, hipMemcpyDeviceToHost, dev->s_out) != hipSuccess)
             return JFS_ERR_HIP;
         if (dir == COMPRESS && fetch_crc(c, sl) != JFS_OK) return JFS_ERR_HIP;
+        if (fetch_csum(c, sl) != JFS_OK) return JFS_ERR_HIP;
         if (hipMemcpyAsync(h_out, d_out, (size_t)c.tout, hipMemcpyDeviceToHost, dev->s_out) != hipSuccess)
             return JFS_ERR_HIP;
         if (hipEventRecord(sl.ev, dev->s_out) != hipSuccess) return JFS_ERR_HIP;
@@ -1025,6 +1088,19 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
             crc_layout(c, sl.h, &h_cd, &h_seed, &h_crc);
             for (int i = c.s; i < c.e; i++) crc_out[i] = out[i] >= 0 ? h_crc[i - c.s] : 0u;
         }
+        if (want_csum) {
+            jfs_dev_block *h_cd;
+            uint8_t *h_area;
+            csum_layout(c, sl.h, &h_cd, &h_area);
+            int64_t o = 0;
+            for (int i = c.s; i < c.e; i++) {
+                if (csum_out[i] && out[i] >= 0) {
+                    const int64_t nw = out[i] > 0 ? (out[i] - 1) / CSUM_SEG + 1 : 1;
+                    jobs.push_back({csum_out[i], h_area + o, 4 * nw});
+                }
+                o += align16(4 * csum_words(i));
+            }
+        }
         par_copy(jobs);
         if (host_trace())
             fprintf(stderr, "[jfs host] t=%.2f chunk %d-%d wait %.2f ms copy-out %.1f MiB %.2f ms\n", now_ms(), c.s, c.e, t1 - t0,
@@ -1069,21 +1145,23 @@ bool lane_healthy(DevCtx *dev, Lane &ln) {
 }
 
 void run_isolated(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_iov *iov, int64_t *out,
-                  const Aead *ae = nullptr, uint32_t *crc = nullptr) {
+                  const Aead *ae = nullptr, uint32_t *crc = nullptr, uint8_t *const *csum = nullptr) {
     if (nblk <= 0) return;
-    const int64_t rc = run_batch(dev, ln, algo, dir, nblk, iov, out, ae, crc);
+    const int64_t rc = run_batch(dev, ln, algo, dir, nblk, iov, out, ae, crc, 0, nullptr, csum);
     if (rc == JFS_OK) return;
     if (nblk == 1 || (rc == JFS_ERR_HIP && !lane_healthy(dev, ln))) {
         for (int i = 0; i < nblk; i++) out[i] = rc;
         return;
     }
     const int h = nblk / 2;
-    run_isolated(dev, ln, algo, dir, h, iov, out, ae, crc);
+    run_isolated(dev, ln, algo, dir, h, iov, out, ae, crc, csum);
     if (ae) {
         const Aead a2 = ae->at(h);
-        run_isolated(dev, ln, algo, dir, nblk - h, iov + h, out + h, &a2, crc ? crc + h : nullptr);
+        run_isolated(dev, ln, algo, dir, nblk - h, iov + h, out + h, &a2, crc ? crc + h : nullptr,
+                     csum ? csum + h : nullptr);
     } else {
-        run_isolated(dev, ln, algo, dir, nblk - h, iov + h, out + h, nullptr, crc ? crc + h : nullptr);
+        run_isolated(dev, ln, algo, dir, nblk - h, iov + h, out + h, nullptr, crc ? crc + h : nullptr,
+                     csum ? csum + h : nullptr);
     }
 }
 
@@ -1131,6 +1209,42 @@ Gather gather_window(int dir) {
     });
     const int64_t gap = g[dir == DECOMPRESS_DIR ? DECOMPRESS_DIR : COMPRESS_DIR];
     return {gap, gap * 16};
+}
+
+// Work of one block for the dealer: the bytes it stages in and out.
+int64_t block_cost(const jfs_iov &v) { return std::max<int64_t>(v.src_len, 0) + std::max<int64_t>(v.dst_cap, 0) + 4096; }
+
+// Size-balanced deal (SURVEY.md 8e, config 4's mixed 64 KiB - 4 MiB blocks):
+// longest-processing-time greedy -- blocks by decreasing cost (ties in block
+// order), each to the device with the least cost so far (ties to the lowest
+// device).  No device ends more than one block's cost above another.
+void plan_deal(const int64_t *cost, int n, int ndev, int32_t *out_dev) {
+    if (n <= 0) return;
+    if (ndev <= 1) {
+        for (int i = 0; i < n; i++) out_dev[i] = 0;
+        return;
+    }
+    std::vector<int> ord(n);
+    for (int i = 0; i < n; i++) ord[i] = i;
+    std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return cost[a] > cost[b]; });
+    std::vector<int64_t> load(ndev, 0);
+    for (int i : ord) {
+        int best = 0;
+        for (int d = 1; d < ndev; d++)
+            if (load[d] < load[best]) best = d;
+        out_dev[i] = best;
+        load[best] += std::max<int64_t>(cost[i], 0);
+    }
+}
+
+// A gathered burst is spread over other devices' idle lanes when it holds at
+// least this many staged bytes (JFS_SPREAD_MIN_MB; default 8 MiB: two 4 MiB blocks).
+int64_t spread_min_bytes() {
+    static const int64_t v = [] {
+        const char *e = getenv("JFS_SPREAD_MIN_MB");
+        return e ? std::max(0ll, atoll(e)) << 20 : (int64_t)8 << 20;
+    }();
+    return v;
 }
 
 class Coalescer {
@@ -1218,37 +1332,83 @@ class Coalescer {
             for (size_t i = 0; i < batch.size(); i++) iov[i] = batch[i]->iov;
             {
                 const double t0 = host_trace() ? now_ms() : 0.0;
-                std::lock_guard<std::mutex> llk(ln.mu);
                 const int algo = batch[0]->algo, dir = batch[0]->dir, n = (int)batch.size();
-                // chunks of a decode batch release their callers as they finish:
-                // those callers' next calls gather while the rest of the batch runs
-                const std::function<void(int, int)> release = [&](int s, int e) {
-                    {
-                        std::lock_guard<std::mutex> lk(mu_);
-                        for (int i = s; i < e; i++) {
-                            batch[i]->res = out[i];
-                            batch[i]->done = true;
-                            released[i] = 1;
+                // Other devices with an idle lane take a size-balanced share of
+                // the gathered burst: their lanes are locked here
+                // and released after their parts finish.
+                std::vector<DevCtx *> hdev;
+                std::vector<Lane *> hlane;
+                std::vector<std::unique_lock<std::mutex>> hlock;
+                std::vector<int64_t> cost(n);
+                int64_t tot = 0;
+                for (int i = 0; i < n; i++) tot += (cost[i] = block_cost(iov[i]));
+                if (n >= 2 && tot >= spread_min_bytes()) {
+                    for (DevCtx *d : devices()) {
+                        if (d == dev || (int)hdev.size() + 1 >= n) continue;
+                        for (int k = 0; k < NLANE; k++) {
+                            std::unique_lock<std::mutex> t(d->lane[k].mu, std::try_to_lock);
+                            if (t.owns_lock()) {
+                                hdev.push_back(d);
+                                hlane.push_back(&d->lane[k]);
+                                hlock.push_back(std::move(t));
+                                break;
+                            }
                         }
                     }
-                    cv_done_.notify_all();
-                };
-                const int cb = dir == DECOMPRESS ? coalesce_chunk_blocks() : 0;
-                if (run_batch(dev, ln, algo, dir, n, iov.data(), out.data(), nullptr, nullptr, cb, &release) != JFS_OK) {
-                    // what was not released yet goes through the error-isolating path
-                    std::vector<int> idx;
-                    for (int i = 0; i < n; i++)
-                        if (!released[i]) idx.push_back(i);
-                    std::vector<jfs_iov> iv2(idx.size());
-                    std::vector<int64_t> o2(idx.size(), 0);
-                    for (size_t k = 0; k < idx.size(); k++) iv2[k] = iov[idx[k]];
-                    run_isolated(dev, ln, algo, dir, (int)idx.size(), iv2.data(), o2.data());
-                    for (size_t k = 0; k < idx.size(); k++) out[idx[k]] = o2[k];
                 }
+                const int G = 1 + (int)hdev.size();
+                std::vector<int32_t> where(n, 0);
+                plan_deal(cost.data(), n, G, where.data());
+                std::vector<std::vector<int>> pidx(G);
+                for (int i = 0; i < n; i++) pidx[where[i]].push_back(i);
+                // chunks of a decode batch release their callers as they finish:
+                // those callers' next calls gather while the rest of the batch runs
+                const int cb = dir == DECOMPRESS ? coalesce_chunk_blocks() : 0;
+                auto run_part = [&](DevCtx *d, Lane &L, const std::vector<int> &idx) {
+                    const int np = (int)idx.size();
+                    if (np == 0) return;
+                    std::vector<jfs_iov> piov(np);
+                    std::vector<int64_t> pout(np, 0);
+                    std::vector<char> prel(np, 0);
+                    for (int k = 0; k < np; k++) piov[k] = iov[idx[k]];
+                    const std::function<void(int, int)> release = [&](int s, int e) {
+                        {
+                            std::lock_guard<std::mutex> lk(mu_);
+                            for (int k = s; k < e; k++) {
+                                batch[idx[k]]->res = pout[k];
+                                batch[idx[k]]->done = true;
+                                released[idx[k]] = 1;
+                                prel[k] = 1;
+                            }
+                        }
+                        cv_done_.notify_all();
+                    };
+                    if (run_batch(d, L, algo, dir, np, piov.data(), pout.data(), nullptr, nullptr, cb, &release) !=
+                        JFS_OK) {
+                        // what was not released yet goes through the error-isolating path
+                        std::vector<int> rest;
+                        for (int k = 0; k < np; k++)
+                            if (!prel[k]) rest.push_back(k);
+                        std::vector<jfs_iov> iv2(rest.size());
+                        std::vector<int64_t> o2(rest.size(), 0);
+                        for (size_t q = 0; q < rest.size(); q++) iv2[q] = piov[rest[q]];
+                        run_isolated(d, L, algo, dir, (int)rest.size(), iv2.data(), o2.data());
+                        for (size_t q = 0; q < rest.size(); q++) pout[rest[q]] = o2[q];
+                    }
+                    for (int k = 0; k < np; k++) out[idx[k]] = pout[k];
+                };
+                std::vector<std::thread> th;
+                for (int g = 1; g < G; g++) th.emplace_back([&, g] { run_part(hdev[g - 1], *hlane[g - 1], pidx[g]); });
+                {
+                    std::lock_guard<std::mutex> llk(ln.mu);
+                    run_part(dev, ln, pidx[0]);
+                }
+                for (auto &t : th) t.join();
+                hlock.clear();
                 if (host_trace())
-                    fprintf(stderr, "[jfs coalescer] t=%.2f dev %d lane %d algo %d dir %d: %zu calls, gathered %.2f ms, ran %.2f ms\n",
-                            now_ms(), dev->id, (int)(&ln - dev->lane), batch[0]->algo, batch[0]->dir, batch.size(),
-                            t0 - t_gather, now_ms() - t0);
+                    fprintf(stderr, "[jfs coalescer] t=%.2f dev %d lane %d algo %d dir %d: %zu calls on %d device(s), gathered %.2f ms, ran %.2f ms\n",
+                            now_ms(), dev->id, (int)(&ln - dev->lane), algo, dir, batch.size(), G, t0 - t_gather,
+                            now_ms() - t0);
             }
             {
                 std::lock_guard<std::mutex> lk(mu_);
@@ -1281,10 +1441,10 @@ bool pre_answer(int algo, int dir, const jfs_iov &v, int64_t *res) {
     return false;
 }
 
-// Deal the todo blocks round-robin over the selected devices
-// and run them; ae_all (optional) is parallel to iov2.
+// Deal the todo blocks over the selected devices, size-balanced
+// (plan_deal) and run them; ae_all (optional) is parallel to iov2.
 int64_t deal(int algo, int dir, const std::vector<int> &todo, const std::vector<jfs_iov> &iov2, int64_t *out_n,
-             uint32_t mask, const Aead *ae_all, uint32_t *crc = nullptr) {
+             uint32_t mask, const Aead *ae_all, uint32_t *crc = nullptr, uint8_t *const *csum = nullptr) {
     std::vector<DevCtx *> &all = devices();
     std::vector<DevCtx *> ds;
     for (DevCtx *d : all)
@@ -1297,13 +1457,19 @@ int64_t deal(int algo, int dir, const std::vector<int> &todo, const std::vector<
         std::vector<jfs_seal_param> sp;
         std::vector<int64_t> hdr, res;
         std::vector<uint32_t> crc;
+        std::vector<uint8_t *> csum;
         std::vector<int> idx;
     };
     std::vector<Part> part(G);
+    std::vector<int64_t> cost(todo.size());
+    for (size_t k = 0; k < todo.size(); k++) cost[k] = block_cost(iov2[k]);
+    std::vector<int32_t> where(todo.size(), 0);
+    plan_deal(cost.data(), (int)todo.size(), (int)G, where.data());
     for (size_t k = 0; k < todo.size(); k++) {
-        Part &p = part[k % G];
+        Part &p = part[where[k]];
         p.iov.push_back(iov2[k]);
         p.idx.push_back(todo[k]);
+        if (csum) p.csum.push_back(csum[todo[k]]);
         if (ae_all) {
             p.orig.push_back(ae_all->orig[k]);
             p.key.push_back(ae_all->key[k]);
@@ -1324,7 +1490,8 @@ int64_t deal(int algo, int dir, const std::vector<int> &todo, const std::vector<
                    ae_all->sp ? p.sp.data() : nullptr, ae_all->hdr ? p.hdr.data() : nullptr};
             run_isolated(ds[g], ln, algo, dir, (int)p.iov.size(), p.iov.data(), p.res.data(), &a, pc);
         } else {
-            run_isolated(ds[g], ln, algo, dir, (int)p.iov.size(), p.iov.data(), p.res.data(), nullptr, pc);
+            run_isolated(ds[g], ln, algo, dir, (int)p.iov.size(), p.iov.data(), p.res.data(), nullptr, pc,
+                         csum ? p.csum.data() : nullptr);
         }
     };
     if (G == 1) work(0);
@@ -1352,19 +1519,37 @@ int64_t envelope_parse(const uint8_t *src, int64_t n, int64_t *woff, int64_t *wl
     return 3 + kl + nl;
 }
 
+// disk_cache_file.go checksum() of n bytes on the host (blocks answered
+// without the GPU: the "none" codec)
+void host_csum(const uint8_t *p, int64_t n, uint8_t *out) {
+    const int64_t nw = n > 0 ? (n - 1) / CSUM_SEG + 1 : 1;
+    for (int64_t w = 0; w < nw; w++) {
+        const int64_t a = w * CSUM_SEG, e = std::min<int64_t>(n, a + CSUM_SEG);
+        const uint32_t v = n > 0 ? host_crc32c(0, p + a, e - a) : 0u;
+        out[4 * w] = (uint8_t)(v >> 24);
+        out[4 * w + 1] = (uint8_t)(v >> 16);
+        out[4 * w + 2] = (uint8_t)(v >> 8);
+        out[4 * w + 3] = (uint8_t)v;
+    }
+}
+
 int64_t batch_common(int algo, int dir, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t mask,
-                     uint32_t *crc = nullptr) {
+                     uint32_t *crc = nullptr, uint8_t *const *csum = nullptr) {
     if (nblk < 0 || (nblk > 0 && (!iov || !out_n))) return JFS_ERR_INVALID;
     if (algo != JFS_ALGO_NONE && algo != JFS_ALGO_LZ4 && algo != JFS_ALGO_ZSTD) return JFS_ERR_INVALID;
     std::vector<int> todo;
     for (int i = 0; i < nblk; i++) {
-        if (!pre_answer(algo, dir, iov[i], &out_n[i])) todo.push_back(i);
-        else if (crc) crc[i] = out_n[i] >= 0 ? host_crc32c(0, iov[i].dst, out_n[i]) : 0u;  // "none": the payload is dst
+        if (!pre_answer(algo, dir, iov[i], &out_n[i])) {
+            todo.push_back(i);
+        } else {
+            if (crc) crc[i] = out_n[i] >= 0 ? host_crc32c(0, iov[i].dst, out_n[i]) : 0u;  // "none": the payload is dst
+            if (csum && csum[i] && out_n[i] >= 0) host_csum(iov[i].dst, out_n[i], csum[i]);
+        }
     }
     if (todo.empty()) return JFS_OK;
     std::vector<jfs_iov> iov2(todo.size());
     for (size_t k = 0; k < todo.size(); k++) iov2[k] = iov[todo[k]];
-    return deal(algo, dir, todo, iov2, out_n, mask, nullptr, crc);
+    return deal(algo, dir, todo, iov2, out_n, mask, nullptr, crc, csum);
 }
 
 }  // namespace
@@ -1429,9 +1614,9 @@ int64_t jfs_decompress(int algo, uint8_t *dst, int64_t dst_cap, const uint8_t *s
 }
 
 static int64_t batch_call(int algo, int dir, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t device_mask,
-                          uint32_t *crc = nullptr) {
+                          uint32_t *crc = nullptr, uint8_t *const *csum = nullptr) {
     const int64_t t0 = steady_ns();
-    const int64_t r = batch_common(algo, dir, nblk, iov, out_n, device_mask, crc);
+    const int64_t r = batch_common(algo, dir, nblk, iov, out_n, device_mask, crc, csum);
     if (OpStats *st = op_stats(algo, dir)) {
         st->calls.fetch_add(1, std::memory_order_relaxed);
         if (r == JFS_OK)
@@ -1583,6 +1768,17 @@ int64_t jfs_compress_batch_crc(int algo, int nblk, const jfs_iov *iov, int64_t *
 
 int64_t jfs_decompress_batch(int algo, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t device_mask) {
     return batch_call(algo, DECOMPRESS, nblk, iov, out_n, device_mask);
+}
+
+int64_t jfs_decompress_batch_csum(int algo, int nblk, const jfs_iov *iov, int64_t *out_n, uint8_t *const *csum,
+                                  uint32_t device_mask) {
+    if (nblk > 0 && !csum) return JFS_ERR_INVALID;
+    return batch_call(algo, DECOMPRESS, nblk, iov, out_n, device_mask, nullptr, csum);
+}
+
+void jfs_deal_plan(const int64_t *cost, int n, int ndev, int32_t *out_dev) {
+    if (!cost || !out_dev || n <= 0) return;
+    plan_deal(cost, n, ndev, out_dev);
 }
 
 // The device-resident entry points launch on the caller's current device; it

@@ -149,7 +149,7 @@ __global__ __launch_bounds__(LANES) void crc32c_kernel(const jfs_dev_block *__re
     g_u8 *out = (g_u8 *)blk.dst;
     const int64_t n = lens ? (int64_t)lens[b] : (int64_t)blk.src_len;
     const uint32_t seed = seeds ? seeds[b] : 0u;
-    if (lens && n <= 0) {
+    if (lens && (emit_segments ? n < 0 : n <= 0)) {  // the producing kernel failed (or, for a payload, wrote nothing)
         if (t == 0 && crc_out) crc_out[b] = 0;
         return;
     }
@@ -244,5 +244,15 @@ extern "C" int jfs_launch_crc32c_lens(const jfs_dev_block *d_blocks, int nblk, c
     if (nblk <= 0) return 0;
     hipLaunchKernelGGL(crc32c_kernel, dim3(nblk), dim3(LANES), 0, stream, d_blocks, nblk, (32 << 10) / ROW, 0, d_crc,
                        (int32_t *)nullptr, d_lens, d_seeds);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int jfs_launch_crc32c_segs_lens(const jfs_dev_block *d_blocks, int nblk, int32_t seg_bytes,
+                                           const int32_t *d_lens, hipStream_t stream) {
+    using namespace jfs::crc;
+    if (nblk <= 0) return 0;
+    if (seg_bytes <= 0 || seg_bytes % ROW != 0 || seg_bytes > (64 << 20)) return -1;
+    hipLaunchKernelGGL(crc32c_kernel, dim3(nblk), dim3(LANES), 0, stream, d_blocks, nblk, seg_bytes / ROW, 1,
+                       (uint32_t *)nullptr, (int32_t *)nullptr, d_lens, (const uint32_t *)nullptr);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -42,6 +42,10 @@ int jfs_launch_crc32c(const jfs_dev_block *d_blocks, int nblk, int32_t seg_bytes
                       hipStream_t stream);
 int jfs_launch_crc32c_lens(const jfs_dev_block *d_blocks, int nblk, const int32_t *d_lens, const uint32_t *d_seeds,
                            uint32_t *d_crc, hipStream_t stream);
+// per-seg_bytes checksums (jfs_crc32c_device's dst layout) of device blocks
+// whose length the previous kernel wrote (lens; < 0: it failed, nothing written)
+int jfs_launch_crc32c_segs_lens(const jfs_dev_block *d_blocks, int nblk, int32_t seg_bytes, const int32_t *d_lens,
+                                hipStream_t stream);
 int jfs_launch_aes256gcm(const jfs_aead_block *d_blocks, int nblk, int mode, int32_t *d_ret, const int32_t *d_lens,
                          hipStream_t stream);
 int jfs_launch_aead(int cipher, const jfs_aead_block *d_blocks, int nblk, int mode, int32_t *d_ret,

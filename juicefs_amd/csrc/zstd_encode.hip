@@ -49,6 +49,9 @@ namespace jfs {
 namespace zl1 {
 
 constexpr int32_t BLK = 128 << 10;  // ZSTD_BLOCKSIZE_MAX
+#ifndef JFS_ZL1_PB
+#define JFS_ZL1_PB 16  // search iterations tried at once right after a match (then 64)
+#endif
 
 // ---------------------------------------------------------------------------
 // parameters: ZSTD_getCParams(1, n, 0) (level-1 row of the size tier, then
@@ -102,45 +105,50 @@ __device__ __forceinline__ uint64_t seq_pack(uint32_t ll, uint32_t mlb, uint32_t
 }
 
 // ---------------------------------------------------------------------------
-// source access: aligned dword loads that never touch a dword holding no input
-// byte (so never a page the input does not reach), bytes past the end read 0
+// source access through a buffer resource: the descriptor covers exactly the
+// dwords that hold input bytes, so every load is range-checked by the
+// hardware (out-of-range dwords read 0, nothing past the input is touched)
+// and needs only a 32-bit offset -- no per-load guards or 64-bit address math
 // ---------------------------------------------------------------------------
 struct Src {
-    const gc_u32 *w;
-    uint32_t sh;
-    int32_t nw;  // dwords holding at least one input byte
-    const gc_u8 *b;
+    __amdgpu_buffer_rsrc_t r;
+    int32_t sh;  // input byte 0 sits at byte sh of the first dword
 };
 __device__ __forceinline__ Src make_src(const uint8_t *p, int32_t n) {
     Src s;
-    s.w = (const gc_u32 *)((uintptr_t)p & ~(uintptr_t)3);
-    s.sh = (uint32_t)((uintptr_t)p & 3u);
-    s.nw = n > 0 ? (int32_t)((n - 1 + s.sh) >> 2) + 1 : 0;
-    s.b = (const gc_u8 *)p;
+    const uintptr_t a = (uintptr_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)(a & ~(uintptr_t)3));
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    s.sh = (int32_t)__builtin_amdgcn_readfirstlane((uint32_t)(a & 3u));
+    const int32_t nb = n > 0 ? (int32_t)((n + s.sh + 3) & ~3) : 0;
+    s.r = __builtin_amdgcn_make_buffer_rsrc((void *)(((uintptr_t)hi << 32) | lo), 0,
+                                            (int)__builtin_amdgcn_readfirstlane((uint32_t)nb), 0x00020000);
     return s;
 }
-__device__ __forceinline__ uint32_t wd(const Src &S, int32_t i) { return (i >= 0 && i < S.nw) ? S.w[i] : 0u; }
-// 4 bytes at position p (p may be negative / past the end: those bytes read as 0)
-__device__ __forceinline__ uint32_t ld32(const Src &S, int32_t p) {
-    const int32_t b = p + (int32_t)S.sh;
-    const int32_t i = b >> 2;
-    const uint32_t s = (uint32_t)b & 3u;
-    const uint32_t w0 = wd(S, i), w1 = wd(S, i + 1);
-    return __builtin_amdgcn_alignbyte(w1, w0, s);
+__device__ __forceinline__ uint32_t ldw(const Src &S, int32_t byteoff) {
+    return __builtin_amdgcn_raw_buffer_load_b32(S.r, (uint32_t)byteoff, 0, 0);
 }
-__device__ __forceinline__ uint64_t ld64(const Src &S, int32_t p) {
-    const int32_t b = p + (int32_t)S.sh;
-    const int32_t i = b >> 2;
-    const uint32_t s = (uint32_t)b & 3u;
-    const uint32_t w0 = wd(S, i), w1 = wd(S, i + 1), w2 = wd(S, i + 2);
-    return (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, s) | ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, s) << 32);
+// byte at position p
+__device__ __forceinline__ uint32_t ldb(const Src &S, int32_t p) {
+    return __builtin_amdgcn_raw_buffer_load_b8(S.r, (uint32_t)(p + S.sh), 0, 0);
 }
-// 16 bytes at position p
+// 16 bytes at position p (p >= -3; bytes before the input read 0).  A
+// negative offset must never reach a buffer instruction: the compiler merges
+// the five loads into wider ones and the whole merged load would read 0.
 __device__ __forceinline__ uint4 ld128(const Src &S, int32_t p) {
-    const int32_t b = p + (int32_t)S.sh;
-    const int32_t i = b >> 2;
+    const int32_t b = p + S.sh;
+    const int32_t o = b & ~3;
     const uint32_t s = (uint32_t)b & 3u;
-    const uint32_t w0 = wd(S, i), w1 = wd(S, i + 1), w2 = wd(S, i + 2), w3 = wd(S, i + 3), w4 = wd(S, i + 4);
+    const bool neg = o < 0;
+    const int32_t oc = neg ? 0 : o;
+    uint32_t w0 = ldw(S, oc), w1 = ldw(S, oc + 4), w2 = ldw(S, oc + 8), w3 = ldw(S, oc + 12), w4 = ldw(S, oc + 16);
+    if (neg) {  // o == -4: the words are one dword later than loaded
+        w4 = w3;
+        w3 = w2;
+        w2 = w1;
+        w1 = w0;
+        w0 = 0;
+    }
     uint4 r;
     r.x = __builtin_amdgcn_alignbyte(w1, w0, s);
     r.y = __builtin_amdgcn_alignbyte(w2, w1, s);
@@ -148,6 +156,24 @@ __device__ __forceinline__ uint4 ld128(const Src &S, int32_t p) {
     r.w = __builtin_amdgcn_alignbyte(w4, w3, s);
     return r;
 }
+
+#ifdef JFS_PROF
+// diagnostic build only: per-phase s_memtime sums of the parse waves
+// (0 positions + windows + hashes, 1 after-match inserts + repeat loop, 2 table
+// reads + bucket tags, 3 candidate loads + decision, 4 table writes, 5 match
+// extension, 6 block setup (RLE scan, window refresh); 8 sequences, 9 search
+// steps, 10 extension round trips, 11 blocks)
+__device__ unsigned long long g_zpprof[12];
+#define ZP_DECL uint64_t zp_t = __builtin_amdgcn_s_memtime(), zp_acc[12] = {0};
+#define ZP(k) do { const uint64_t x_ = __builtin_amdgcn_s_memtime(); zp_acc[k] += x_ - zp_t; zp_t = x_; } while (0)
+#define ZPC(k) (zp_acc[k] += 1)
+#define ZP_FLUSH() do { if (lane_id() == 0) for (int i_ = 0; i_ < 12; ++i_) atomicAdd(&g_zpprof[i_], (unsigned long long)zp_acc[i_]); } while (0)
+#else
+#define ZP_DECL
+#define ZP(k) do { } while (0)
+#define ZPC(k) do { } while (0)
+#define ZP_FLUSH() do { } while (0)
+#endif
 
 // ZSTD_hashPtr for minMatch 5 / 6 / 7 of the 8 little-endian bytes at a position
 __device__ __forceinline__ uint32_t zhash(uint64_t v, uint32_t hlog, uint32_t mls) {
@@ -201,7 +227,7 @@ __device__ int32_t fwd_count(const Src &S, int32_t a, int32_t b, int32_t lim) {
     if (lim <= 0) return 0;
     {
         bool eq = false;
-        if (l < lim) eq = S.b[a + l] == S.b[b + l];
+        if (l < lim) eq = ldb(S, a + l) == ldb(S, b + l);
         const int r = ctz64(~ballot(eq));
         if (r < 64) return r;
     }
@@ -232,13 +258,66 @@ __device__ int32_t back_count(const Src &S, int32_t a, int32_t b, int32_t lim) {
     for (int guard = 0; guard < 4096 && m < lim; guard++) {
         const int32_t k = m + l;
         bool eq = false;
-        if (k < lim) eq = S.b[a - 1 - k] == S.b[b - 1 - k];
+        if (k < lim) eq = ldb(S, a - 1 - k) == ldb(S, b - 1 - k);
         const int r = ctz64(~ballot(eq));
         if (r < 64) return m + r;
         m += 64;
     }
     return lim < m ? lim : m;
 }
+
+// remaining forward / backward equal-byte counts of a match; the first
+// 64-byte steps of both directions are loaded in one round trip
+__device__ void ext_counts(const Src &S, int32_t fa, int32_t fb, int32_t flim, int32_t ba, int32_t bb, int32_t blim,
+                           int32_t &fwd, int32_t &bk) {
+    const int l = lane_id();
+    uint32_t x0 = 0, x1 = 1, y0 = 0, y1 = 1;
+    if (l < flim) {
+        x0 = ldb(S, fa + l);
+        x1 = ldb(S, fb + l);
+    }
+    if (l < blim) {
+        y0 = ldb(S, ba - 1 - l);
+        y1 = ldb(S, bb - 1 - l);
+    }
+    const int rf = ctz64(~ballot(l < flim && x0 == x1)), rb = ctz64(~ballot(l < blim && y0 == y1));
+    fwd = rf < 64 ? rf : 64 + fwd_count(S, fa + 64, fb + 64, flim - 64);
+    bk = rb < 64 ? rb : 64 + back_count(S, ba - 64, bb - 64, blim - 64);
+}
+
+// bit i set when byte i of a equals byte i of b
+__device__ __forceinline__ uint32_t eqmask16(uint4 a, uint4 b) {
+    const uint32_t x[4] = {a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w};
+    uint32_t m = 0;
+#pragma unroll
+    for (int d = 0; d < 4; d++)
+#pragma unroll
+        for (int k = 0; k < 4; k++) m |= (((x[d] >> (8 * k)) & 0xFFu) == 0u ? 1u : 0u) << (4 * d + k);
+    return m;
+}
+// index, counted from byte k, of the first nonzero byte of x at or after k (16 - k: none)
+__device__ __forceinline__ uint32_t first_diff(uint4 x, int k) {
+    uint64_t lo = (uint64_t)x.x | ((uint64_t)x.y << 32), hi = (uint64_t)x.z | ((uint64_t)x.w << 32);
+    if (k >= 8) {
+        lo = hi >> (8 * (k - 8));
+        hi = 0;
+    } else if (k > 0) {
+        lo = (lo >> (8 * k)) | (hi << (64 - 8 * k));
+        hi >>= 8 * k;
+    }
+    if (lo) return (uint32_t)__builtin_ctzll(lo) >> 3;
+    if (hi) return 8 + ((uint32_t)__builtin_ctzll(hi) >> 3);
+    return (uint32_t)(16 - k);
+}
+__device__ __forceinline__ uint4 readlane4(uint4 v, int j) {
+    return make_uint4(readlane(v.x, j), readlane(v.y, j), readlane(v.z, j), readlane(v.w, j));
+}
+
+// compiler-only ordering point: the LDS executes one wave's DS instructions in
+// issue order, so a one-wave workgroup needs neither s_barrier nor an lgkmcnt
+// drain between its own LDS writes and reads -- only that the compiler keeps
+// their order
+__device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
 
 // step-schedule position of search iteration l from ip0 (ZSTD_compressBlock_fast:
 // ip += ((ip - anchor) >> 7) + 2 on a miss)
@@ -265,7 +344,7 @@ __device__ __forceinline__ int32_t sched_pos(int32_t ip0, int32_t anchor, uint32
 // all bytes of [a, b) equal (ZSTD_isRLE)
 __device__ bool all_equal(const Src &S, int32_t a, int32_t b) {
     const int l = lane_id();
-    const uint32_t c = S.b[a];
+    const uint32_t c = ldb(S, a);
     const uint32_t c4 = c * 0x01010101u;
     for (int32_t p0 = a; p0 < b; p0 += 1024) {
         const int32_t p = p0 + 16 * l;
@@ -307,6 +386,7 @@ __global__ __launch_bounds__(64) void zl1_parse_kernel(const FInfo *__restrict__
     __syncthreads();
     const Src S = make_src(F.src, F.n);
     uint32_t off1 = 1, off2 = 4;  // repStartValue
+    ZP_DECL
     for (int32_t k = 0; k < F.nb; k++) {
         BInfo &B = bi[F.b0 + k];
         const int32_t bs = B.bs, be = B.be;
@@ -329,6 +409,8 @@ __global__ __launch_bounds__(64) void zl1_parse_kernel(const FInfo *__restrict__
                 if (T.get(h, R) <= prefixIdx) T.put(h, prefixIdx);
             __syncthreads();
         }
+        ZP(6);
+        ZPC(11);
         // ---- ZSTD_compressBlock_fast_generic
         uint64_t *sq = seqs + B.seq_off;
         const int32_t ilimit = be - 8;
@@ -344,45 +426,59 @@ __global__ __launch_bounds__(64) void zl1_parse_kernel(const FInfo *__restrict__
         for (int guard = 0; guard < 4 * BLK; guard++) {
             // positions of this search step (after a match: ip0 + 2 l)
             const int32_t q = pend ? ip0 + 2 * l : sched_pos(ip0, anchor, (uint32_t)l);
-            const bool on = q + 1 < ilimit;
+            const bool on = q + 1 < ilimit && (!pend || l < JFS_ZL1_PB);
             const bool ld = on || (pend && l == 0 && ip0 <= ilimit);
-            uint4 W = make_uint4(0, 0, 0, 0);  // bytes [q - 2, q + 14)
-            uint64_t rw = 0;                   // bytes [q + 1 - o1, q + 9 - o1)
-            uint32_t r2 = 0;                   // (lane 0, pend) 4 bytes at ip0 - o2
+            // windows: A = bytes [q - 2, q + 14), AR = the same o1 bytes back
+            // (repeat check + its first extension bytes), R2 = (lane 0, after a
+            // match) the same o2 bytes back from ip0 (the repeat loop)
+            uint4 A = make_uint4(0, 0, 0, 0), AR = make_uint4(0, 0, 0, 0), R2 = make_uint4(0, 0, 0, 0);
             if (ld) {
-                W = ld128(S, q - 2);
-                if (o1 > 0) rw = ld64(S, q + 1 - (int32_t)o1);
-                if (pend && l == 0 && o2 > 0) r2 = ld32(S, ip0 - (int32_t)o2);
+                A = ld128(S, q - 2);
+                AR = ld128(S, q - 2 - (int32_t)o1);
+                if (pend && l == 0) R2 = ld128(S, ip0 - 2 - (int32_t)o2);
             }
-            const uint64_t v0 = (uint64_t)__builtin_amdgcn_alignbyte(W.y, W.x, 2) | ((uint64_t)__builtin_amdgcn_alignbyte(W.z, W.y, 2) << 32);
-            const uint64_t v1 = (uint64_t)__builtin_amdgcn_alignbyte(W.y, W.x, 3) | ((uint64_t)__builtin_amdgcn_alignbyte(W.z, W.y, 3) << 32);
-            const uint32_t val0 = (uint32_t)v0, val1 = (uint32_t)v1, val2 = W.y;
+            const uint64_t v0 = (uint64_t)__builtin_amdgcn_alignbyte(A.y, A.x, 2) | ((uint64_t)__builtin_amdgcn_alignbyte(A.z, A.y, 2) << 32);
+            const uint64_t v1 = (uint64_t)__builtin_amdgcn_alignbyte(A.y, A.x, 3) | ((uint64_t)__builtin_amdgcn_alignbyte(A.z, A.y, 3) << 32);
+            const uint32_t val0 = (uint32_t)v0, val1 = (uint32_t)v1;
             const uint32_t h0 = zhash(v0, hlog, mls), h1 = zhash(v1, hlog, mls);
+            ZP(0);
+            ZPC(9);
             if (pend) {
-                const uint32_t cur = readlane(val0, 0);  // 4 bytes at ip0
                 if (pend == 1) {  // hashTable[hash(ip0 - 2)] = ip0 - 2
-                    const uint64_t vm2 = (uint64_t)W.x | ((uint64_t)W.y << 32);
+                    const uint64_t vm2 = (uint64_t)A.x | ((uint64_t)A.y << 32);
                     const uint32_t hm2 = readlane(zhash(vm2, hlog, mls), 0);
                     if (l == 0) T.put(hm2, (uint32_t)(ip0 - 2 + 1));
-                    __syncthreads();
+                    lds_order();
                 }
                 pend = 0;
-                if (o2 > 0 && ip0 <= ilimit && cur == readlane(r2, 0)) {
-                    // repeat-offset match at ip0 (offset_2), then swap
-                    const int32_t rl = 4 + fwd_count(S, ip0 + 4, ip0 + 4 - (int32_t)o2, be - (ip0 + 4));
-                    const uint32_t t = o2;
-                    o2 = o1;
-                    o1 = t;
-                    if (l == 0) T.put(readlane(h0, 0), (uint32_t)(ip0 + 1));
-                    __syncthreads();
-                    if (l == 0) sq[ns] = seq_pack(0, (uint32_t)(rl - 3), 1);
-                    ns++;
-                    ip0 += rl;
-                    anchor = ip0;
-                    if (ip0 <= ilimit) pend = 2;
-                    continue;
+                if (o2 > 0 && ip0 <= ilimit) {
+                    const uint4 a0 = readlane4(A, 0), r0 = readlane4(R2, 0);
+                    const uint4 X = make_uint4(a0.x ^ r0.x, a0.y ^ r0.y, a0.z ^ r0.z, a0.w ^ r0.w);
+                    if (first_diff(X, 2) >= 4) {  // MEM_read32(ip0) == MEM_read32(ip0 - offset_2)
+                        // repeat-offset match at ip0 (offset_2), then swap
+                        const int32_t flim = be - (ip0 + 4);
+                        int32_t rl = (int32_t)umin32(first_diff(X, 6), (uint32_t)flim);
+                        if (rl == 10 && rl < flim) {
+                            int32_t f2 = 0, b2 = 0;
+                            ext_counts(S, ip0 + 4 + rl, ip0 + 4 + rl - (int32_t)o2, flim - rl, 0, 0, 0, f2, b2);
+                            rl += f2;
+                        }
+                        rl += 4;
+                        const uint32_t t = o2;
+                        o2 = o1;
+                        o1 = t;
+                        if (l == 0) T.put(readlane(h0, 0), (uint32_t)(ip0 + 1));
+                        lds_order();
+                        if (l == 0) sq[ns] = seq_pack(0, (uint32_t)(rl - 3), 1);
+                        ns++;
+                        ip0 += rl;
+                        anchor = ip0;
+                        if (ip0 <= ilimit) pend = 2;
+                        continue;
+                    }
                 }
             }
+            ZP(1);
             const uint64_t onm = ballot(on);
             if (!onm) break;  // ip1 >= ilimit: no more positions in this block
             const int non = 64 - __builtin_clzll(onm);  // lanes [0, non) are on
@@ -395,12 +491,12 @@ __global__ __launch_bounds__(64) void zl1_parse_kernel(const FInfo *__restrict__
                 i0 = T.get(h0, R);
                 i1 = T.get(h1, R);
             }
-            __syncthreads();
+            lds_order();
             if (on) {
                 T.lo[h0] = (uint16_t)l;
                 T.lo[h1] = (uint16_t)l;
             }
-            __syncthreads();
+            lds_order();
             uint32_t cm = 64;
             if (on) {
                 const uint32_t t0 = T.lo[h0], t1 = T.lo[h1];
@@ -409,70 +505,104 @@ __global__ __launch_bounds__(64) void zl1_parse_kernel(const FInfo *__restrict__
             }
             const int cut = (int)dwave_min(cm) + 1;
             const int nbt = cut < non ? cut : non;  // lanes [0, nbt) read exactly what the serial loop reads
+            ZP(2);
             const bool dec = l < nbt;
-            const bool rep = dec && o1 > 0 && (uint32_t)(rw >> 8) == val2;
+            const bool rep = dec && o1 > 0 && AR.y == A.y;  // MEM_read32(ip2 - offset_1) == MEM_read32(ip2)
             const bool c0 = dec && i0 > prefixIdx, c1 = dec && i1 > prefixIdx;
-            uint32_t m0 = 0, m1 = 0;
-            if (c0) m0 = ld32(S, (int32_t)i0 - 1);
-            if (c1) m1 = ld32(S, (int32_t)i1 - 1);
-            const bool k0 = c0 && m0 == val0, k1 = c1 && m1 == val1;
+            // candidates: bytes [cand - 2, cand + 14) (check + first extension bytes)
+            uint4 X0 = make_uint4(0, 0, 0, 0), X1 = make_uint4(0, 0, 0, 0);
+            if (c0) X0 = ld128(S, (int32_t)i0 - 3);
+            if (c1) X1 = ld128(S, (int32_t)i1 - 3);
+            const bool k0 = c0 && __builtin_amdgcn_alignbyte(X0.y, X0.x, 2) == val0;
+            const bool k1 = c1 && __builtin_amdgcn_alignbyte(X1.y, X1.x, 2) == val1;
             const int j = ctz64(ballot(rep || k0 || k1));
+            ZP(3);
             // lanes after the first hit (and past the cut) put their buckets
             // back; then the lanes up to the hit insert ip0 and ip1
-            __syncthreads();
+            lds_order();
             if (on && (l >= nbt || l > j)) {
                 T.lo[h0] = (uint16_t)olo0;
                 T.lo[h1] = (uint16_t)olo1;
             }
-            __syncthreads();
+            lds_order();
             if (on && l < nbt && l <= j) {
                 T.put(h0, (uint32_t)q + 1);
                 T.put(h1, (uint32_t)q + 2);
             }
-            __syncthreads();
+            lds_order();
+            ZP(4);
             if (j >= 64) {
                 const int32_t ql = (int32_t)readlane((uint32_t)q, nbt - 1);
                 ip0 = ql + ((ql - anchor) >> 7) + 2;
                 continue;
             }
-            // ---- a match at iteration j
+            // ---- a match at iteration j: the cheap part of its extension
+            // comes from the windows already loaded (uniform values)
             const int32_t qj = (int32_t)readlane((uint32_t)q, j);
-            const bool jrep = readlane(rep ? 1u : 0u, j) != 0, jk0 = readlane(k0 ? 1u : 0u, j) != 0;
-            const uint32_t h2 = zhash((uint64_t)W.y | ((uint64_t)W.z << 32), hlog, mls);  // hash at q + 2
-            const uint32_t jh2 = readlane(h2, j);
-            int32_t start, mst, mlen;
+            const int jt = (int)readlane(rep ? 0u : k0 ? 1u : 2u, j);
+            const uint4 Aj = readlane4(A, j);
+            const uint4 Bj = readlane4(jt == 0 ? AR : jt == 1 ? X0 : X1, j);
+            const uint32_t jh2 = zhash((uint64_t)Aj.y | ((uint64_t)Aj.z << 32), hlog, mls);  // hash at q + 2
+            int32_t start, mst, mlen, fcheap, bcheap;
+            bool fex, bex;
             uint32_t ofv;
-            if (jrep) {
-                const uint32_t bq1 = readlane(W.x >> 24, j), brp = readlane((uint32_t)rw & 0xFFu, j);
-                const int32_t ml0 = bq1 == brp ? 1 : 0;
+            if (jt == 0) {
+                const uint4 X = make_uint4(Aj.x ^ Bj.x, Aj.y ^ Bj.y, Aj.z ^ Bj.z, Aj.w ^ Bj.w);
+                const int32_t ml0 = (X.x >> 24) == 0u ? 1 : 0;  // ip2[-1] == repMatch[-1]
                 start = qj + 2 - ml0;
                 mst = start - (int32_t)o1;
                 mlen = 4 + ml0;
+                fcheap = (int32_t)first_diff(X, 8);  // bytes q+6 .. q+13
+                fex = fcheap == 8;
+                bcheap = 0;
+                bex = false;
                 ofv = 1;
             } else {
-                start = jk0 ? qj : qj + 1;
-                mst = (int32_t)readlane(jk0 ? i0 : i1, j) - 1;
+                uint4 Aa = Aj;
+                if (jt == 2)  // the match starts at q + 1: shift the window by a byte
+                    Aa = make_uint4(__builtin_amdgcn_alignbyte(Aj.y, Aj.x, 1), __builtin_amdgcn_alignbyte(Aj.z, Aj.y, 1),
+                                    __builtin_amdgcn_alignbyte(Aj.w, Aj.z, 1), Aj.w >> 8);
+                const uint4 X = make_uint4(Aa.x ^ Bj.x, Aa.y ^ Bj.y, Aa.z ^ Bj.z, Aa.w ^ Bj.w);
+                start = jt == 1 ? qj : qj + 1;
+                mst = (int32_t)readlane(jt == 1 ? i0 : i1, j) - 1;
                 o2 = o1;
                 o1 = (uint32_t)(start - mst);
                 ofv = o1 + 3;
                 mlen = 4;
-                const int32_t lim = umin32((uint32_t)(start - anchor), (uint32_t)(mst - prefixPos));
-                const int32_t bk = back_count(S, start, mst, lim);
-                start -= bk;
-                mst -= bk;
-                mlen += bk;
+                const int32_t favail = jt == 1 ? 10 : 9;  // bytes start+4 .. (window end)
+                fcheap = (int32_t)umin32(first_diff(X, 6), (uint32_t)favail);
+                fex = fcheap == favail;
+                bcheap = ((X.x >> 8) & 0xFFu) ? 0 : ((X.x & 0xFFu) ? 1 : 2);
+                bex = bcheap == 2;
             }
-            mlen += fwd_count(S, start + mlen, mst + mlen, be - (start + mlen));
+            const int32_t flim = be - (start + mlen);
+            const int32_t blim = jt == 0 ? 0 : (int32_t)umin32((uint32_t)(start - anchor), (uint32_t)(mst - prefixPos));
+            if (fcheap > flim) fcheap = flim;
+            if (bcheap > blim) bcheap = blim;
+            const bool nf = fex && fcheap < flim, nbk = bex && bcheap < blim;
+            if (nf || nbk) {
+                ZPC(10);
+                int32_t f2 = 0, b2 = 0;
+                ext_counts(S, start + mlen + fcheap, mst + mlen + fcheap, nf ? flim - fcheap : 0, start - bcheap,
+                           mst - bcheap, nbk ? blim - bcheap : 0, f2, b2);
+                fcheap += f2;
+                bcheap += b2;
+            }
+            start -= bcheap;
+            mst -= bcheap;
+            mlen += bcheap + fcheap;
             if (l == 0) sq[ns] = seq_pack((uint32_t)(start - anchor), (uint32_t)(mlen - 3), ofv);
             ns++;
+            ZPC(8);
             nl += start - anchor;
             ip0 = start + mlen;
             anchor = ip0;
             if (ip0 <= ilimit) {
                 if (l == 0) T.put(jh2, (uint32_t)(qj + 2 + 1));  // hashTable[hash(current0 + 2)]
-                __syncthreads();
+                lds_order();
                 pend = 1;
             }
+            ZP(5);
         }
         nl += be - anchor;
         const uint32_t ro0 = o1 ? o1 : saved, ro1 = o2 ? o2 : saved;
@@ -488,6 +618,7 @@ __global__ __launch_bounds__(64) void zl1_parse_kernel(const FInfo *__restrict__
             off2 = ro1;
         }
     }
+    ZP_FLUSH();
 }
 
 // ---------------------------------------------------------------------------
@@ -844,7 +975,8 @@ __global__ __launch_bounds__(64) void zl1_seq_kernel(const FInfo *__restrict__ f
                     const uint32_t lpr = (uint32_t)__shfl((int)lp, lo, 64), spr = (uint32_t)__shfl((int)sp, lo, 64);
                     const int32_t pos = bs + sbase + (int32_t)spr + (int32_t)(te - lpr);
                     xs[u] = t < Lc ? lbase + (int32_t)t : -1;
-                    bv[u] = t < Lc ? (uint32_t)S.b[pos] : 0u;
+                    bv[u] = ldb(S, pos);
+                    if (t >= Lc) bv[u] = 0u;
                 }
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
@@ -1567,7 +1699,8 @@ __global__ __launch_bounds__(64) void zl1_lit_kernel(FInfo *__restrict__ fi, con
             op += 3 + bsz;
         } else if (cS == 1) {
             put_bytes(dst, op, (uint32_t)(last ? 1 : 0) | (1u << 1) | ((uint32_t)bsz << 3), 3);
-            if (l == 0) dst[op + 3] = S.b[bs];
+            const uint32_t rb = ldb(S, bs);
+            if (l == 0) dst[op + 3] = (uint8_t)rb;
             op += 4;
         } else {
             put_bytes(dst, op, (uint32_t)(last ? 1 : 0) | (2u << 1) | ((uint32_t)cS << 3), 3);
@@ -1664,6 +1797,16 @@ struct ZL1Scratch {
 ZL1Scratch g_zl1[16];
 inline size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
 }  // namespace
+
+#ifdef JFS_PROF
+extern "C" int jfs_zpprof_read(unsigned long long *out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(jfs::zl1::g_zpprof), sizeof(unsigned long long) * 12) == hipSuccess ? 0 : -1;
+}
+extern "C" int jfs_zpprof_reset() {
+    unsigned long long z[12] = {0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(jfs::zl1::g_zpprof), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" int jfs_launch_zstd_encode(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, hipStream_t stream) {
     if (nblk <= 0) return 0;

@@ -232,3 +232,32 @@ def test_blocks_dealt_to_distinct_devices(gpu, oracle):
         assert max(used.values()) - min(used.values()) <= 2 * 1 + 2, used  # round-robin: balanced
     else:
         assert len(used) == 1, used
+
+
+def test_decompress_batch_disk_cache_checksums(gpu, oracle):
+    """jfs_decompress_batch_csum: the disk-cache checksum of each decoded block
+    (pkg/chunk/disk_cache.go:536-537 / disk_cache_file.go:139-152: big-endian
+    CRC-32C per 32 KiB), computed on the GPU, equals the oracle's layout; LZ4
+    and Zstd, ragged sizes, a corrupt block (no checksum, error), "none"."""
+    from juicefs_amd import compress as C
+    sizes = [1, 100, 32767, 32768, 32769, 65536 + 5, 1 << 20, 4 << 20]
+    raws = [gen_block("TZR"[i % 3], 6100 + i, n) for i, n in enumerate(sizes)]
+    for name in ("lz4", "zstd", "none"):
+        c = C.NewCompressor(name)
+        comps = []
+        for r in raws:
+            d = bytearray(c.CompressBound(len(r)))
+            n, e = c.Compress(d, r)
+            assert e is None
+            comps.append(bytes(d[:n]))
+        if name != "none":
+            comps.append(comps[3][: len(comps[3]) // 2])  # truncated: fails, no checksum
+        outs = [bytearray(len(r)) for r in raws] + ([bytearray(32769)] if name != "none" else [])
+        res = c.DecompressBatchChecksum(list(zip(outs, comps)))
+        for i, r in enumerate(raws):
+            n, e, cs = res[i]
+            assert e is None and n == len(r) and bytes(outs[i][:n]) == r, (name, len(r))
+            assert cs == oracle.crc32c_segments(r), (name, len(r))
+        if name != "none":
+            n, e, cs = res[-1]
+            assert e is not None and cs is None

@@ -139,3 +139,35 @@ def test_seal_and_open_refuse_wrong_key_and_nonce_sizes(lib):
             E.compress_seal_batch(0, algo, [(dst, raw)], [(b"k" * ks, b"n" * 8, b"w")])
         with pytest.raises(ValueError, match="key"):
             E.open_decompress_batch(0, algo, [(dst, raw)], [b"k" * 16 if ks == 32 else b"k" * 32])
+
+
+def test_deal_plan_size_balanced(lib):
+    """the batch calls deal blocks over devices size-balanced
+    (config 4's mixed 64 KiB - 4 MiB blocks), not by count -- checked on the
+    policy itself with fake device counts (no GPU needed)."""
+    import random
+    i64, i32 = ctypes.c_int64, ctypes.c_int32
+
+    def plan(cost, ndev):
+        c = (i64 * len(cost))(*cost)
+        o = (i32 * len(cost))()
+        lib.jfs_deal_plan(c, len(cost), ndev, o)
+        return list(o)
+
+    rng = random.Random(8)
+    for ndev in (1, 2, 3, 8):
+        for n in (1, 5, 64, 500):
+            cost = [int(2 ** rng.uniform(16, 22)) for _ in range(n)]  # 64 KiB .. 4 MiB, log-uniform
+            w = plan(cost, ndev)
+            assert all(0 <= d < ndev for d in w)
+            load = [0] * ndev
+            for c, d in zip(cost, w):
+                load[d] += c
+            used = [x for x in load if x > 0]
+            assert len(used) == min(ndev, n)
+            assert max(load) - min(load) <= max(cost) or n < ndev  # LPT: within one block
+            assert plan(cost, ndev) == w  # deterministic
+    # count-balanced round robin would put both 4 MiB blocks on device 0 here
+    cost = [4 << 20, 64 << 10, 4 << 20, 64 << 10]
+    w = plan(cost, 2)
+    assert w[0] != w[2]

@@ -174,7 +174,7 @@ def test_split_one_segment_exact_cap_stays_on_split_path(gpu, oracle):
     """A block of <= 256 compressed bytes decoded into exactly its size (the
     one-call path's dst) is decoded by the split path itself: the count of a
     segment that ends exactly at dst_cap is not an overflow."""
-    srcs = [gen_block("T", 5100 + i, n) for i, n in enumerate((40, 100, 300, 500))] + [b"a" * 200, b"ab" * 150]
+    srcs = [gen_block("T", 5100 + i, n) for i, n in enumerate((40, 100, 200, 250))] + [b"a" * 200, b"ab" * 150]
     comps = [oracle.lz4_compress(s)[1] for s in srcs]
     assert all(len(c) <= 256 for c in comps), [len(c) for c in comps]
     D.lz4_split_counts(reset=True)
