@@ -50,7 +50,7 @@ namespace zl1 {
 
 constexpr int32_t BLK = 128 << 10;  // ZSTD_BLOCKSIZE_MAX
 #ifndef JFS_ZL1_PB
-#define JFS_ZL1_PB 16  // search iterations tried at once right after a match (then 64)
+#define JFS_ZL1_PB 64  // search iterations tried at once right after a match
 #endif
 
 // ---------------------------------------------------------------------------
@@ -204,16 +204,16 @@ struct Tab {
         const uint32_t e = raw(h);
         return WIDE ? R - ((R - e) & 0xFFFFFu) : e;
     }
+    // fire-and-forget: a u16 store and two LDS atomics (clear, set) on the
+    // nibble's dword, no read round trip; lanes sharing the dword touch
+    // disjoint nibbles
     __device__ __forceinline__ void put(uint32_t h, uint32_t idx) {
         lo[h] = (uint16_t)idx;
         if (WIDE) {
             const uint32_t sh = (h & 7) * 4;
-            const uint32_t nv = ((idx >> 16) & 15u) << sh;
-            const uint32_t cur = hi[h >> 3];
-            if (((cur >> sh) & 15u) != ((idx >> 16) & 15u)) {
-                atomicAnd(&hi[h >> 3], ~(15u << sh));
-                atomicOr(&hi[h >> 3], nv);
-            }
+            (void)__hip_atomic_fetch_and(&hi[h >> 3], ~(15u << sh), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            (void)__hip_atomic_fetch_or(&hi[h >> 3], ((idx >> 16) & 15u) << sh, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     }
 };
@@ -422,66 +422,75 @@ __global__ __launch_bounds__(64) void zl1_parse_kernel(const FInfo *__restrict__
             if (o2 > maxRep) { saved = o2; o2 = 0; }
             if (o1 > maxRep) { saved = o1; o1 = 0; }
         }
+        // sequence records collect in a VGPR (lane i: record 64 g + i) and are
+        // stored 64 at a time: no store per sequence for later vmcnt waits to drain
+        uint64_t sbuf = 0;
+        auto emit = [&](uint32_t ll, uint32_t mlb, uint32_t ofv) {
+            const uint64_t r = seq_pack(ll, mlb, ofv);
+            if (l == (ns & 63)) sbuf = r;
+            if ((ns & 63) == 63) sq[ns - 63 + l] = sbuf;
+            ns++;
+        };
         int pend = 0;  // 1: after a search match (insert ip0-2, then the repeat loop); 2: after a repeat-loop match
+        // windows of the last step whose positions were bp + 2 l (lanes [0, bvalid) valid)
+        uint4 Ap = make_uint4(0, 0, 0, 0);
+        int32_t bp = -1, bvalid = 0;
         for (int guard = 0; guard < 4 * BLK; guard++) {
+            const bool pb = pend != 0;
+            const int32_t ipb = ip0;
             // positions of this search step (after a match: ip0 + 2 l)
-            const int32_t q = pend ? ip0 + 2 * l : sched_pos(ip0, anchor, (uint32_t)l);
-            const bool on = q + 1 < ilimit && (!pend || l < JFS_ZL1_PB);
-            const bool ld = on || (pend && l == 0 && ip0 <= ilimit);
-            // windows: A = bytes [q - 2, q + 14), AR = the same o1 bytes back
-            // (repeat check + its first extension bytes), R2 = (lane 0, after a
-            // match) the same o2 bytes back from ip0 (the repeat loop)
-            uint4 A = make_uint4(0, 0, 0, 0), AR = make_uint4(0, 0, 0, 0), R2 = make_uint4(0, 0, 0, 0);
-            if (ld) {
-                A = ld128(S, q - 2);
-                AR = ld128(S, q - 2 - (int32_t)o1);
-                if (pend && l == 0) R2 = ld128(S, ip0 - 2 - (int32_t)o2);
+            const int32_t q = pb ? ip0 + 2 * l : sched_pos(ip0, anchor, (uint32_t)l);
+            // windows A = bytes [q - 2, q + 14).  After a match they come from
+            // the previous step's lanes when those hold them (a cross-lane
+            // permute instead of a memory round trip); lanes without a source
+            // sit this step out
+            uint4 A = make_uint4(0, 0, 0, 0);
+            const bool use_sh = pb && bp >= 0 && ip0 - bp <= 2 * (bvalid - 2);
+            bool have = true;
+            if (use_sh) {
+                const int32_t e = (ip0 - bp) + 2 * l;
+                const int s0 = e >> 1;
+                const uint32_t dl = (uint32_t)e & 1u;
+                const int sa = s0 < 63 ? s0 : 63, sb = s0 + 1 < 63 ? s0 + 1 : 63;
+                const uint32_t x0 = (uint32_t)__shfl((int)Ap.x, sa, 64), x1 = (uint32_t)__shfl((int)Ap.y, sa, 64),
+                               x2 = (uint32_t)__shfl((int)Ap.z, sa, 64), x3 = (uint32_t)__shfl((int)Ap.w, sa, 64),
+                               y3 = (uint32_t)__shfl((int)Ap.w, sb, 64);
+                A = dl ? make_uint4(__builtin_amdgcn_alignbyte(x1, x0, 1), __builtin_amdgcn_alignbyte(x2, x1, 1),
+                                    __builtin_amdgcn_alignbyte(x3, x2, 1), __builtin_amdgcn_alignbyte(y3 >> 16, x3, 1))
+                       : make_uint4(x0, x1, x2, x3);
+                have = s0 + (int)dl < bvalid;
             }
+            const bool on = q + 1 < ilimit && (!pb || l < JFS_ZL1_PB) && have;
+            // (after a match every lane loads its window, on or not: the next
+            // step's windows then come from these)
+            const bool ld = !use_sh && (pb || on);
+            // AR = the same bytes o1 back (repeat check + its first extension
+            // bytes), R2 = (lane 0, after a match) 16 bytes at ip0 - 2 - o2 (the
+            // repeat loop): both awaited only where used
+            uint4 AR = make_uint4(0, 0, 0, 0), R2 = make_uint4(0, 0, 0, 0);
+            if (ld) A = ld128(S, q - 2);
+            if (on) AR = ld128(S, q - 2 - (int32_t)o1);
+            if (pb && l == 0) R2 = ld128(S, ip0 - 2 - (int32_t)o2);
+            const int32_t vcount = pb ? (int32_t)__builtin_popcountll(ballot(use_sh ? have : ld)) : 0;
             const uint64_t v0 = (uint64_t)__builtin_amdgcn_alignbyte(A.y, A.x, 2) | ((uint64_t)__builtin_amdgcn_alignbyte(A.z, A.y, 2) << 32);
             const uint64_t v1 = (uint64_t)__builtin_amdgcn_alignbyte(A.y, A.x, 3) | ((uint64_t)__builtin_amdgcn_alignbyte(A.z, A.y, 3) << 32);
             const uint32_t val0 = (uint32_t)v0, val1 = (uint32_t)v1;
             const uint32_t h0 = zhash(v0, hlog, mls), h1 = zhash(v1, hlog, mls);
             ZP(0);
             ZPC(9);
-            if (pend) {
-                if (pend == 1) {  // hashTable[hash(ip0 - 2)] = ip0 - 2
-                    const uint64_t vm2 = (uint64_t)A.x | ((uint64_t)A.y << 32);
-                    const uint32_t hm2 = readlane(zhash(vm2, hlog, mls), 0);
-                    if (l == 0) T.put(hm2, (uint32_t)(ip0 - 2 + 1));
-                    lds_order();
-                }
-                pend = 0;
-                if (o2 > 0 && ip0 <= ilimit) {
-                    const uint4 a0 = readlane4(A, 0), r0 = readlane4(R2, 0);
-                    const uint4 X = make_uint4(a0.x ^ r0.x, a0.y ^ r0.y, a0.z ^ r0.z, a0.w ^ r0.w);
-                    if (first_diff(X, 2) >= 4) {  // MEM_read32(ip0) == MEM_read32(ip0 - offset_2)
-                        // repeat-offset match at ip0 (offset_2), then swap
-                        const int32_t flim = be - (ip0 + 4);
-                        int32_t rl = (int32_t)umin32(first_diff(X, 6), (uint32_t)flim);
-                        if (rl == 10 && rl < flim) {
-                            int32_t f2 = 0, b2 = 0;
-                            ext_counts(S, ip0 + 4 + rl, ip0 + 4 + rl - (int32_t)o2, flim - rl, 0, 0, 0, f2, b2);
-                            rl += f2;
-                        }
-                        rl += 4;
-                        const uint32_t t = o2;
-                        o2 = o1;
-                        o1 = t;
-                        if (l == 0) T.put(readlane(h0, 0), (uint32_t)(ip0 + 1));
-                        lds_order();
-                        if (l == 0) sq[ns] = seq_pack(0, (uint32_t)(rl - 3), 1);
-                        ns++;
-                        ip0 += rl;
-                        anchor = ip0;
-                        if (ip0 <= ilimit) pend = 2;
-                        continue;
-                    }
-                }
+            if (pend == 1) {  // hashTable[hash(ip0 - 2)] = ip0 - 2
+                const uint64_t vm2 = (uint64_t)A.x | ((uint64_t)A.y << 32);
+                const uint32_t hm2 = readlane(zhash(vm2, hlog, mls), 0);
+                if (l == 0) T.put(hm2, (uint32_t)(ip0 - 2 + 1));
+                lds_order();
             }
-            ZP(1);
+            // the repeat loop's check waits for R2: the search step's table
+            // reads and bucket tags go first (undone if the repeat loop fires)
+            const bool rchk = pb && o2 > 0 && ip0 <= ilimit;
+            pend = 0;
             const uint64_t onm = ballot(on);
-            if (!onm) break;  // ip1 >= ilimit: no more positions in this block
-            const int non = 64 - __builtin_clzll(onm);  // lanes [0, non) are on
+            if (!onm && !rchk) break;  // ip1 >= ilimit: no more positions in this block
+            const int non = onm ? 64 - __builtin_clzll(onm) : 0;  // lanes [0, non) are on
             // table reads (before any write of this step), then tags to find
             // lanes sharing a bucket
             uint32_t olo0 = 0, olo1 = 0, i0 = 0, i1 = 0;
@@ -505,14 +514,50 @@ __global__ __launch_bounds__(64) void zl1_parse_kernel(const FInfo *__restrict__
             }
             const int cut = (int)dwave_min(cm) + 1;
             const int nbt = cut < non ? cut : non;  // lanes [0, nbt) read exactly what the serial loop reads
-            ZP(2);
             const bool dec = l < nbt;
-            const bool rep = dec && o1 > 0 && AR.y == A.y;  // MEM_read32(ip2 - offset_1) == MEM_read32(ip2)
             const bool c0 = dec && i0 > prefixIdx, c1 = dec && i1 > prefixIdx;
             // candidates: bytes [cand - 2, cand + 14) (check + first extension bytes)
             uint4 X0 = make_uint4(0, 0, 0, 0), X1 = make_uint4(0, 0, 0, 0);
             if (c0) X0 = ld128(S, (int32_t)i0 - 3);
             if (c1) X1 = ld128(S, (int32_t)i1 - 3);
+            ZP(2);
+            if (rchk) {
+                const uint4 a0 = readlane4(A, 0), r0 = readlane4(R2, 0);
+                const uint4 X = make_uint4(a0.x ^ r0.x, a0.y ^ r0.y, a0.z ^ r0.z, a0.w ^ r0.w);
+                if (first_diff(X, 2) >= 4) {  // MEM_read32(ip0) == MEM_read32(ip0 - offset_2)
+                    if (on) {  // the search step did not happen: its tags come off
+                        T.lo[h0] = (uint16_t)olo0;
+                        T.lo[h1] = (uint16_t)olo1;
+                    }
+                    lds_order();
+                    // repeat-offset match at ip0 (offset_2), then swap
+                    const int32_t flim = be - (ip0 + 4);
+                    int32_t rl = (int32_t)umin32(first_diff(X, 6), (uint32_t)flim);
+                    if (rl == 10 && rl < flim) {
+                        int32_t f2 = 0, b2 = 0;
+                        ext_counts(S, ip0 + 4 + rl, ip0 + 4 + rl - (int32_t)o2, flim - rl, 0, 0, 0, f2, b2);
+                        rl += f2;
+                    }
+                    rl += 4;
+                    const uint32_t t = o2;
+                    o2 = o1;
+                    o1 = t;
+                    if (l == 0) T.put(readlane(h0, 0), (uint32_t)(ip0 + 1));
+                    lds_order();
+                    emit(0, (uint32_t)(rl - 3), 1);
+                    Ap = A;
+                    bp = ipb;
+                    bvalid = vcount;
+                    ip0 += rl;
+                    anchor = ip0;
+                    if (ip0 <= ilimit) pend = 2;
+                    ZP(1);
+                    continue;
+                }
+            }
+            ZP(1);
+            if (!onm) break;
+            const bool rep = dec && o1 > 0 && AR.y == A.y;  // MEM_read32(ip2 - offset_1) == MEM_read32(ip2)
             const bool k0 = c0 && __builtin_amdgcn_alignbyte(X0.y, X0.x, 2) == val0;
             const bool k1 = c1 && __builtin_amdgcn_alignbyte(X1.y, X1.x, 2) == val1;
             const int j = ctz64(ballot(rep || k0 || k1));
@@ -534,49 +579,56 @@ __global__ __launch_bounds__(64) void zl1_parse_kernel(const FInfo *__restrict__
             if (j >= 64) {
                 const int32_t ql = (int32_t)readlane((uint32_t)q, nbt - 1);
                 ip0 = ql + ((ql - anchor) >> 7) + 2;
+                bp = -1;
                 continue;
             }
-            // ---- a match at iteration j: the cheap part of its extension
-            // comes from the windows already loaded (uniform values)
+            Ap = A;
+            bp = pb ? ipb : -1;
+            bvalid = vcount;
+            // ---- a match at iteration j.  Every lane works out, in VGPRs, the
+            // match its own iteration would give (start, source, the cheap
+            // part of the extension from the windows already loaded); lane j's
+            // values are then read once (few SGPRs live: no SGPR spills)
+            uint32_t mstart = 0, msrc = 0, mlen0 = 4, fch = 0, bch = 0, mflags = 0;
+            {
+                const int ty = rep ? 0 : k0 ? 1 : 2;
+                uint4 Aa = A;
+                if (ty == 2)  // the match starts at q + 1: shift the window by a byte
+                    Aa = make_uint4(__builtin_amdgcn_alignbyte(A.y, A.x, 1), __builtin_amdgcn_alignbyte(A.z, A.y, 1),
+                                    __builtin_amdgcn_alignbyte(A.w, A.z, 1), A.w >> 8);
+                const uint4 Bb = ty == 0 ? AR : ty == 1 ? X0 : X1;
+                const uint4 X = make_uint4(Aa.x ^ Bb.x, Aa.y ^ Bb.y, Aa.z ^ Bb.z, Aa.w ^ Bb.w);
+                if (ty == 0) {
+                    const uint32_t ml0 = (X.x >> 24) == 0u ? 1u : 0u;  // ip2[-1] == repMatch[-1]
+                    mstart = (uint32_t)q + 2 - ml0;
+                    msrc = mstart - o1;
+                    mlen0 = 4 + ml0;
+                    fch = first_diff(X, 8);  // bytes q+6 .. q+13
+                    mflags = fch == 8 ? 1u : 0u;
+                } else {
+                    mstart = ty == 1 ? (uint32_t)q : (uint32_t)q + 1;
+                    msrc = (ty == 1 ? i0 : i1) - 1;
+                    const uint32_t favail = ty == 1 ? 10 : 9;  // bytes start+4 .. (window end)
+                    fch = umin32(first_diff(X, 6), favail);
+                    bch = ((X.x >> 8) & 0xFFu) ? 0u : ((X.x & 0xFFu) ? 1u : 2u);
+                    mflags = (fch == favail ? 1u : 0u) | (bch == 2 ? 2u : 0u) | 4u;
+                }
+            }
+            const uint32_t h2 = zhash((uint64_t)A.y | ((uint64_t)A.z << 32), hlog, mls);  // hash at q + 2
             const int32_t qj = (int32_t)readlane((uint32_t)q, j);
-            const int jt = (int)readlane(rep ? 0u : k0 ? 1u : 2u, j);
-            const uint4 Aj = readlane4(A, j);
-            const uint4 Bj = readlane4(jt == 0 ? AR : jt == 1 ? X0 : X1, j);
-            const uint32_t jh2 = zhash((uint64_t)Aj.y | ((uint64_t)Aj.z << 32), hlog, mls);  // hash at q + 2
-            int32_t start, mst, mlen, fcheap, bcheap;
-            bool fex, bex;
-            uint32_t ofv;
-            if (jt == 0) {
-                const uint4 X = make_uint4(Aj.x ^ Bj.x, Aj.y ^ Bj.y, Aj.z ^ Bj.z, Aj.w ^ Bj.w);
-                const int32_t ml0 = (X.x >> 24) == 0u ? 1 : 0;  // ip2[-1] == repMatch[-1]
-                start = qj + 2 - ml0;
-                mst = start - (int32_t)o1;
-                mlen = 4 + ml0;
-                fcheap = (int32_t)first_diff(X, 8);  // bytes q+6 .. q+13
-                fex = fcheap == 8;
-                bcheap = 0;
-                bex = false;
-                ofv = 1;
-            } else {
-                uint4 Aa = Aj;
-                if (jt == 2)  // the match starts at q + 1: shift the window by a byte
-                    Aa = make_uint4(__builtin_amdgcn_alignbyte(Aj.y, Aj.x, 1), __builtin_amdgcn_alignbyte(Aj.z, Aj.y, 1),
-                                    __builtin_amdgcn_alignbyte(Aj.w, Aj.z, 1), Aj.w >> 8);
-                const uint4 X = make_uint4(Aa.x ^ Bj.x, Aa.y ^ Bj.y, Aa.z ^ Bj.z, Aa.w ^ Bj.w);
-                start = jt == 1 ? qj : qj + 1;
-                mst = (int32_t)readlane(jt == 1 ? i0 : i1, j) - 1;
+            const uint32_t jh2 = readlane(h2, j);
+            int32_t start = (int32_t)readlane(mstart, j), mst = (int32_t)readlane(msrc, j);
+            int32_t mlen = (int32_t)readlane(mlen0, j), fcheap = (int32_t)readlane(fch, j), bcheap = (int32_t)readlane(bch, j);
+            const uint32_t fl = readlane(mflags, j);
+            const bool fex = fl & 1u, bex = (fl & 2u) != 0, regular = (fl & 4u) != 0;
+            uint32_t ofv = 1;
+            if (regular) {
                 o2 = o1;
                 o1 = (uint32_t)(start - mst);
                 ofv = o1 + 3;
-                mlen = 4;
-                const int32_t favail = jt == 1 ? 10 : 9;  // bytes start+4 .. (window end)
-                fcheap = (int32_t)umin32(first_diff(X, 6), (uint32_t)favail);
-                fex = fcheap == favail;
-                bcheap = ((X.x >> 8) & 0xFFu) ? 0 : ((X.x & 0xFFu) ? 1 : 2);
-                bex = bcheap == 2;
             }
             const int32_t flim = be - (start + mlen);
-            const int32_t blim = jt == 0 ? 0 : (int32_t)umin32((uint32_t)(start - anchor), (uint32_t)(mst - prefixPos));
+            const int32_t blim = !regular ? 0 : (int32_t)umin32((uint32_t)(start - anchor), (uint32_t)(mst - prefixPos));
             if (fcheap > flim) fcheap = flim;
             if (bcheap > blim) bcheap = blim;
             const bool nf = fex && fcheap < flim, nbk = bex && bcheap < blim;
@@ -591,8 +643,7 @@ __global__ __launch_bounds__(64) void zl1_parse_kernel(const FInfo *__restrict__
             start -= bcheap;
             mst -= bcheap;
             mlen += bcheap + fcheap;
-            if (l == 0) sq[ns] = seq_pack((uint32_t)(start - anchor), (uint32_t)(mlen - 3), ofv);
-            ns++;
+            emit((uint32_t)(start - anchor), (uint32_t)(mlen - 3), ofv);
             ZPC(8);
             nl += start - anchor;
             ip0 = start + mlen;
@@ -603,6 +654,10 @@ __global__ __launch_bounds__(64) void zl1_parse_kernel(const FInfo *__restrict__
                 pend = 1;
             }
             ZP(5);
+        }
+        if (ns & 63) {  // the last partial group
+            const int32_t g0 = ns & ~63;
+            if (g0 + l < ns) sq[g0 + l] = sbuf;
         }
         nl += be - anchor;
         const uint32_t ro0 = o1 ? o1 : saved, ro1 = o2 ? o2 : saved;
