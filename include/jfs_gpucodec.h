@@ -221,6 +221,14 @@ int jfs_lz4_eseg_counts(uint64_t *out, int reset);
  * than dst_cap ("Destination buffer is too small"), -3 src size incorrect
  * (truncated / trailing bytes). */
 int64_t jfs_zstd_decompress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream);
+/* Batches of at most JFS_ZSTD_SPLIT_MAX inputs (default 64; also the batch
+ * ABI's staged chunks and jfs_decompress) decode one workgroup per Zstd block
+ * with an origin-map replay; an input outside that path's proven cases (not
+ * exactly one frame, a checksum, any error) is replayed by the exact one-wave
+ * kernel -- same results either way.  Diagnostics: out[0] = inputs the
+ * small-batch path replayed itself, out[1] = inputs it handed over; on the
+ * current device since the last reset.  Synchronous; 0 on success. */
+int jfs_zstd_split_counts(uint64_t *out, int reset);
 /* Zstd frame per block; ret[i] = frame size, or -2 when dst_cap < CompressBound(src_len).
  * Synchronous with respect to `stream` (it uses per-device scratch). */
 int64_t jfs_zstd_compress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream);

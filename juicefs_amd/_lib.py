@@ -34,7 +34,7 @@ EXPORTS = [
     "jfs_gen_block_host", "jfs_release_staging", "jfs_crc32c_device", "jfs_aes256gcm_seal_device",
     "jfs_aes256gcm_open_device", "jfs_lz4_compress_seal_device", "jfs_open_lz4_decompress_device",
     "jfs_gpu_mode", "jfs_stats", "jfs_stats_reset", "jfs_device_stats", "jfs_lz4_decompress_device_small",
-    "jfs_lz4_split_counts", "jfs_lz4_compress_device_small", "jfs_lz4_eseg_counts", "jfs_cipher_from_name", "jfs_cipher_key_size", "jfs_aead_seal_device",
+    "jfs_lz4_split_counts", "jfs_zstd_split_counts", "jfs_lz4_compress_device_small", "jfs_lz4_eseg_counts", "jfs_cipher_from_name", "jfs_cipher_key_size", "jfs_aead_seal_device",
     "jfs_aead_open_device", "jfs_envelope_bound", "jfs_envelope_parse", "jfs_compress_seal_batch",
     "jfs_open_decompress_batch", "jfs_compress_batch_crc", "jfs_decompress_batch_csum", "jfs_deal_plan",
 ]
@@ -101,6 +101,8 @@ def load() -> ctypes.CDLL:
     lib.jfs_lz4_decompress_device_small.restype = i64
     lib.jfs_lz4_split_counts.argtypes = [vp, ctypes.c_int]
     lib.jfs_lz4_split_counts.restype = ctypes.c_int
+    lib.jfs_zstd_split_counts.argtypes = [vp, ctypes.c_int]
+    lib.jfs_zstd_split_counts.restype = ctypes.c_int
     lib.jfs_lz4_compress_device_small.argtypes = [vp, vp, ctypes.c_int, vp, vp]
     lib.jfs_lz4_compress_device_small.restype = ctypes.c_int64
     lib.jfs_lz4_eseg_counts.argtypes = [vp, ctypes.c_int]

@@ -69,7 +69,7 @@ struct Slot {
     uint8_t *z_lit = nullptr, *z_items = nullptr;
     uint16_t *z_tabs = nullptr;
     uint64_t z_lit_cap = 0, z_items_cap = 0, z_tabs_cap = 0;
-    // small-batch LZ4 decode scratch (lz4_split.hip)
+    // small-batch decode scratch (LZ4: lz4_split.hip, Zstd: zstd_split.inc)
     uint8_t *sp = nullptr;
     int64_t sp_cap = 0;
 
@@ -968,6 +968,7 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
             fprintf(stderr, "[jfs host] t=%.2f chunk %d-%d stage-in %.1f MiB %.2f ms\n", now_ms(), c.s, c.e,
                     c.tin / 1048576.0, now_ms() - t0);
         const int n = c.e - c.s;
+        uint64_t ztot[6] = {0, 0, 0, 0, 0, 0};
         if (ae) return launch_aead(c, sl, h_in, h_out, h_desc, h_ret, d_in, d_out, d_desc, d_ret);
         if (algo != JFS_ALGO_LZ4 && algo != JFS_ALGO_ZSTD) return JFS_ERR_UNSUPPORTED;
         if (zplan) {  // plan the Zstd scratch from the staged inputs: no device round trip
@@ -978,9 +979,9 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
                 lens[k] = h_desc[k].src_len;
                 caps[k] = h_desc[k].dst_cap;
             }
-            uint64_t tot[3];
-            jfs_zstd_plan_host(srcs.data(), lens.data(), caps.data(), n, h_zi, tot);
-            if (!sl.ensure_zstd(tot)) return JFS_ERR_NO_MEMORY;
+            jfs_zstd_plan_host(srcs.data(), lens.data(), caps.data(), n, h_zi, ztot);
+            if (!sl.ensure_zstd(ztot)) return JFS_ERR_NO_MEMORY;
+            if (n <= jfs_zstd_split_max() && !sl.ensure_split(jfs_zstd_split_bytes(n, ztot))) return JFS_ERR_NO_MEMORY;
         }
         if (hipMemcpyAsync(d_in, h_in, (size_t)c.tin, hipMemcpyHostToDevice, dev->s_in) != hipSuccess) return JFS_ERR_HIP;
         if (hipMemcpyAsync(d_desc, h_desc, (size_t)n * sizeof(jfs_dev_block), hipMemcpyHostToDevice, dev->s_in) !=
@@ -994,7 +995,8 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
         if (hipStreamWaitEvent(c.ks, sl.ev_in, 0) != hipSuccess) return JFS_ERR_HIP;
         int lk;
         if (zplan) {
-            lk = jfs_launch_zstd_decode_planned(d_desc, n, d_ret, d_zi, sl.z_lit, sl.z_tabs, sl.z_items, c.ks);
+            lk = jfs_launch_zstd_decode_planned(d_desc, n, d_ret, d_zi, sl.z_lit, sl.z_tabs, sl.z_items,
+                                                n <= jfs_zstd_split_max() ? sl.sp : nullptr, ztot, c.ks);
         } else if (algo == JFS_ALGO_LZ4 && dir == DECOMPRESS && n <= split_max()) {
             std::vector<int32_t> lens(n), caps(n);
             int64_t nseg = 0, max_cap = 0, norg = 0;

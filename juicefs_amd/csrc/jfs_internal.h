@@ -33,11 +33,17 @@ int jfs_launch_lz4_encode_seg(const jfs_dev_block *d_blocks, int nblk, const int
 int jfs_launch_zstd_encode(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, hipStream_t stream);
 int jfs_launch_zstd_decode(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, uint8_t *d_scratch,
                            hipStream_t stream);
+// d_split: the small-batch path's scratch (jfs_zstd_split_bytes), or null;
+// tot: jfs_zstd_plan_host's six totals
 int jfs_launch_zstd_decode_planned(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *d_info,
-                                   uint8_t *d_lit, uint16_t *d_tabs, void *d_items, hipStream_t stream);
+                                   uint8_t *d_lit, uint16_t *d_tabs, void *d_items, void *d_split,
+                                   const uint64_t *tot, hipStream_t stream);
 size_t jfs_zstd_info_bytes(void);
+// totals[6]: items, literal bytes, table cells, blocks, origin entries, largest dst_cap
 void jfs_zstd_plan_host(const uint8_t *const *srcs, const int32_t *lens, const int32_t *caps, int nblk, void *info_out,
                         uint64_t *totals);
+int jfs_zstd_split_max(void);
+int64_t jfs_zstd_split_bytes(int nblk, const uint64_t *tot);
 int jfs_launch_crc32c(const jfs_dev_block *d_blocks, int nblk, int32_t seg_bytes, uint32_t *d_crc, int32_t *d_ret,
                       hipStream_t stream);
 int jfs_launch_crc32c_lens(const jfs_dev_block *d_blocks, int nblk, const int32_t *d_lens, const uint32_t *d_seeds,

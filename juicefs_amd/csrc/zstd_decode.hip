@@ -74,6 +74,8 @@ struct ZInfo {
     int32_t lit_err_code;
     uint32_t ovf;           // zplan: the scratch cannot hold this input (ret = E_SCRATCH)
     uint32_t n_sblk;        // zseqa: compressed blocks described (ZDesc after each table area)
+    uint32_t n_blk;         // zscan: blocks of every type (small-batch path: one record each)
+    int32_t cap;            // zscan: the input's dst_cap
 };
 constexpr int TAB_CELLS = 1280;  // u16 FSE cells per compressed block: LL 512, OF 256, ML 512
 constexpr int TAB_STRIDE = TAB_CELLS + 32;  // table area stride: the cells, then the block's ZDesc (64 B)
@@ -683,6 +685,8 @@ __host__ __device__ inline void zscan_one(const gc_u8 *src, int32_t n, int32_t c
     out.n_items = (uint32_t)(items + 1);
     out.lit_bytes = (uint32_t)(lits + 16);
     out.n_cblk = cblk;
+    out.n_blk = w.ordinal;
+    out.cap = cap;
 }
 
 __global__ void zscan_kernel(const jfs_dev_block *__restrict__ blocks, int nblk, ZInfo *__restrict__ info) {
@@ -702,7 +706,9 @@ __global__ __launch_bounds__(PLAN_T) void zplan_kernel(ZInfo *__restrict__ info,
                                                        uint64_t cap_lits, uint64_t cap_tabs,
                                                        uint64_t *__restrict__ need) {
     __shared__ uint64_t sh[3][PLAN_T];
+    __shared__ unsigned long long xb, xo, xm;  // small-batch path: blocks, origin entries, largest cap
     const int t = threadIdx.x;
+    if (t == 0) xb = xo = xm = 0;
     const int per = (nblk + PLAN_T - 1) / PLAN_T;
     const int b0 = t * per, b1 = b0 + per < nblk ? b0 + per : nblk;
     uint64_t a = 0, c = 0, d = 0;
@@ -711,6 +717,17 @@ __global__ __launch_bounds__(PLAN_T) void zplan_kernel(ZInfo *__restrict__ info,
         c += (info[i].lit_bytes + 15u) & ~15u;
         d += (uint64_t)info[i].n_cblk * TAB_STRIDE;
     }
+    uint64_t nbk = 0, norg = 0, mcap = 0;
+    for (int i = b0; i < b1; i++) {
+        const uint64_t c = info[i].cap > 0 ? (uint64_t)info[i].cap : 0u;
+        nbk += info[i].n_blk;
+        norg += (c + 3) & ~3ull;
+        mcap = c > mcap ? c : mcap;
+    }
+    __syncthreads();
+    if (nbk) atomicAdd(&xb, (unsigned long long)nbk);
+    if (norg) atomicAdd(&xo, (unsigned long long)norg);
+    if (mcap) atomicMax(&xm, (unsigned long long)mcap);
     sh[0][t] = a;
     sh[1][t] = c;
     sh[2][t] = d;
@@ -741,6 +758,9 @@ __global__ __launch_bounds__(PLAN_T) void zplan_kernel(ZInfo *__restrict__ info,
         need[0] = sh[0][t];
         need[1] = sh[1][t];
         need[2] = sh[2][t];
+        need[3] = xb;
+        need[4] = xo;
+        need[5] = xm;
     }
 }
 
@@ -2655,10 +2675,12 @@ __device__ __forceinline__ void x_run(XSmem &s, X &x, uint32_t n, uint32_t ll, u
 
 __global__ __launch_bounds__(64) void zexec_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
                                                    const ZInfo *__restrict__ info, const uint8_t *__restrict__ litbuf,
-                                                   const uint4 *__restrict__ items, int32_t *__restrict__ ret) {
+                                                   const uint4 *__restrict__ items, int32_t *__restrict__ ret,
+                                                   const int32_t *__restrict__ todo) {
     __shared__ XSmem s;
     const int bi = blockIdx.x;
     if (bi >= nblk) return;
+    if (todo && !todo[bi]) return;  // small-batch path: replayed by the origin map
     const int l = lane_id();
     const jfs_dev_block b = blocks[bi];
     const ZInfo zi = info[bi];
@@ -2767,6 +2789,8 @@ __global__ __launch_bounds__(64) void zexec_kernel(const jfs_dev_block *__restri
     if (l == 0) ret[bi] = result;
 }
 
+#include "zstd_split.inc"
+
 }  // namespace zstdd
 }  // namespace jfs
 
@@ -2789,6 +2813,9 @@ struct ZScratch {
     // the event that orders launches sharing this scratch on different streams
     uint64_t *d_need = nullptr, *h_need = nullptr;
     hipEvent_t ev_need = nullptr, ev_done = nullptr;
+    // small-batch path scratch (zstd_split.inc)
+    uint8_t *d_split = nullptr;
+    size_t split_cap = 0;
     std::mutex mu;
 };
 ZScratch g_scr[16];
@@ -2823,10 +2850,85 @@ int launch_entropy_exec(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret,
                        d_info, d_tabs, d_items, g_strict_reserved);
 #endif
     if (hipGetLastError() != hipSuccess) return -1;
-    hipLaunchKernelGGL(zexec_kernel, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, d_info, d_lit, d_items, d_ret);
+    hipLaunchKernelGGL(zexec_kernel, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, d_info, d_lit, d_items, d_ret,
+                       (const int32_t *)nullptr);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 }  // namespace
+
+namespace {
+// Batches of at most this many inputs take the small-batch path
+// (zstd_split.inc: one workgroup per block, origin-map replay);
+// JFS_ZSTD_SPLIT_MAX overrides (0 = never).
+int zsplit_max() {
+    static int v = [] {
+        const char *e = getenv("JFS_ZSTD_SPLIT_MAX");
+        return e ? std::max(0, atoi(e)) : 64;
+    }();
+    return v;
+}
+
+int64_t a256(int64_t x) { return (x + 255) & ~255ll; }
+
+// tot: the plan totals (zplan need[] / jfs_zstd_plan_host): [3] blocks,
+// [4] origin entries, [5] largest dst_cap
+int64_t split_bytes(int nblk, const uint64_t *tot) {
+    using namespace jfs::zstdd;
+    return a256((int64_t)nblk * (int64_t)sizeof(SIn)) + a256((int64_t)tot[3] * (int64_t)sizeof(SBlk)) +
+           a256((int64_t)nblk * 4) + a256((int64_t)tot[4] * 4) + 256;
+}
+
+int launch_split(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, jfs::zstdd::ZInfo *d_info, uint8_t *d_lit,
+                 uint4 *d_items, void *d_split, const uint64_t *tot, hipStream_t st) {
+    using namespace jfs::zstdd;
+    uint8_t *p = (uint8_t *)(((uintptr_t)d_split + 255) & ~(uintptr_t)255);
+    SScr sc;
+    sc.in = (SIn *)p;
+    p += a256((int64_t)nblk * (int64_t)sizeof(SIn));
+    sc.blk = (SBlk *)p;
+    p += a256((int64_t)tot[3] * (int64_t)sizeof(SBlk));
+    sc.todo = (int32_t *)p;
+    p += a256((int64_t)nblk * 4);
+    sc.org = (int32_t *)p;
+    const int64_t nbk = (int64_t)tot[3], max_cap = (int64_t)tot[5];
+    hipLaunchKernelGGL(zsplan_kernel, dim3(1), dim3(64), 0, st, d_info, nblk, sc);
+    hipLaunchKernelGGL(zswalk_kernel, dim3(nblk), dim3(64), 0, st, d_blocks, nblk, d_info, d_items, sc,
+                       g_strict_reserved);
+    if (nbk > 0)
+        hipLaunchKernelGGL(zsblk_kernel, dim3((unsigned)nbk), dim3(128), 0, st, d_blocks, nblk, d_info, d_lit, d_items,
+                           sc);
+    hipLaunchKernelGGL(zsfix_kernel, dim3(nblk), dim3(64), 0, st, d_blocks, nblk, d_info, d_items, sc);
+    if (nbk > 0)
+        hipLaunchKernelGGL(zsemit_kernel, dim3((unsigned)nbk), dim3(ST), 0, st, nblk, (const ZInfo *)d_info,
+                           (const uint4 *)d_items, sc);
+    const unsigned jx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((max_cap / 4 + ST) / ST, (2048 + nblk - 1) / nblk));
+    for (int r = 0; r < SJ_ROUNDS; r++) hipLaunchKernelGGL(zsjump_kernel, dim3(jx, (unsigned)nblk), dim3(ST), 0, st, sc, r);
+    hipLaunchKernelGGL(zsverd_kernel, dim3((nblk + 63) / 64), dim3(64), 0, st, nblk, sc, d_ret);
+    hipLaunchKernelGGL(zsgather_kernel, dim3((unsigned)((max_cap / 4 + ST) / ST), (unsigned)nblk), dim3(ST), 0, st,
+                       d_blocks, (const ZInfo *)d_info, (const uint8_t *)d_lit, sc);
+    hipLaunchKernelGGL(zexec_kernel, dim3(nblk), dim3(64), 0, st, d_blocks, nblk, (const ZInfo *)d_info,
+                       (const uint8_t *)d_lit, (const uint4 *)d_items, d_ret, (const int32_t *)sc.todo);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+}  // namespace
+
+extern "C" int jfs_zstd_split_max(void) { return zsplit_max(); }
+extern "C" int64_t jfs_zstd_split_bytes(int nblk, const uint64_t *tot) { return split_bytes(nblk, tot); }
+
+// Diagnostics: inputs the small-batch path replayed itself (out[0]) and
+// inputs it handed to the exact replay (out[1]) on the current device since
+// the last reset; synchronous.
+extern "C" int jfs_zstd_split_counts(uint64_t *out, int reset) {
+    unsigned long long v[2] = {0, 0};
+    if (hipMemcpyFromSymbol(v, HIP_SYMBOL(jfs::zstdd::g_zsplit_counts), sizeof(v)) != hipSuccess) return -1;
+    out[0] = v[0];
+    out[1] = v[1];
+    if (reset) {
+        unsigned long long z[2] = {0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(jfs::zstdd::g_zsplit_counts), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
 
 // Device API: zscan -> zplan -> entropy -> execute on `stream`.  The call
 // waits once on the host for zscan/zplan (the inputs' frame headers: a few
@@ -2843,11 +2945,11 @@ extern "C" int jfs_launch_zstd_decode(const jfs_dev_block *d_blocks, int nblk, i
     ZScratch &z = g_scr[dev];
     std::lock_guard<std::mutex> lk(z.mu);
     if (!z.d_need) {
-        if (hipMalloc((void **)&z.d_need, 3 * sizeof(uint64_t)) != hipSuccess) return -1;
-        if (hipHostMalloc((void **)&z.h_need, 3 * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess) return -1;
+        if (hipMalloc((void **)&z.d_need, 6 * sizeof(uint64_t)) != hipSuccess) return -1;
+        if (hipHostMalloc((void **)&z.h_need, 6 * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess) return -1;
         if (hipEventCreateWithFlags(&z.ev_need, hipEventDisableTiming) != hipSuccess) return -1;
         if (hipEventCreateWithFlags(&z.ev_done, hipEventDisableTiming) != hipSuccess) return -1;
-        z.h_need[0] = z.h_need[1] = z.h_need[2] = 0;
+        for (int i = 0; i < 6; i++) z.h_need[i] = 0;
     }
     if ((size_t)nblk > z.info_cap) {
         // earlier launches (any stream) may still read the old scratch
@@ -2861,7 +2963,7 @@ extern "C" int jfs_launch_zstd_decode(const jfs_dev_block *d_blocks, int nblk, i
     hipLaunchKernelGGL(zplan_kernel, dim3(1), dim3(PLAN_T), 0, stream, z.d_info, nblk, (uint64_t)z.items_cap,
                        (uint64_t)z.lit_cap, (uint64_t)z.tabs_cap, z.d_need);
     if (hipGetLastError() != hipSuccess) return -1;
-    if (hipMemcpyAsync(z.h_need, z.d_need, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, stream) != hipSuccess)
+    if (hipMemcpyAsync(z.h_need, z.d_need, 6 * sizeof(uint64_t), hipMemcpyDeviceToHost, stream) != hipSuccess)
         return -1;
     if (hipEventRecord(z.ev_need, stream) != hipSuccess) return -1;
     if (hipEventSynchronize(z.ev_need) != hipSuccess) return -1;
@@ -2877,7 +2979,14 @@ extern "C" int jfs_launch_zstd_decode(const jfs_dev_block *d_blocks, int nblk, i
                            (uint64_t)z.lit_cap, (uint64_t)z.tabs_cap, z.d_need);
         if (hipGetLastError() != hipSuccess) return -1;
     }
-    if (launch_entropy_exec(d_blocks, nblk, d_ret, z.d_info, z.d_lit, z.d_tabs, z.d_items, stream) != 0) return -1;
+    if (nblk <= zsplit_max()) {
+        uint64_t tot[6];
+        for (int i = 0; i < 6; i++) tot[i] = z.h_need[i];
+        if (!grow_dev(&z.d_split, &z.split_cap, (size_t)split_bytes(nblk, tot))) return -1;
+        if (launch_split(d_blocks, nblk, d_ret, z.d_info, z.d_lit, z.d_items, z.d_split, tot, stream) != 0) return -1;
+    } else if (launch_entropy_exec(d_blocks, nblk, d_ret, z.d_info, z.d_lit, z.d_tabs, z.d_items, stream) != 0) {
+        return -1;
+    }
     return hipEventRecord(z.ev_done, stream) == hipSuccess ? 0 : -1;
 }
 
@@ -2885,20 +2994,25 @@ extern "C" int jfs_launch_zstd_decode(const jfs_dev_block *d_blocks, int nblk, i
 // from its host copy of the inputs (jfs_zstd_plan_host) and owns the scratch
 // (one per staging slot), so nothing is shared and nothing waits.
 extern "C" int jfs_launch_zstd_decode_planned(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *d_info,
-                                              uint8_t *d_lit, uint16_t *d_tabs, void *d_items, hipStream_t stream) {
+                                              uint8_t *d_lit, uint16_t *d_tabs, void *d_items, void *d_split,
+                                              const uint64_t *tot, hipStream_t stream) {
     if (nblk <= 0) return 0;
+    if (d_split && nblk <= zsplit_max())
+        return launch_split(d_blocks, nblk, d_ret, (jfs::zstdd::ZInfo *)d_info, d_lit, (uint4 *)d_items, d_split, tot,
+                            stream);
     return launch_entropy_exec(d_blocks, nblk, d_ret, (jfs::zstdd::ZInfo *)d_info, d_lit, d_tabs, (uint4 *)d_items,
                                stream);
 }
 
-// Host plan of a batch: info[i] (ZInfo, 48 bytes each) from the host copy of
-// input i; returns the scratch totals (items, literal bytes, table cells).
+// Host plan of a batch: info[i] (ZInfo, 64 bytes each) from the host copy of
+// input i; returns the scratch totals (items, literal bytes, table cells) and
+// the small-batch path's (blocks, origin entries, largest dst_cap).
 extern "C" size_t jfs_zstd_info_bytes(void) { return sizeof(jfs::zstdd::ZInfo); }
 extern "C" void jfs_zstd_plan_host(const uint8_t *const *srcs, const int32_t *lens, const int32_t *caps, int nblk,
                                    void *info_out, uint64_t *totals) {
     using namespace jfs::zstdd;
     ZInfo *info = (ZInfo *)info_out;
-    uint64_t oi = 0, ol = 0, ot = 0;
+    uint64_t oi = 0, ol = 0, ot = 0, ob = 0, oo = 0, mc = 0;
     for (int i = 0; i < nblk; i++) {
         ZInfo &z = info[i];
         z = ZInfo{};
@@ -2912,10 +3026,17 @@ extern "C" void jfs_zstd_plan_host(const uint8_t *const *srcs, const int32_t *le
         oi += z.n_items;
         ol += (z.lit_bytes + 15u) & ~15u;
         ot += (uint64_t)z.n_cblk * TAB_STRIDE;
+        const uint64_t c = caps[i] > 0 ? (uint64_t)caps[i] : 0u;
+        ob += z.n_blk;
+        oo += (c + 3) & ~3ull;
+        mc = std::max(mc, c);
     }
     totals[0] = oi + 64;
     totals[1] = ol + 4096 + 64;
     totals[2] = ot + 64;
+    totals[3] = ob;
+    totals[4] = oo;
+    totals[5] = mc;
 }
 
 #ifdef JFS_PROF

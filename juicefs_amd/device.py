@@ -72,6 +72,14 @@ def lz4_split_counts(reset: bool = False):
     return tuple(int(x) for x in out)
 
 
+def zstd_split_counts(reset: bool = False):
+    """(inputs the Zstd small-batch path replayed itself, inputs it handed to
+    the exact one-wave replay) on the current device."""
+    out = (ctypes.c_uint64 * 2)()
+    _check(L.load().jfs_zstd_split_counts(out, 1 if reset else 0), "jfs_zstd_split_counts")
+    return tuple(int(x) for x in out)
+
+
 def lz4_compress_small(desc: torch.Tensor, ret: torch.Tensor, src_lens, stream=None):
     """jfs_lz4_compress_device_small: few blocks, each parsed as segments
     across the GPU (same bytes as lz4_compress); src_lens = host copies."""
