@@ -221,7 +221,7 @@ int jfs_lz4_eseg_counts(uint64_t *out, int reset);
  * than dst_cap ("Destination buffer is too small"), -3 src size incorrect
  * (truncated / trailing bytes). */
 int64_t jfs_zstd_decompress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream);
-/* Batches of at most JFS_ZSTD_SPLIT_MAX inputs (default 64; also the batch
+/* Batches of at most JFS_ZSTD_SPLIT_MAX inputs (default 128; also the batch
  * ABI's staged chunks and jfs_decompress) decode one workgroup per Zstd block
  * with an origin-map replay; an input outside that path's proven cases (not
  * exactly one frame, a checksum, any error) is replayed by the exact one-wave

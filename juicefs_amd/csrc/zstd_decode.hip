@@ -2863,7 +2863,7 @@ namespace {
 int zsplit_max() {
     static int v = [] {
         const char *e = getenv("JFS_ZSTD_SPLIT_MAX");
-        return e ? std::max(0, atoi(e)) : 64;
+        return e ? std::max(0, atoi(e)) : 128;
     }();
     return v;
 }

@@ -136,13 +136,13 @@ def test_split_level1_cases_roundtrip(gpu):
 
 def test_split_matches_exact_path(gpu, golden, frames_bin):
     """The same frames through the small-batch path (batch of 8) and the
-    one-wave path (batch of 80 > JFS_ZSTD_SPLIT_MAX's default 64): identical
+    one-wave path (batch of 160 > JFS_ZSTD_SPLIT_MAX's default 128): identical
     results."""
     ents = [f for f in golden["zstd"]["frames"] if f["size"] >= 100000][:8]
     srcs = [frames_bin[f["off"]:f["off"] + f["csize"]] for f in ents]
     caps = [f["size"] for f in ents]
     r1, o1 = run_device(srcs, caps, gpu)
-    k = (80 + len(srcs) - 1) // len(srcs)
+    k = (160 + len(srcs) - 1) // len(srcs)
     r2, o2 = run_device(srcs * k, caps * k, gpu)
     assert r1 == r2[:len(srcs)] and o1 == o2[:len(srcs)]
     for f, x, o in zip(ents, r1, o1):
