@@ -453,6 +453,17 @@ int64_t chunk_limit() {
     return v;
 }
 
+// Decode chunk ramp (run_batch): the number of small first chunks (32, 64,
+// 128, then 128 blocks); JFS_HOST_RAMP overrides (0 = off).
+int host_ramp_len() {
+    static int v = [] {
+        const char *e = getenv("JFS_HOST_RAMP");
+        return e ? std::max(0, atoi(e)) : 3;
+    }();
+    return v;
+}
+bool host_ramp() { return host_ramp_len() > 0; }
+
 // LZ4 compress chunks: the serial-parse encoder holds 8 blocks per CU and a
 // launch lasts one block's parse (~0.5 s) whatever its size, so a 2 GiB chunk
 // (256 blocks at ~8 MiB staged each) fills an eighth of the GPU; 4 GiB chunks
@@ -675,13 +686,27 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
     std::vector<Chunk> ch;
     {
         const int64_t limit = algo == JFS_ALGO_LZ4 && dir == COMPRESS && !ae ? chunk_limit_lz4c() : chunk_limit();
+        // Decode ramp: the first output cannot leave before chunk 0's H2D and
+        // kernel are done, and the one-workgroup-per-block kernels take a
+        // block's whole latency (~20 ms) whatever the chunk size; so a long
+        // decode starts with chunks of 32, 64 and 128 blocks (the small-batch
+        // kernels) that put the D2H stream to work while the first full chunk
+        // is staged and decoded, and ends with a chunk of at most 128 blocks
+        // so that little copy-out is left after the last D2H.  Measured on
+        // 2,048 x 4 MiB LZ4 (scripts/hostpath.py): no ramp 34.9-36.5 GiB/s,
+        // 3 ramp chunks 39.7-40.0, 5: 37.5, 7: 36.5.
+        int64_t total = 0;
+        for (int i = 0; i < nblk; i++) total += staged_bytes(algo, dir, iov[i]);
+        const bool ramp = dir == DECOMPRESS && !ae && max_chunk_blocks <= 0 && total > 2 * limit && host_ramp();
         int s = 0;
         while (s < nblk) {
             Chunk c{s, s, (int)(ch.size() % NSLOT), 0, 0, kstream((int)ch.size())};
+            const int k = (int)ch.size();
+            const int cap_blocks = ramp && k < host_ramp_len() ? std::min(32 << k, 128) : max_chunk_blocks;
             while (c.e < nblk) {
                 const int64_t ci = ae ? iov[c.e].dst_cap : staged_cap(algo, dir, iov[c.e]);
                 const int64_t ib = align16(iov[c.e].src_len), ob = align16(ci);  // = staged_bytes()
-                if (c.e > s && (c.tin + c.tout + ib + ob > limit || (max_chunk_blocks > 0 && c.e - s >= max_chunk_blocks)))
+                if (c.e > s && (c.tin + c.tout + ib + ob > limit || (cap_blocks > 0 && c.e - s >= cap_blocks)))
                     break;
                 cap[c.e] = ci;
                 in_off[c.e] = c.tin;
@@ -692,6 +717,26 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
             }
             ch.push_back(c);
             s = c.e;
+        }
+        if (ramp && ch.size() > 4 && ch.back().e - ch.back().s > 128) {  // ramp down: split the last chunk
+            Chunk &l = ch.back();
+            const int mid = l.e - 128;
+            Chunk t{mid, l.e, (int)(ch.size() % NSLOT), 0, 0, kstream((int)ch.size())};
+            l.e = mid;
+            l.tin = l.tout = 0;
+            for (int i = l.s; i < l.e; i++) {
+                in_off[i] = l.tin;
+                out_off[i] = l.tout;
+                l.tin += align16(iov[i].src_len);
+                l.tout += align16(cap[i]);
+            }
+            for (int i = t.s; i < t.e; i++) {
+                in_off[i] = t.tin;
+                out_off[i] = t.tout;
+                t.tin += align16(iov[i].src_len);
+                t.tout += align16(cap[i]);
+            }
+            ch.push_back(t);
         }
     }
     // Zstd decode: the per-input scratch plan (ZInfo) rides in the chunk
