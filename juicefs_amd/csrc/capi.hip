@@ -1026,7 +1026,7 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
             }
             jfs_zstd_plan_host(srcs.data(), lens.data(), caps.data(), n, h_zi, ztot);
             if (!sl.ensure_zstd(ztot)) return JFS_ERR_NO_MEMORY;
-            if (n <= jfs_zstd_split_max() && !sl.ensure_split(jfs_zstd_split_bytes(n, ztot))) return JFS_ERR_NO_MEMORY;
+            if (jfs_zstd_split_ok(n, ztot) && !sl.ensure_split(jfs_zstd_split_bytes(n, ztot))) return JFS_ERR_NO_MEMORY;
         }
         if (hipMemcpyAsync(d_in, h_in, (size_t)c.tin, hipMemcpyHostToDevice, dev->s_in) != hipSuccess) return JFS_ERR_HIP;
         if (hipMemcpyAsync(d_desc, h_desc, (size_t)n * sizeof(jfs_dev_block), hipMemcpyHostToDevice, dev->s_in) !=
@@ -1041,7 +1041,7 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
         int lk;
         if (zplan) {
             lk = jfs_launch_zstd_decode_planned(d_desc, n, d_ret, d_zi, sl.z_lit, sl.z_tabs, sl.z_items,
-                                                n <= jfs_zstd_split_max() ? sl.sp : nullptr, ztot, c.ks);
+                                                jfs_zstd_split_ok(n, ztot) ? sl.sp : nullptr, ztot, c.ks);
         } else if (algo == JFS_ALGO_LZ4 && dir == DECOMPRESS && n <= split_max()) {
             std::vector<int32_t> lens(n), caps(n);
             int64_t nseg = 0, max_cap = 0, norg = 0;

@@ -42,7 +42,7 @@ size_t jfs_zstd_info_bytes(void);
 // totals[6]: items, literal bytes, table cells, blocks, origin entries, largest dst_cap
 void jfs_zstd_plan_host(const uint8_t *const *srcs, const int32_t *lens, const int32_t *caps, int nblk, void *info_out,
                         uint64_t *totals);
-int jfs_zstd_split_max(void);
+int jfs_zstd_split_ok(int nblk, const uint64_t *tot);  // the small-batch path takes this batch
 int64_t jfs_zstd_split_bytes(int nblk, const uint64_t *tot);
 int jfs_launch_crc32c(const jfs_dev_block *d_blocks, int nblk, int32_t seg_bytes, uint32_t *d_crc, int32_t *d_ret,
                       hipStream_t stream);

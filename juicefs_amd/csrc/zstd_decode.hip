@@ -2870,6 +2870,13 @@ int zsplit_max() {
 
 int64_t a256(int64_t x) { return (x + 255) & ~255ll; }
 
+// The small-batch path's scratch grows with the blocks (one record each) and
+// the output capacity (one origin entry per byte): inputs made of very many
+// tiny blocks, or huge capacities, take the one-wave path instead.
+bool split_ok(int nblk, const uint64_t *tot) {
+    return nblk <= zsplit_max() && tot[3] <= (uint64_t)nblk * 512 + 4096 && tot[4] <= (1ull << 30);
+}
+
 // tot: the plan totals (zplan need[] / jfs_zstd_plan_host): [3] blocks,
 // [4] origin entries, [5] largest dst_cap
 int64_t split_bytes(int nblk, const uint64_t *tot) {
@@ -2912,7 +2919,7 @@ int launch_split(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, jfs::z
 }
 }  // namespace
 
-extern "C" int jfs_zstd_split_max(void) { return zsplit_max(); }
+extern "C" int jfs_zstd_split_ok(int nblk, const uint64_t *tot) { return split_ok(nblk, tot) ? 1 : 0; }
 extern "C" int64_t jfs_zstd_split_bytes(int nblk, const uint64_t *tot) { return split_bytes(nblk, tot); }
 
 // Diagnostics: inputs the small-batch path replayed itself (out[0]) and
@@ -2979,9 +2986,9 @@ extern "C" int jfs_launch_zstd_decode(const jfs_dev_block *d_blocks, int nblk, i
                            (uint64_t)z.lit_cap, (uint64_t)z.tabs_cap, z.d_need);
         if (hipGetLastError() != hipSuccess) return -1;
     }
-    if (nblk <= zsplit_max()) {
-        uint64_t tot[6];
-        for (int i = 0; i < 6; i++) tot[i] = z.h_need[i];
+    uint64_t tot[6];
+    for (int i = 0; i < 6; i++) tot[i] = z.h_need[i];
+    if (split_ok(nblk, tot)) {
         if (!grow_dev(&z.d_split, &z.split_cap, (size_t)split_bytes(nblk, tot))) return -1;
         if (launch_split(d_blocks, nblk, d_ret, z.d_info, z.d_lit, z.d_items, z.d_split, tot, stream) != 0) return -1;
     } else if (launch_entropy_exec(d_blocks, nblk, d_ret, z.d_info, z.d_lit, z.d_tabs, z.d_items, stream) != 0) {
@@ -2997,7 +3004,7 @@ extern "C" int jfs_launch_zstd_decode_planned(const jfs_dev_block *d_blocks, int
                                               uint8_t *d_lit, uint16_t *d_tabs, void *d_items, void *d_split,
                                               const uint64_t *tot, hipStream_t stream) {
     if (nblk <= 0) return 0;
-    if (d_split && nblk <= zsplit_max())
+    if (d_split && split_ok(nblk, tot))
         return launch_split(d_blocks, nblk, d_ret, (jfs::zstdd::ZInfo *)d_info, d_lit, (uint4 *)d_items, d_split, tot,
                             stream);
     return launch_entropy_exec(d_blocks, nblk, d_ret, (jfs::zstdd::ZInfo *)d_info, d_lit, d_tabs, (uint4 *)d_items,

@@ -177,3 +177,20 @@ def test_split_one_call_lone_latency(gpu, golden, frames_bin):
         lat[name] = round(statistics.median(ts[2:]) * 1e3, 2)
     print("lone 4 MiB zstd decode p50 ms:", lat)
     assert lat and all(v < 40 for v in lat.values()), lat
+
+
+def test_split_declines_block_heavy_inputs(gpu, oracle):
+    """An input of thousands of tiny blocks (here 5,000 empty raw blocks
+    before the data) would need a record per block: the batch takes the
+    one-wave path instead (the split counters do not move), same result."""
+    import struct
+    data = bytes(range(100))
+    frame = struct.pack("<I", 0xFD2FB528) + bytes([0x00, 0x00])  # no FCS, window 1 KiB
+    frame += b"\x00\x00\x00" * 5000  # empty raw blocks
+    frame += (1 | (len(data) << 3)).to_bytes(3, "little") + data
+    want, wo = oracle.zstd_decompress(frame, 1000)
+    assert want == len(data) and wo == data
+    D.zstd_split_counts(reset=True)
+    r, outs = run_device([frame], [1000], gpu)
+    assert r[0] == want and outs[0] == data
+    assert D.zstd_split_counts() == (0, 0)
