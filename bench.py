@@ -623,7 +623,7 @@ def timed_launches(fn, steps, warmup, S, world, dev):
 def configs3_zstd(a, S, world, rank, dev):
     """BASELINE configs[3]: Zstd level-3 decode of 4096 x 4 MiB frames in HBM."""
     from juicefs_amd import device as D
-    zb = D.ZstdBatch(a.blocks, a.block_bytes, a.cls, level=a.level, distinct=16, seed_base=S.seed_base(rank, 16),
+    zb = D.ZstdBatch(a.blocks, a.block_bytes, a.cls, level=a.level, distinct=256, seed_base=S.seed_base(rank, 256),
                      device=dev)
     el, kms = timed_launches(zb.decompress, a.zstd_steps, 1, S, world, dev)
     if not S.all_ranks_ok(zb.verify(), world, dev):
@@ -781,7 +781,7 @@ def main():
     if a.codec == "lz4":
         batch = D.Lz4Batch(nblk, U, a.cls, seed_base=S.seed_base(rank, nblk), device=dev)
     else:
-        batch = D.ZstdBatch(nblk, U, a.cls, level=a.level, distinct=16, seed_base=S.seed_base(rank, 16), device=dev)
+        batch = D.ZstdBatch(nblk, U, a.cls, level=a.level, distinct=256, seed_base=S.seed_base(rank, 256), device=dev)
     C = batch.comp_bytes
     setup_s = time.perf_counter() - t_setup
 

@@ -12,7 +12,7 @@ codec = sys.argv[4] if len(sys.argv) > 4 else "lz4"
 if codec == "lz4":
     b = D.Lz4Batch(nblk, 4 << 20, cls, seed_base=1)
 else:
-    b = D.ZstdBatch(nblk, 4 << 20, cls, level=3, distinct=16, seed_base=1,
+    b = D.ZstdBatch(nblk, 4 << 20, cls, level=3, distinct=256, seed_base=1,
                     cache_dir=os.path.join(ROOT, "gpurun_out", "frames"))
 if k == 0:  # generate the frame cache only (no GPU work)
     print("cached"); sys.exit(0)
