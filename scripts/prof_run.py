@@ -13,7 +13,7 @@ if codec == "lz4":
     b = D.Lz4Batch(nblk, 4 << 20, cls, seed_base=1)
 else:
     b = D.ZstdBatch(nblk, 4 << 20, cls, level=3, distinct=256, seed_base=1,
-                    cache_dir=os.path.join(ROOT, "gpurun_out", "frames"))
+                    cache_dir=os.path.join(os.environ.get("TMPDIR", "/tmp"), "jfs_frames"))
 if k == 0:  # generate the frame cache only (no GPU work)
     print("cached"); sys.exit(0)
 import time

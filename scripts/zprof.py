@@ -8,7 +8,7 @@ from juicefs_amd import _lib, device as D
 lib = _lib.load()
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 b = D.ZstdBatch(n, 4 << 20, "T", level=3, distinct=16, seed_base=1,
-                cache_dir=os.path.join(ROOT, "gpurun_out", "frames"))
+                cache_dir=os.path.join(os.environ.get("TMPDIR", "/tmp"), "jfs_frames"))
 b.decompress(); torch.cuda.synchronize()
 lib.jfs_zprof_reset()
 b.decompress(); torch.cuda.synchronize()
