@@ -1149,6 +1149,9 @@ struct ASmem {  // zseqa: table-build scratch
     int16_t norm[64];
     uint8_t symat[512], mark[512], ksym[512];
 };
+#ifndef JFS_ZSEQ_AB
+#define JFS_ZSEQ_AB 1  // decoder: serial state pass + lane-parallel value pass per period
+#endif
 struct SeqSmem {  // zseqb
     alignas(16) uint8_t bring[ZNB][ZRB2 + 16];   // per-lane bitstream rings (+ a mirror of block slot 0)
     alignas(16) uint16_t arena[ZNB][TAB_CELLS];  // the group's tables (LL 0, OF 512, ML 768)
@@ -1157,6 +1160,12 @@ struct SeqSmem {  // zseqb
     int32_t pos[2][ZNB];  // decoder bit positions published at each period's barrier
     int32_t more[2];      // any lane still decoding (per period parity)
     int32_t cmd;          // wave 0 -> wave 1: blocks in the group, 0 = done
+#if JFS_ZSEQ_AB
+    uint2 rec[2][ZK2][ZNB];    // a period's sequences (period parity): bit position, states (sll | sof << 10 | sml << 20)
+    uint32_t carry[3][ZNB];    // repeat offsets after the block's sequences so far (symbolic in its entry state)
+    int32_t rcnt[2][ZNB];      // sequences recorded in the period
+    uint32_t ibase[2][ZNB];    // sequence index of the period's first record
+#endif
 };
 static_assert(sizeof(SeqSmem) * (ZNB <= 12 ? 4 : 3) <= 160 * 1024, "sequence workgroups per CU (one decoder wave per SIMD)");
 static_assert(ZMQ == 4, "the mover serves each block with four lanes (stride-4 block loads)");
@@ -1702,6 +1711,9 @@ __device__ __forceinline__ uint64_t zw_shift(uint64_t hi, uint32_t lo, int32_t c
     return c ? (hi << c) | (((uint64_t)lo << 32) >> (64 - c)) : hi;
 }
 
+#if JFS_ZSEQ_AB
+__device__ __forceinline__ void zvalues(SeqSmem &sm, int gn, int b);
+#endif
 // Wave 1: stage the group's tables (built in HBM by zseqa) into the arena,
 // prefill the rings, then one refill round per period until the decoder
 // reports no lane running.
@@ -1771,11 +1783,15 @@ __device__ __forceinline__ void zmover(SeqSmem &sm, int gn, const gc_u16 *tabs) 
     for (int d = 0; d < ZMD; ++d)
 #pragma unroll
         for (int i = 0; i < 2; ++i) { pend_k[d][i] = 0; pend_v[d][i] = make_uint4(0, 0, 0, 0); pend_on[d][i] = false; }
-    for (int p = 0;; ++p) {
+    int p = 0;
+    for (;; ++p) {
         // land the blocks loaded ZMD periods ago
 #pragma unroll
         for (int i = 0; i < 2; ++i)
             if (pend_on[0][i]) zr_put(ring, pend_k[0][i], zclip(pend_v[0][i], pend_k[0][i], g.m));
+#if JFS_ZSEQ_AB
+        if (p > 0) zvalues(sm, gn, (p - 1) & 1);  // the decoder's previous period
+#endif
 #pragma unroll
         for (int d = 0; d + 1 < ZMD; ++d)
 #pragma unroll
@@ -1799,8 +1815,200 @@ __device__ __forceinline__ void zmover(SeqSmem &sm, int gn, const gc_u16 *tabs) 
         zsync();
         if (!sm.more[p & 1]) break;
     }
+#if JFS_ZSEQ_AB
+    zvalues(sm, gn, p & 1);  // the last period
+    zsync();
+#endif
 }
 
+#if JFS_ZSEQ_AB
+// Phase B for the group (lane = block), tables and bitstreams in LDS, in two
+// passes per period.  The STATE pass (wave 0, the decoder) is the serial part:
+// per lane and sequence three cells, two extra-bit lookups and one bitstream
+// window, only the FSE state updates and the bit position (recorded in LDS,
+// double-buffered by period parity).  The VALUE pass (wave 1, the mover, one
+// period behind) runs on all 64 lanes over a period's records (lane = block +
+// 16 x record): extra bits -> lengths and offset value, and the repeat-offset
+// updates as per-sequence transforms of (rep0, rep1, rep2) composed by a
+// segmented prefix over the lanes of the same block (terms: constants or
+// SYMB | j << 29 | d = max(1, rep_j - d), see rep_res); every block carries
+// its composition across periods.  The records of period p-1 lie at most one
+// 16-byte block above the position published at the end of period p-2, and
+// the blocks the mover lands in period p were targeted from the position
+// published at the end of period p-3: they evict ring slots >= 5 blocks
+// above it, so the value pass still finds every record's bytes.
+__device__ __forceinline__ uint32_t zsub(uint32_t x, uint32_t a0, uint32_t a1, uint32_t a2) {
+    if (!(x & SYMB)) return x;
+    const uint32_t j = (x >> 29) & 3u, dd = x & 0x1FFFFFFFu;
+    const uint32_t y = j == 0 ? a0 : j == 1 ? a1 : a2;
+    if (y & SYMB) return y + dd;
+    return y > dd ? y - dd : 1u;
+}
+__device__ __forceinline__ void zvalues(SeqSmem &sm, int gn, int b) {
+    const int l = lane_id();
+    const int j = l & (ZNB - 1);
+    static_assert(ZNB == 16 && ZK2 == 8, "value pass layout: 16 blocks x 4 records per round, two rounds");
+    const bool blk = j < gn;
+    const GBlk &d = sm.g[blk ? j : 0];
+    const uint16_t *tl = sm.arena[j], *to = tl + 512, *tm = tl + 768;
+    const uint8_t *ring = sm.bring[j];
+    const int32_t cntj = blk ? sm.rcnt[b][j] : 0;
+    const uint32_t ib0 = sm.ibase[b][j];
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+        const int kk = half * 4 + (l >> 4);
+        const bool on = blk && kk < cntj;
+        uint32_t ll = 0, ml = 0, ofv = 4;
+        if (on) {
+            const uint2 r = sm.rec[b][kk][j];
+            const uint32_t cl = tl[r.y & 1023u], co = to[(r.y >> 10) & 1023u], cm = tm[r.y >> 20];
+            uint64_t hi;
+            uint32_t lo;
+            zw_fill(ring, (int32_t)r.x, hi, lo);
+            const uint32_t lv = sm.lut_ll[cl & 63], mv = sm.lut_ml[cm & 63], ofc = co & 63;
+            int32_t c = 0;
+            ofv = (1u << ofc) + zw_get(hi, c, ofc);
+            ml = (mv & 0xFFFFFFu) + zw_get(hi, c, mv >> 24);
+            ll = (lv & 0xFFFFFFu) + zw_get(hi, c, lv >> 24);
+        }
+        const uint32_t I0 = SYMB, I1 = SYMB | (1u << 29), I2 = SYMB | (2u << 29);
+        uint32_t t0 = I0, t1 = I1, t2 = I2;
+        if (on) {
+            if (ofv > 3) {
+                t0 = ofv - 3; t1 = I0; t2 = I1;
+            } else {
+                const uint32_t k = ofv - 1 + (ll == 0 ? 1u : 0u);
+                if (k == 1) { t0 = I1; t1 = I0; }
+                else if (k == 2) { t0 = I2; t1 = I0; t2 = I1; }
+                else if (k == 3) { t0 = I0 + 1u; t1 = I0; t2 = I1; }
+            }
+        }
+#pragma unroll
+        for (int sft = 16; sft < 64; sft <<= 1) {  // prefix over the block's lanes (j, j + 16, ...)
+            const uint32_t a0 = (uint32_t)__shfl_up((int)t0, sft, 64), a1 = (uint32_t)__shfl_up((int)t1, sft, 64),
+                           a2 = (uint32_t)__shfl_up((int)t2, sft, 64);
+            if (l >= sft) {
+                const uint32_t n0 = zsub(t0, a0, a1, a2), n1 = zsub(t1, a0, a1, a2), n2 = zsub(t2, a0, a1, a2);
+                t0 = n0; t1 = n1; t2 = n2;
+            }
+        }
+        const uint32_t c0 = sm.carry[0][j], c1 = sm.carry[1][j], c2 = sm.carry[2][j];
+        if (on) d.ib[d.item + 2 + ib0 + (uint32_t)kk] = make_uint4(ll, ml, zsub(t0, c0, c1, c2), IT_SEQ);
+        const int nh = cntj - half * 4;  // records of this round for block j
+        __builtin_amdgcn_wave_barrier();
+        if (blk && nh > 0 && (l >> 4) == (nh < 4 ? nh : 4) - 1) {
+            const uint32_t n0 = zsub(t0, c0, c1, c2), n1 = zsub(t1, c0, c1, c2), n2 = zsub(t2, c0, c1, c2);
+            sm.carry[0][j] = n0; sm.carry[1][j] = n1; sm.carry[2][j] = n2;
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+__device__ __forceinline__ void zdecode(SeqSmem &sm, int gn, uint32_t &r0, uint32_t &r1, uint32_t &r2,
+                                        uint32_t &brep) {
+    const int l = lane_id();
+    const bool mine = l < gn;
+    const GBlk d = sm.g[mine ? l : 0];
+    const ZGeo g = zgeo(d);
+    const uint8_t *ring = sm.bring[l < ZNB ? l : 0];
+    const uint16_t *tl = sm.arena[l < ZNB ? l : 0], *to = tl + 512, *tm = tl + 768;
+    const int32_t all = d.al & 0xFF, alof = (d.al >> 8) & 0xFF, alml = (d.al >> 16) & 0xFF;
+    const int32_t m8 = 8 * g.m;
+    g_u4 *it = d.ib + d.item;
+    if (l < ZNB) {
+        sm.carry[0][l] = SYMB;
+        sm.carry[1][l] = SYMB | (1u << 29);
+        sm.carry[2][l] = SYMB | (2u << 29);
+    }
+    zsync();  // the mover has staged the tables and prefilled the rings
+    [[maybe_unused]] uint64_t zt = ZP_NOW();
+    bool run = false;
+    int32_t left = 0, i = 0;
+    uint32_t sll = 0, sof = 0, sml = 0;
+    if (mine) {
+        if (d.nseq == 0) {
+            it[1] = make_uint4(0, 0, 0, IT_BREP);
+            it[2] = make_uint4(0, 0, 0, IT_BEND);
+            brep = 1;
+        } else {
+            const uint32_t last = d.bsz > 0 ? ring[(g.top - 1) & (ZRB2 - 1)] : 0u;
+            if (last == 0) {
+                it[1] = make_uint4(0, 0, (uint32_t)E_CORRUPT, IT_ERR);
+            } else {
+                brep = 1;
+                run = true;
+                left = 8 * (g.top - 1) + (31 - __builtin_clz(last));
+            }
+        }
+    }
+    if (run) {
+        uint64_t hi;
+        uint32_t lo;
+        zw_fill(ring, left, hi, lo);
+        int32_t c = 0;
+        sll = zw_get(hi, c, all);
+        sof = zw_get(hi, c, alof);
+        sml = zw_get(hi, c, alml);
+        left -= c;
+    }
+    const uint32_t szl = 1u << all, szo = 1u << alof, szm = 1u << alml;
+    const uint32_t kl31 = (uint32_t)all - 31u, ko31 = (uint32_t)alof - 31u, km31 = (uint32_t)alml - 31u;
+    for (int p = 0;; ++p) {
+        const int32_t i0 = i;
+#pragma unroll
+        for (int k = 0; k < ZK2; ++k) {
+            if (run) {
+                if (left < m8) {  // overflow
+                    it[2 + i] = make_uint4(0, 0, (uint32_t)E_CORRUPT, IT_ERR);
+                    run = false;
+                } else {
+                    const uint32_t cl = tl[sll], co = to[sof], cm = tm[sml];
+                    uint64_t hi;
+                    uint32_t lo;
+                    zw_fill(ring, left, hi, lo);
+                    sm.rec[p & 1][k][l] = make_uint2((uint32_t)left, sll | (sof << 10) | (sml << 20));
+                    const int32_t c = (int32_t)((sm.lut_ll[cl & 63] >> 24) + (sm.lut_ml[cm & 63] >> 24) + (co & 63));
+                    int32_t c2 = 0;
+                    if (i + 1 < d.nseq) {
+                        const uint64_t h2 = zw_shift(hi, lo, c);
+                        const uint32_t nsl = cl >> 6, nso = co >> 6, nsm = cm >> 6;
+                        const uint32_t nbl = kl31 + (uint32_t)__builtin_clz(nsl);
+                        const uint32_t nbm = km31 + (uint32_t)__builtin_clz(nsm);
+                        const uint32_t nbo = ko31 + (uint32_t)__builtin_clz(nso);
+                        sll = ((nsl << nbl) - szl) + zw_get(h2, c2, nbl);
+                        sml = ((nsm << nbm) - szm) + zw_get(h2, c2, nbm);
+                        sof = ((nso << nbo) - szo) + zw_get(h2, c2, nbo);
+                    }
+                    left -= c + c2;
+                    ++i;
+                    if (i == d.nseq) {
+                        it[2 + i] = left == m8 ? make_uint4(0, 0, 0, IT_BEND) : make_uint4(0, 0, (uint32_t)E_CORRUPT, IT_ERR);
+                        run = false;
+                    }
+                }
+            }
+        }
+        if (l < ZNB) {
+            sm.rcnt[p & 1][l] = i - i0;
+            sm.ibase[p & 1][l] = (uint32_t)i0;
+            sm.pos[p & 1][l] = left;
+        }
+        const bool any = __ballot(run) != 0;
+        if (l == 0) sm.more[p & 1] = any ? 1 : 0;
+        [[maybe_unused]] const uint64_t tw = ZP_NOW();
+        zsync();  // the mover takes this period's records (value pass) during the next
+        ZS_ADD(4, ZP_NOW() - tw);
+        if (!any) break;
+    }
+    zsync();  // the mover's value pass of the last period
+    if (l < ZNB) {
+        r0 = sm.carry[0][l];
+        r1 = sm.carry[1][l];
+        r2 = sm.carry[2][l];
+    }
+    { const uint64_t t = ZP_NOW(); ZS_ADD(2, t - zt); }
+}
+#else
 // Wave 0: phase B for the group (lane = block), tables and bitstreams in LDS.
 __device__ __forceinline__ void zdecode(SeqSmem &sm, int gn, uint32_t &r0, uint32_t &r1, uint32_t &r2,
                                         uint32_t &brep) {
@@ -1939,6 +2147,8 @@ __device__ __forceinline__ void zdecode(SeqSmem &sm, int gn, uint32_t &r0, uint3
     }
     { const uint64_t t = ZP_NOW(); ZS_ADD(2, t - zt); }
 }
+
+#endif  // JFS_ZSEQ_AB
 
 // phases B (both waves) and C (wave 0) for the collected group
 __device__ __forceinline__ void seq_group2(SeqSmem &sm, int gn, uint32_t *e0, uint32_t *e1, uint32_t *e2) {

@@ -66,6 +66,20 @@ def test_zstd_frames_vs_golden(gpu, golden, frames_bin):
         assert x == f["size"] and sha(o) == f["src_sha"], (f.get("name"), f["cls"], f.get("level"), f["size"], x)
 
 
+def test_zstd_frames_one_wave_path(gpu, golden, frames_bin):
+    """The golden frames in one batch larger than JFS_ZSTD_SPLIT_MAX (128):
+    the one-wave-per-input kernels (zlit / zseqa / zseqb / zexec) decode them
+    (smaller batches take zstd_split.inc, tests/test_zstd_split_gpu.py)."""
+    ents = golden["zstd"]["frames"] + golden["zstd"]["special"]
+    srcs = [frames_bin[f["off"]:f["off"] + f["csize"]] for f in ents]
+    caps = [f["size"] for f in ents]
+    k = 129 // len(srcs) + 1
+    r, outs = run_device(srcs * k, caps * k, gpu, src_mis=2, dst_mis=5)
+    assert len(r) > 128
+    for f, x, o in zip(ents * k, r, outs):
+        assert x == f["size"] and sha(o) == f["src_sha"], (f.get("name"), f["cls"], f.get("level"), f["size"], x)
+
+
 def test_zstd_frames_unaligned_and_short(gpu, golden, frames_bin, oracle):
     ents = [f for f in golden["zstd"]["frames"] if f["size"] <= 300000]
     srcs = [frames_bin[f["off"]:f["off"] + f["csize"]] for f in ents]
