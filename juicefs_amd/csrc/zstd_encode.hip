@@ -368,6 +368,302 @@ __device__ bool all_equal(const Src &S, int32_t a, int32_t b) {
 // ---------------------------------------------------------------------------
 // kernel 1: the parse (one wave per frame)
 // ---------------------------------------------------------------------------
+// One block of ZSTD_compressBlock_fast_generic (+ the block decisions the
+// parse must predict), on the wave's LDS table T; off1 / off2 = the repeat
+// offsets handed in (updated as the serial loop passes them on).
+template <bool WIDE>
+__device__ __forceinline__ void parse_block(const FInfo &F, BInfo &B, int32_t k, Tab<WIDE> &T, const Src &S,
+                            uint64_t *__restrict__ seqs, uint32_t &off1, uint32_t &off2) {
+    const int l = lane_id();
+    const uint32_t hlog = F.hlog, mls = F.mls, tsize = 1u << hlog;
+    const int32_t maxDist = 1 << F.wlog;
+    ZP_DECL
+    const int32_t bs = B.bs, be = B.be;
+    const uint32_t rin0 = off1, rin1 = off2;
+    if (be - bs < 7) {  // ZSTD_buildSeqStore: too small to compress, match state untouched
+        if (l == 0) {
+            B.ns = 0;
+            B.nl = be - bs;
+            B.rin0 = rin0; B.rin1 = rin1; B.rout0 = rin0; B.rout1 = rin1;
+            B.flags = F_NOCOMP;
+        }
+        return;
+    }
+    const bool rle = k > 0 && all_equal(S, bs, be);
+    const int32_t prefixPos = be > maxDist ? be - maxDist : 0;
+    const uint32_t prefixIdx = (uint32_t)prefixPos + 1, R = (uint32_t)be;
+    if (WIDE && prefixPos > 0) {  // entries that left the window: the window's lowest index
+        __syncthreads();
+        for (uint32_t h = l; h < tsize; h += 64)
+            if (T.get(h, R) <= prefixIdx) T.put(h, prefixIdx);
+        __syncthreads();
+    }
+    ZP(6);
+    ZPC(11);
+    // ---- ZSTD_compressBlock_fast_generic
+    uint64_t *sq = seqs + B.seq_off;
+    const int32_t ilimit = be - 8;
+    int32_t ip0 = bs, anchor = bs, ns = 0, nl = 0;
+    uint32_t o1 = off1, o2 = off2, saved = 0;
+    if (ip0 == prefixPos) ip0++;
+    {
+        const uint32_t maxRep = (uint32_t)(ip0 > maxDist ? maxDist : ip0);
+        if (o2 > maxRep) { saved = o2; o2 = 0; }
+        if (o1 > maxRep) { saved = o1; o1 = 0; }
+    }
+    // sequence records collect in a VGPR (lane i: record 64 g + i) and are
+    // stored 64 at a time: no store per sequence for later vmcnt waits to drain
+    uint64_t sbuf = 0;
+    auto emit = [&](uint32_t ll, uint32_t mlb, uint32_t ofv) {
+        const uint64_t r = seq_pack(ll, mlb, ofv);
+        if (l == (ns & 63)) sbuf = r;
+        if ((ns & 63) == 63) sq[ns - 63 + l] = sbuf;
+        ns++;
+    };
+    int pend = 0;  // 1: after a search match (insert ip0-2, then the repeat loop); 2: after a repeat-loop match
+    // windows of the last step whose positions were bp + 2 l (lanes [0, bvalid) valid)
+    uint4 Ap = make_uint4(0, 0, 0, 0);
+    int32_t bp = -1, bvalid = 0;
+    for (int guard = 0; guard < 4 * BLK; guard++) {
+        const bool pb = pend != 0;
+        const int32_t ipb = ip0;
+        // positions of this search step (after a match: ip0 + 2 l)
+        const int32_t q = pb ? ip0 + 2 * l : sched_pos(ip0, anchor, (uint32_t)l);
+        // windows A = bytes [q - 2, q + 14).  After a match they come from
+        // the previous step's lanes when those hold them (a cross-lane
+        // permute instead of a memory round trip); lanes without a source
+        // sit this step out
+        uint4 A = make_uint4(0, 0, 0, 0);
+        const bool use_sh = pb && bp >= 0 && ip0 - bp <= 2 * (bvalid - 2);
+        bool have = true;
+        if (use_sh) {
+            const int32_t e = (ip0 - bp) + 2 * l;
+            const int s0 = e >> 1;
+            const uint32_t dl = (uint32_t)e & 1u;
+            const int sa = s0 < 63 ? s0 : 63, sb = s0 + 1 < 63 ? s0 + 1 : 63;
+            const uint32_t x0 = (uint32_t)__shfl((int)Ap.x, sa, 64), x1 = (uint32_t)__shfl((int)Ap.y, sa, 64),
+                           x2 = (uint32_t)__shfl((int)Ap.z, sa, 64), x3 = (uint32_t)__shfl((int)Ap.w, sa, 64),
+                           y3 = (uint32_t)__shfl((int)Ap.w, sb, 64);
+            A = dl ? make_uint4(__builtin_amdgcn_alignbyte(x1, x0, 1), __builtin_amdgcn_alignbyte(x2, x1, 1),
+                                __builtin_amdgcn_alignbyte(x3, x2, 1), __builtin_amdgcn_alignbyte(y3 >> 16, x3, 1))
+                   : make_uint4(x0, x1, x2, x3);
+            have = s0 + (int)dl < bvalid;
+        }
+        const bool on = q + 1 < ilimit && (!pb || l < JFS_ZL1_PB) && have;
+        // (after a match every lane loads its window, on or not: the next
+        // step's windows then come from these)
+        const bool ld = !use_sh && (pb || on);
+        // AR = the same bytes o1 back (repeat check + its first extension
+        // bytes), R2 = (lane 0, after a match) 16 bytes at ip0 - 2 - o2 (the
+        // repeat loop): both awaited only where used
+        uint4 AR = make_uint4(0, 0, 0, 0), R2 = make_uint4(0, 0, 0, 0);
+        if (ld) A = ld128(S, q - 2);
+        if (on) AR = ld128(S, q - 2 - (int32_t)o1);
+        if (pb && l == 0) R2 = ld128(S, ip0 - 2 - (int32_t)o2);
+        const int32_t vcount = pb ? (int32_t)__builtin_popcountll(ballot(use_sh ? have : ld)) : 0;
+        const uint64_t v0 = (uint64_t)__builtin_amdgcn_alignbyte(A.y, A.x, 2) | ((uint64_t)__builtin_amdgcn_alignbyte(A.z, A.y, 2) << 32);
+        const uint64_t v1 = (uint64_t)__builtin_amdgcn_alignbyte(A.y, A.x, 3) | ((uint64_t)__builtin_amdgcn_alignbyte(A.z, A.y, 3) << 32);
+        const uint32_t val0 = (uint32_t)v0, val1 = (uint32_t)v1;
+        const uint32_t h0 = zhash(v0, hlog, mls), h1 = zhash(v1, hlog, mls);
+        ZP(0);
+        ZPC(9);
+        if (pend == 1) {  // hashTable[hash(ip0 - 2)] = ip0 - 2
+            const uint64_t vm2 = (uint64_t)A.x | ((uint64_t)A.y << 32);
+            const uint32_t hm2 = readlane(zhash(vm2, hlog, mls), 0);
+            if (l == 0) T.put(hm2, (uint32_t)(ip0 - 2 + 1));
+            lds_order();
+        }
+        // the repeat loop's check waits for R2: the search step's table
+        // reads and bucket tags go first (undone if the repeat loop fires)
+        const bool rchk = pb && o2 > 0 && ip0 <= ilimit;
+        pend = 0;
+        const uint64_t onm = ballot(on);
+        if (!onm && !rchk) break;  // ip1 >= ilimit: no more positions in this block
+        const int non = onm ? 64 - __builtin_clzll(onm) : 0;  // lanes [0, non) are on
+        // table reads (before any write of this step), then tags to find
+        // lanes sharing a bucket
+        uint32_t olo0 = 0, olo1 = 0, i0 = 0, i1 = 0;
+        if (on) {
+            olo0 = T.lo[h0];
+            olo1 = T.lo[h1];
+            i0 = T.get(h0, R);
+            i1 = T.get(h1, R);
+        }
+        lds_order();
+        if (on) {
+            T.lo[h0] = (uint16_t)l;
+            T.lo[h1] = (uint16_t)l;
+        }
+        lds_order();
+        uint32_t cm = 64;
+        if (on) {
+            const uint32_t t0 = T.lo[h0], t1 = T.lo[h1];
+            if (t0 != (uint32_t)l) cm = umin32((uint32_t)l, t0);
+            if (t1 != (uint32_t)l) cm = umin32(cm, umin32((uint32_t)l, t1));
+        }
+        const int cut = (int)dwave_min(cm) + 1;
+        const int nbt = cut < non ? cut : non;  // lanes [0, nbt) read exactly what the serial loop reads
+        const bool dec = l < nbt;
+        const bool c0 = dec && i0 > prefixIdx, c1 = dec && i1 > prefixIdx;
+        // candidates: bytes [cand - 2, cand + 14) (check + first extension bytes)
+        uint4 X0 = make_uint4(0, 0, 0, 0), X1 = make_uint4(0, 0, 0, 0);
+        if (c0) X0 = ld128(S, (int32_t)i0 - 3);
+        if (c1) X1 = ld128(S, (int32_t)i1 - 3);
+        ZP(2);
+        if (rchk) {
+            const uint4 a0 = readlane4(A, 0), r0 = readlane4(R2, 0);
+            const uint4 X = make_uint4(a0.x ^ r0.x, a0.y ^ r0.y, a0.z ^ r0.z, a0.w ^ r0.w);
+            if (first_diff(X, 2) >= 4) {  // MEM_read32(ip0) == MEM_read32(ip0 - offset_2)
+                if (on) {  // the search step did not happen: its tags come off
+                    T.lo[h0] = (uint16_t)olo0;
+                    T.lo[h1] = (uint16_t)olo1;
+                }
+                lds_order();
+                // repeat-offset match at ip0 (offset_2), then swap
+                const int32_t flim = be - (ip0 + 4);
+                int32_t rl = (int32_t)umin32(first_diff(X, 6), (uint32_t)flim);
+                if (rl == 10 && rl < flim) {
+                    int32_t f2 = 0, b2 = 0;
+                    ext_counts(S, ip0 + 4 + rl, ip0 + 4 + rl - (int32_t)o2, flim - rl, 0, 0, 0, f2, b2);
+                    rl += f2;
+                }
+                rl += 4;
+                const uint32_t t = o2;
+                o2 = o1;
+                o1 = t;
+                if (l == 0) T.put(readlane(h0, 0), (uint32_t)(ip0 + 1));
+                lds_order();
+                emit(0, (uint32_t)(rl - 3), 1);
+                Ap = A;
+                bp = ipb;
+                bvalid = vcount;
+                ip0 += rl;
+                anchor = ip0;
+                if (ip0 <= ilimit) pend = 2;
+                ZP(1);
+                continue;
+            }
+        }
+        ZP(1);
+        if (!onm) break;
+        const bool rep = dec && o1 > 0 && AR.y == A.y;  // MEM_read32(ip2 - offset_1) == MEM_read32(ip2)
+        const bool k0 = c0 && __builtin_amdgcn_alignbyte(X0.y, X0.x, 2) == val0;
+        const bool k1 = c1 && __builtin_amdgcn_alignbyte(X1.y, X1.x, 2) == val1;
+        const int j = ctz64(ballot(rep || k0 || k1));
+        ZP(3);
+        // lanes after the first hit (and past the cut) put their buckets
+        // back; then the lanes up to the hit insert ip0 and ip1
+        lds_order();
+        if (on && (l >= nbt || l > j)) {
+            T.lo[h0] = (uint16_t)olo0;
+            T.lo[h1] = (uint16_t)olo1;
+        }
+        lds_order();
+        if (on && l < nbt && l <= j) {
+            T.put(h0, (uint32_t)q + 1);
+            T.put(h1, (uint32_t)q + 2);
+        }
+        lds_order();
+        ZP(4);
+        if (j >= 64) {
+            const int32_t ql = (int32_t)readlane((uint32_t)q, nbt - 1);
+            ip0 = ql + ((ql - anchor) >> 7) + 2;
+            bp = -1;
+            continue;
+        }
+        Ap = A;
+        bp = pb ? ipb : -1;
+        bvalid = vcount;
+        // ---- a match at iteration j.  Every lane works out, in VGPRs, the
+        // match its own iteration would give (start, source, the cheap
+        // part of the extension from the windows already loaded); lane j's
+        // values are then read once (few SGPRs live: no SGPR spills)
+        uint32_t mstart = 0, msrc = 0, mlen0 = 4, fch = 0, bch = 0, mflags = 0;
+        {
+            const int ty = rep ? 0 : k0 ? 1 : 2;
+            uint4 Aa = A;
+            if (ty == 2)  // the match starts at q + 1: shift the window by a byte
+                Aa = make_uint4(__builtin_amdgcn_alignbyte(A.y, A.x, 1), __builtin_amdgcn_alignbyte(A.z, A.y, 1),
+                                __builtin_amdgcn_alignbyte(A.w, A.z, 1), A.w >> 8);
+            const uint4 Bb = ty == 0 ? AR : ty == 1 ? X0 : X1;
+            const uint4 X = make_uint4(Aa.x ^ Bb.x, Aa.y ^ Bb.y, Aa.z ^ Bb.z, Aa.w ^ Bb.w);
+            if (ty == 0) {
+                const uint32_t ml0 = (X.x >> 24) == 0u ? 1u : 0u;  // ip2[-1] == repMatch[-1]
+                mstart = (uint32_t)q + 2 - ml0;
+                msrc = mstart - o1;
+                mlen0 = 4 + ml0;
+                fch = first_diff(X, 8);  // bytes q+6 .. q+13
+                mflags = fch == 8 ? 1u : 0u;
+            } else {
+                mstart = ty == 1 ? (uint32_t)q : (uint32_t)q + 1;
+                msrc = (ty == 1 ? i0 : i1) - 1;
+                const uint32_t favail = ty == 1 ? 10 : 9;  // bytes start+4 .. (window end)
+                fch = umin32(first_diff(X, 6), favail);
+                bch = ((X.x >> 8) & 0xFFu) ? 0u : ((X.x & 0xFFu) ? 1u : 2u);
+                mflags = (fch == favail ? 1u : 0u) | (bch == 2 ? 2u : 0u) | 4u;
+            }
+        }
+        const uint32_t h2 = zhash((uint64_t)A.y | ((uint64_t)A.z << 32), hlog, mls);  // hash at q + 2
+        const int32_t qj = (int32_t)readlane((uint32_t)q, j);
+        const uint32_t jh2 = readlane(h2, j);
+        int32_t start = (int32_t)readlane(mstart, j), mst = (int32_t)readlane(msrc, j);
+        int32_t mlen = (int32_t)readlane(mlen0, j), fcheap = (int32_t)readlane(fch, j), bcheap = (int32_t)readlane(bch, j);
+        const uint32_t fl = readlane(mflags, j);
+        const bool fex = fl & 1u, bex = (fl & 2u) != 0, regular = (fl & 4u) != 0;
+        uint32_t ofv = 1;
+        if (regular) {
+            o2 = o1;
+            o1 = (uint32_t)(start - mst);
+            ofv = o1 + 3;
+        }
+        const int32_t flim = be - (start + mlen);
+        const int32_t blim = !regular ? 0 : (int32_t)umin32((uint32_t)(start - anchor), (uint32_t)(mst - prefixPos));
+        if (fcheap > flim) fcheap = flim;
+        if (bcheap > blim) bcheap = blim;
+        const bool nf = fex && fcheap < flim, nbk = bex && bcheap < blim;
+        if (nf || nbk) {
+            ZPC(10);
+            int32_t f2 = 0, b2 = 0;
+            ext_counts(S, start + mlen + fcheap, mst + mlen + fcheap, nf ? flim - fcheap : 0, start - bcheap,
+                       mst - bcheap, nbk ? blim - bcheap : 0, f2, b2);
+            fcheap += f2;
+            bcheap += b2;
+        }
+        start -= bcheap;
+        mst -= bcheap;
+        mlen += bcheap + fcheap;
+        emit((uint32_t)(start - anchor), (uint32_t)(mlen - 3), ofv);
+        ZPC(8);
+        nl += start - anchor;
+        ip0 = start + mlen;
+        anchor = ip0;
+        if (ip0 <= ilimit) {
+            if (l == 0) T.put(jh2, (uint32_t)(qj + 2 + 1));  // hashTable[hash(current0 + 2)]
+            lds_order();
+            pend = 1;
+        }
+        ZP(5);
+    }
+    if (ns & 63) {  // the last partial group
+        const int32_t g0 = ns & ~63;
+        if (g0 + l < ns) sq[g0 + l] = sbuf;
+    }
+    nl += be - anchor;
+    const uint32_t ro0 = o1 ? o1 : saved, ro1 = o2 ? o2 : saved;
+    const bool assumed = B.conf ? B.conf == 1 : !rle;
+    if (l == 0) {
+        B.ns = ns;
+        B.nl = nl;
+        B.rin0 = rin0; B.rin1 = rin1; B.rout0 = ro0; B.rout1 = ro1;
+        B.flags = (rle ? F_RLE : 0) | (assumed ? F_ASSUMED : 0);
+    }
+    if (assumed) {
+        off1 = ro0;
+        off2 = ro1;
+    }
+    ZP_FLUSH();
+}
+
 template <bool WIDE>
 __global__ __launch_bounds__(64) void zl1_parse_kernel(const FInfo *__restrict__ fi, const int32_t *__restrict__ flist,
                                                        BInfo *__restrict__ bi, uint64_t *__restrict__ seqs) {
@@ -375,8 +671,7 @@ __global__ __launch_bounds__(64) void zl1_parse_kernel(const FInfo *__restrict__
     const int l = lane_id();
     const FInfo F = fi[flist[blockIdx.x]];
     if (F.status < 0) return;
-    const uint32_t hlog = F.hlog, mls = F.mls, tsize = 1u << hlog;
-    const int32_t maxDist = 1 << F.wlog;
+    const uint32_t tsize = 1u << F.hlog;
     Tab<WIDE> T;
     T.lo = (uint16_t *)smem;
     T.hi = smem + (tsize >> 1);
@@ -386,294 +681,120 @@ __global__ __launch_bounds__(64) void zl1_parse_kernel(const FInfo *__restrict__
     __syncthreads();
     const Src S = make_src(F.src, F.n);
     uint32_t off1 = 1, off2 = 4;  // repStartValue
-    ZP_DECL
-    for (int32_t k = 0; k < F.nb; k++) {
-        BInfo &B = bi[F.b0 + k];
-        const int32_t bs = B.bs, be = B.be;
-        const uint32_t rin0 = off1, rin1 = off2;
-        if (be - bs < 7) {  // ZSTD_buildSeqStore: too small to compress, match state untouched
-            if (l == 0) {
-                B.ns = 0;
-                B.nl = be - bs;
-                B.rin0 = rin0; B.rin1 = rin1; B.rout0 = rin0; B.rout1 = rin1;
-                B.flags = F_NOCOMP;
+    for (int32_t k = 0; k < F.nb; k++) parse_block<WIDE>(F, bi[F.b0 + k], k, T, S, seqs, off1, off2);
+}
+
+// ---------------------------------------------------------------------------
+// small batches: block-parallel speculative parse (exact)
+// ---------------------------------------------------------------------------
+// The frame-serial parse runs one wave per frame: a lone 4 MiB frame is 32
+// block parses in a row (~0.7 s).  A block's parse depends on the frame only
+// through its starting hash table and repeat offsets, and the table at the
+// start of block k holds, for every bucket, the last index any earlier block
+// wrote there -- the maximum over those blocks' WRITE SETS (indices grow with
+// the block).  So every block parses at once from inputs built out of the
+// other blocks' latest results (zl1_spec_merge: prefix maxima of the write
+// sets, the repeat offsets passed on in block order), and again whenever its
+// inputs changed; when a round changes no block's inputs, each block's inputs
+// are what its predecessors' parses produce, and by induction from block 0
+// (whose inputs are the empty table and repStartValue) every block's parse is
+// the serial one.  Text settles in 7-8 rounds, random and zero data in 3 (CPU
+// simulation on the fixture inputs); at most nb + 1 rounds in any case.
+struct SpecB {
+    int32_t chg;          // run this round
+    uint32_t rin0, rin1;  // repeat offsets handed in
+    uint32_t pad;
+};
+constexpr uint32_t SPEC_TSZ = 1u << 14;  // table slots per block (wide frames: hashLog <= 14)
+
+// one workgroup per frame
+__global__ __launch_bounds__(256) void zl1_spec_merge(const FInfo *__restrict__ fi, const int32_t *__restrict__ sflist,
+                                                      const int32_t *__restrict__ sslot, const BInfo *__restrict__ bi,
+                                                      const uint32_t *__restrict__ W, uint32_t *__restrict__ I,
+                                                      SpecB *__restrict__ sp, int32_t *__restrict__ any, int first) {
+    const FInfo F = fi[sflist[blockIdx.x]];
+    const int32_t s0 = sslot[blockIdx.x];
+    const uint32_t tsize = 1u << F.hlog;
+    const int t = threadIdx.x;
+    if (t == 0) {  // repeat offsets in block order (the serial kernel's off1 / off2)
+        uint32_t r0 = 1, r1 = 4;
+        for (int32_t k = 0; k < F.nb; k++) {
+            SpecB &x = sp[s0 + k];
+            const BInfo &B = bi[F.b0 + k];
+            x.chg = first || x.rin0 != r0 || x.rin1 != r1;
+            x.rin0 = r0;
+            x.rin1 = r1;
+            if (B.be - B.bs >= 7 && (B.flags & F_ASSUMED)) {
+                r0 = B.rout0;
+                r1 = B.rout1;
             }
-            continue;
-        }
-        const bool rle = k > 0 && all_equal(S, bs, be);
-        const int32_t prefixPos = be > maxDist ? be - maxDist : 0;
-        const uint32_t prefixIdx = (uint32_t)prefixPos + 1, R = (uint32_t)be;
-        if (WIDE && prefixPos > 0) {  // entries that left the window: the window's lowest index
-            __syncthreads();
-            for (uint32_t h = l; h < tsize; h += 64)
-                if (T.get(h, R) <= prefixIdx) T.put(h, prefixIdx);
-            __syncthreads();
-        }
-        ZP(6);
-        ZPC(11);
-        // ---- ZSTD_compressBlock_fast_generic
-        uint64_t *sq = seqs + B.seq_off;
-        const int32_t ilimit = be - 8;
-        int32_t ip0 = bs, anchor = bs, ns = 0, nl = 0;
-        uint32_t o1 = off1, o2 = off2, saved = 0;
-        if (ip0 == prefixPos) ip0++;
-        {
-            const uint32_t maxRep = (uint32_t)(ip0 > maxDist ? maxDist : ip0);
-            if (o2 > maxRep) { saved = o2; o2 = 0; }
-            if (o1 > maxRep) { saved = o1; o1 = 0; }
-        }
-        // sequence records collect in a VGPR (lane i: record 64 g + i) and are
-        // stored 64 at a time: no store per sequence for later vmcnt waits to drain
-        uint64_t sbuf = 0;
-        auto emit = [&](uint32_t ll, uint32_t mlb, uint32_t ofv) {
-            const uint64_t r = seq_pack(ll, mlb, ofv);
-            if (l == (ns & 63)) sbuf = r;
-            if ((ns & 63) == 63) sq[ns - 63 + l] = sbuf;
-            ns++;
-        };
-        int pend = 0;  // 1: after a search match (insert ip0-2, then the repeat loop); 2: after a repeat-loop match
-        // windows of the last step whose positions were bp + 2 l (lanes [0, bvalid) valid)
-        uint4 Ap = make_uint4(0, 0, 0, 0);
-        int32_t bp = -1, bvalid = 0;
-        for (int guard = 0; guard < 4 * BLK; guard++) {
-            const bool pb = pend != 0;
-            const int32_t ipb = ip0;
-            // positions of this search step (after a match: ip0 + 2 l)
-            const int32_t q = pb ? ip0 + 2 * l : sched_pos(ip0, anchor, (uint32_t)l);
-            // windows A = bytes [q - 2, q + 14).  After a match they come from
-            // the previous step's lanes when those hold them (a cross-lane
-            // permute instead of a memory round trip); lanes without a source
-            // sit this step out
-            uint4 A = make_uint4(0, 0, 0, 0);
-            const bool use_sh = pb && bp >= 0 && ip0 - bp <= 2 * (bvalid - 2);
-            bool have = true;
-            if (use_sh) {
-                const int32_t e = (ip0 - bp) + 2 * l;
-                const int s0 = e >> 1;
-                const uint32_t dl = (uint32_t)e & 1u;
-                const int sa = s0 < 63 ? s0 : 63, sb = s0 + 1 < 63 ? s0 + 1 : 63;
-                const uint32_t x0 = (uint32_t)__shfl((int)Ap.x, sa, 64), x1 = (uint32_t)__shfl((int)Ap.y, sa, 64),
-                               x2 = (uint32_t)__shfl((int)Ap.z, sa, 64), x3 = (uint32_t)__shfl((int)Ap.w, sa, 64),
-                               y3 = (uint32_t)__shfl((int)Ap.w, sb, 64);
-                A = dl ? make_uint4(__builtin_amdgcn_alignbyte(x1, x0, 1), __builtin_amdgcn_alignbyte(x2, x1, 1),
-                                    __builtin_amdgcn_alignbyte(x3, x2, 1), __builtin_amdgcn_alignbyte(y3 >> 16, x3, 1))
-                       : make_uint4(x0, x1, x2, x3);
-                have = s0 + (int)dl < bvalid;
-            }
-            const bool on = q + 1 < ilimit && (!pb || l < JFS_ZL1_PB) && have;
-            // (after a match every lane loads its window, on or not: the next
-            // step's windows then come from these)
-            const bool ld = !use_sh && (pb || on);
-            // AR = the same bytes o1 back (repeat check + its first extension
-            // bytes), R2 = (lane 0, after a match) 16 bytes at ip0 - 2 - o2 (the
-            // repeat loop): both awaited only where used
-            uint4 AR = make_uint4(0, 0, 0, 0), R2 = make_uint4(0, 0, 0, 0);
-            if (ld) A = ld128(S, q - 2);
-            if (on) AR = ld128(S, q - 2 - (int32_t)o1);
-            if (pb && l == 0) R2 = ld128(S, ip0 - 2 - (int32_t)o2);
-            const int32_t vcount = pb ? (int32_t)__builtin_popcountll(ballot(use_sh ? have : ld)) : 0;
-            const uint64_t v0 = (uint64_t)__builtin_amdgcn_alignbyte(A.y, A.x, 2) | ((uint64_t)__builtin_amdgcn_alignbyte(A.z, A.y, 2) << 32);
-            const uint64_t v1 = (uint64_t)__builtin_amdgcn_alignbyte(A.y, A.x, 3) | ((uint64_t)__builtin_amdgcn_alignbyte(A.z, A.y, 3) << 32);
-            const uint32_t val0 = (uint32_t)v0, val1 = (uint32_t)v1;
-            const uint32_t h0 = zhash(v0, hlog, mls), h1 = zhash(v1, hlog, mls);
-            ZP(0);
-            ZPC(9);
-            if (pend == 1) {  // hashTable[hash(ip0 - 2)] = ip0 - 2
-                const uint64_t vm2 = (uint64_t)A.x | ((uint64_t)A.y << 32);
-                const uint32_t hm2 = readlane(zhash(vm2, hlog, mls), 0);
-                if (l == 0) T.put(hm2, (uint32_t)(ip0 - 2 + 1));
-                lds_order();
-            }
-            // the repeat loop's check waits for R2: the search step's table
-            // reads and bucket tags go first (undone if the repeat loop fires)
-            const bool rchk = pb && o2 > 0 && ip0 <= ilimit;
-            pend = 0;
-            const uint64_t onm = ballot(on);
-            if (!onm && !rchk) break;  // ip1 >= ilimit: no more positions in this block
-            const int non = onm ? 64 - __builtin_clzll(onm) : 0;  // lanes [0, non) are on
-            // table reads (before any write of this step), then tags to find
-            // lanes sharing a bucket
-            uint32_t olo0 = 0, olo1 = 0, i0 = 0, i1 = 0;
-            if (on) {
-                olo0 = T.lo[h0];
-                olo1 = T.lo[h1];
-                i0 = T.get(h0, R);
-                i1 = T.get(h1, R);
-            }
-            lds_order();
-            if (on) {
-                T.lo[h0] = (uint16_t)l;
-                T.lo[h1] = (uint16_t)l;
-            }
-            lds_order();
-            uint32_t cm = 64;
-            if (on) {
-                const uint32_t t0 = T.lo[h0], t1 = T.lo[h1];
-                if (t0 != (uint32_t)l) cm = umin32((uint32_t)l, t0);
-                if (t1 != (uint32_t)l) cm = umin32(cm, umin32((uint32_t)l, t1));
-            }
-            const int cut = (int)dwave_min(cm) + 1;
-            const int nbt = cut < non ? cut : non;  // lanes [0, nbt) read exactly what the serial loop reads
-            const bool dec = l < nbt;
-            const bool c0 = dec && i0 > prefixIdx, c1 = dec && i1 > prefixIdx;
-            // candidates: bytes [cand - 2, cand + 14) (check + first extension bytes)
-            uint4 X0 = make_uint4(0, 0, 0, 0), X1 = make_uint4(0, 0, 0, 0);
-            if (c0) X0 = ld128(S, (int32_t)i0 - 3);
-            if (c1) X1 = ld128(S, (int32_t)i1 - 3);
-            ZP(2);
-            if (rchk) {
-                const uint4 a0 = readlane4(A, 0), r0 = readlane4(R2, 0);
-                const uint4 X = make_uint4(a0.x ^ r0.x, a0.y ^ r0.y, a0.z ^ r0.z, a0.w ^ r0.w);
-                if (first_diff(X, 2) >= 4) {  // MEM_read32(ip0) == MEM_read32(ip0 - offset_2)
-                    if (on) {  // the search step did not happen: its tags come off
-                        T.lo[h0] = (uint16_t)olo0;
-                        T.lo[h1] = (uint16_t)olo1;
-                    }
-                    lds_order();
-                    // repeat-offset match at ip0 (offset_2), then swap
-                    const int32_t flim = be - (ip0 + 4);
-                    int32_t rl = (int32_t)umin32(first_diff(X, 6), (uint32_t)flim);
-                    if (rl == 10 && rl < flim) {
-                        int32_t f2 = 0, b2 = 0;
-                        ext_counts(S, ip0 + 4 + rl, ip0 + 4 + rl - (int32_t)o2, flim - rl, 0, 0, 0, f2, b2);
-                        rl += f2;
-                    }
-                    rl += 4;
-                    const uint32_t t = o2;
-                    o2 = o1;
-                    o1 = t;
-                    if (l == 0) T.put(readlane(h0, 0), (uint32_t)(ip0 + 1));
-                    lds_order();
-                    emit(0, (uint32_t)(rl - 3), 1);
-                    Ap = A;
-                    bp = ipb;
-                    bvalid = vcount;
-                    ip0 += rl;
-                    anchor = ip0;
-                    if (ip0 <= ilimit) pend = 2;
-                    ZP(1);
-                    continue;
-                }
-            }
-            ZP(1);
-            if (!onm) break;
-            const bool rep = dec && o1 > 0 && AR.y == A.y;  // MEM_read32(ip2 - offset_1) == MEM_read32(ip2)
-            const bool k0 = c0 && __builtin_amdgcn_alignbyte(X0.y, X0.x, 2) == val0;
-            const bool k1 = c1 && __builtin_amdgcn_alignbyte(X1.y, X1.x, 2) == val1;
-            const int j = ctz64(ballot(rep || k0 || k1));
-            ZP(3);
-            // lanes after the first hit (and past the cut) put their buckets
-            // back; then the lanes up to the hit insert ip0 and ip1
-            lds_order();
-            if (on && (l >= nbt || l > j)) {
-                T.lo[h0] = (uint16_t)olo0;
-                T.lo[h1] = (uint16_t)olo1;
-            }
-            lds_order();
-            if (on && l < nbt && l <= j) {
-                T.put(h0, (uint32_t)q + 1);
-                T.put(h1, (uint32_t)q + 2);
-            }
-            lds_order();
-            ZP(4);
-            if (j >= 64) {
-                const int32_t ql = (int32_t)readlane((uint32_t)q, nbt - 1);
-                ip0 = ql + ((ql - anchor) >> 7) + 2;
-                bp = -1;
-                continue;
-            }
-            Ap = A;
-            bp = pb ? ipb : -1;
-            bvalid = vcount;
-            // ---- a match at iteration j.  Every lane works out, in VGPRs, the
-            // match its own iteration would give (start, source, the cheap
-            // part of the extension from the windows already loaded); lane j's
-            // values are then read once (few SGPRs live: no SGPR spills)
-            uint32_t mstart = 0, msrc = 0, mlen0 = 4, fch = 0, bch = 0, mflags = 0;
-            {
-                const int ty = rep ? 0 : k0 ? 1 : 2;
-                uint4 Aa = A;
-                if (ty == 2)  // the match starts at q + 1: shift the window by a byte
-                    Aa = make_uint4(__builtin_amdgcn_alignbyte(A.y, A.x, 1), __builtin_amdgcn_alignbyte(A.z, A.y, 1),
-                                    __builtin_amdgcn_alignbyte(A.w, A.z, 1), A.w >> 8);
-                const uint4 Bb = ty == 0 ? AR : ty == 1 ? X0 : X1;
-                const uint4 X = make_uint4(Aa.x ^ Bb.x, Aa.y ^ Bb.y, Aa.z ^ Bb.z, Aa.w ^ Bb.w);
-                if (ty == 0) {
-                    const uint32_t ml0 = (X.x >> 24) == 0u ? 1u : 0u;  // ip2[-1] == repMatch[-1]
-                    mstart = (uint32_t)q + 2 - ml0;
-                    msrc = mstart - o1;
-                    mlen0 = 4 + ml0;
-                    fch = first_diff(X, 8);  // bytes q+6 .. q+13
-                    mflags = fch == 8 ? 1u : 0u;
-                } else {
-                    mstart = ty == 1 ? (uint32_t)q : (uint32_t)q + 1;
-                    msrc = (ty == 1 ? i0 : i1) - 1;
-                    const uint32_t favail = ty == 1 ? 10 : 9;  // bytes start+4 .. (window end)
-                    fch = umin32(first_diff(X, 6), favail);
-                    bch = ((X.x >> 8) & 0xFFu) ? 0u : ((X.x & 0xFFu) ? 1u : 2u);
-                    mflags = (fch == favail ? 1u : 0u) | (bch == 2 ? 2u : 0u) | 4u;
-                }
-            }
-            const uint32_t h2 = zhash((uint64_t)A.y | ((uint64_t)A.z << 32), hlog, mls);  // hash at q + 2
-            const int32_t qj = (int32_t)readlane((uint32_t)q, j);
-            const uint32_t jh2 = readlane(h2, j);
-            int32_t start = (int32_t)readlane(mstart, j), mst = (int32_t)readlane(msrc, j);
-            int32_t mlen = (int32_t)readlane(mlen0, j), fcheap = (int32_t)readlane(fch, j), bcheap = (int32_t)readlane(bch, j);
-            const uint32_t fl = readlane(mflags, j);
-            const bool fex = fl & 1u, bex = (fl & 2u) != 0, regular = (fl & 4u) != 0;
-            uint32_t ofv = 1;
-            if (regular) {
-                o2 = o1;
-                o1 = (uint32_t)(start - mst);
-                ofv = o1 + 3;
-            }
-            const int32_t flim = be - (start + mlen);
-            const int32_t blim = !regular ? 0 : (int32_t)umin32((uint32_t)(start - anchor), (uint32_t)(mst - prefixPos));
-            if (fcheap > flim) fcheap = flim;
-            if (bcheap > blim) bcheap = blim;
-            const bool nf = fex && fcheap < flim, nbk = bex && bcheap < blim;
-            if (nf || nbk) {
-                ZPC(10);
-                int32_t f2 = 0, b2 = 0;
-                ext_counts(S, start + mlen + fcheap, mst + mlen + fcheap, nf ? flim - fcheap : 0, start - bcheap,
-                           mst - bcheap, nbk ? blim - bcheap : 0, f2, b2);
-                fcheap += f2;
-                bcheap += b2;
-            }
-            start -= bcheap;
-            mst -= bcheap;
-            mlen += bcheap + fcheap;
-            emit((uint32_t)(start - anchor), (uint32_t)(mlen - 3), ofv);
-            ZPC(8);
-            nl += start - anchor;
-            ip0 = start + mlen;
-            anchor = ip0;
-            if (ip0 <= ilimit) {
-                if (l == 0) T.put(jh2, (uint32_t)(qj + 2 + 1));  // hashTable[hash(current0 + 2)]
-                lds_order();
-                pend = 1;
-            }
-            ZP(5);
-        }
-        if (ns & 63) {  // the last partial group
-            const int32_t g0 = ns & ~63;
-            if (g0 + l < ns) sq[g0 + l] = sbuf;
-        }
-        nl += be - anchor;
-        const uint32_t ro0 = o1 ? o1 : saved, ro1 = o2 ? o2 : saved;
-        const bool assumed = B.conf ? B.conf == 1 : !rle;
-        if (l == 0) {
-            B.ns = ns;
-            B.nl = nl;
-            B.rin0 = rin0; B.rin1 = rin1; B.rout0 = ro0; B.rout1 = ro1;
-            B.flags = (rle ? F_RLE : 0) | (assumed ? F_ASSUMED : 0);
-        }
-        if (assumed) {
-            off1 = ro0;
-            off2 = ro1;
         }
     }
-    ZP_FLUSH();
+    __syncthreads();
+    for (uint32_t h = t; h < tsize; h += 256) {
+        uint32_t run = 0;
+        for (int32_t k = 0; k < F.nb; k++) {
+            const size_t o = (size_t)(s0 + k) * SPEC_TSZ + h;
+            if (I[o] != run) {
+                I[o] = run;
+                if (!first) atomicOr(&sp[s0 + k].chg, 1);
+            }
+            run = umax32(run, W[o]);
+        }
+    }
+    __syncthreads();
+    if (t < 64) {
+        int32_t c = 0;
+        for (int32_t k = t; k < F.nb; k += 64) c |= sp[s0 + k].chg;
+        if (__ballot(c != 0) && t == 0) atomicOr(any, 1);
+    }
+}
+
+// one wave per block whose inputs changed
+template <bool WIDE>
+__global__ __launch_bounds__(64) void zl1_spec_parse(const FInfo *__restrict__ fi, const int32_t *__restrict__ sblist,
+                                                     BInfo *__restrict__ bi, uint64_t *__restrict__ seqs,
+                                                     const uint32_t *__restrict__ I, uint32_t *__restrict__ W,
+                                                     const SpecB *__restrict__ sp) {
+    extern __shared__ uint32_t smem[];
+    const int g = blockIdx.x;
+    const SpecB x = sp[g];
+    if (!x.chg) return;
+    const int l = lane_id();
+    BInfo &B = bi[sblist[g]];
+    const FInfo F = fi[B.frame];
+    const int32_t k = sblist[g] - F.b0;
+    const uint32_t tsize = 1u << F.hlog;
+    const int32_t maxDist = 1 << F.wlog;
+    Tab<WIDE> T;
+    T.lo = (uint16_t *)smem;
+    T.hi = smem + (tsize >> 1);
+    // the input table: entries at or below the window's lowest index act as
+    // "no candidate" (and must not alias into the 20-bit window)
+    const uint32_t prefixIdx = (uint32_t)(B.be > maxDist ? B.be - maxDist : 0) + 1;
+    const uint32_t *Ik = I + (size_t)g * SPEC_TSZ;
+    for (uint32_t h8 = l; h8 < (tsize >> 3); h8 += 64) {
+        uint32_t nib = 0;
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const uint32_t v = umax32(Ik[8 * h8 + q], prefixIdx);
+            T.lo[8 * h8 + q] = (uint16_t)v;
+            nib |= ((v >> 16) & 15u) << (4 * q);
+        }
+        if (WIDE) T.hi[h8] = nib;
+    }
+    __syncthreads();
+    const Src S = make_src(F.src, F.n);
+    uint32_t off1 = x.rin0, off2 = x.rin1;
+    parse_block<WIDE>(F, B, k, T, S, seqs, off1, off2);
+    __syncthreads();
+    // the block's write set: the entries now at indices of this block
+    uint32_t *Wk = W + (size_t)g * SPEC_TSZ;
+    const uint32_t R = (uint32_t)B.be;
+    for (uint32_t h = l; h < tsize; h += 64) {
+        const uint32_t e = T.get(h, R);
+        Wk[h] = e > (uint32_t)B.bs ? e : 0u;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1863,6 +1984,17 @@ extern "C" int jfs_zpprof_reset() {
 }
 #endif
 
+// Small batches take the block-parallel speculative parse (zl1_spec_*) for
+// their multi-block frames: at most JFS_ZL1_SPEC_MAX blocks in all (default
+// 2,048; 0 = never).  Larger batches fill the GPU with frame-serial parses.
+int spec_max_blocks() {
+    static int v = [] {
+        const char *e = getenv("JFS_ZL1_SPEC_MAX");
+        return e ? std::max(0, atoi(e)) : 2048;
+    }();
+    return v;
+}
+
 extern "C" int jfs_launch_zstd_encode(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, hipStream_t stream) {
     if (nblk <= 0) return 0;
     int dev = 0;
@@ -1910,10 +2042,36 @@ extern "C" int jfs_launch_zstd_encode(const jfs_dev_block *d_blocks, int nblk, i
         }
     }
     const int nbk = (int)bi.size();
+    // speculative parse: the multi-block (wide) frames of a small batch, their
+    // blocks in slots grouped by hashLog
+    std::vector<int32_t> sf, sslot, sblist;
+    std::vector<std::pair<uint32_t, std::pair<int, int>>> sgrp;  // hashLog -> (first slot, slots)
+    {
+        int64_t cand = 0;
+        for (int f = 0; f < nblk; f++)
+            if (fi[f].status == 0 && fi[f].nb >= 2 && fi[f].n >= 65536) cand += fi[f].nb;
+        if (cand > 0 && cand <= spec_max_blocks()) {
+            for (uint32_t hl = 6; hl <= 14; hl++) {
+                const int g0 = (int)sblist.size();
+                for (int f = 0; f < nblk; f++) {
+                    const FInfo &F = fi[f];
+                    if (F.status != 0 || F.nb < 2 || F.n < 65536 || F.hlog != hl) continue;
+                    sf.push_back(f);
+                    sslot.push_back((int32_t)sblist.size());
+                    for (int k = 0; k < F.nb; k++) sblist.push_back(F.b0 + k);
+                }
+                if ((int)sblist.size() > g0) sgrp.push_back({hl, {g0, (int)sblist.size() - g0}});
+            }
+        }
+    }
+    const int nsf = (int)sf.size(), nsb = (int)sblist.size();
     const size_t fb = a256(sizeof(FInfo) * nblk), bb = a256(sizeof(BInfo) * std::max(nbk, 1)),
                  lb = a256(sizeof(int32_t) * (2 * (size_t)nblk + (size_t)nbk + 16)), sb = a256(sizeof(uint64_t) * (size_t)std::max<int64_t>(seq_total, 1)),
                  yb = a256((size_t)std::max<int64_t>(byte_total, 1)), hb = a256(sizeof(uint32_t) * 1024 * (size_t)std::max(nbk, 1));
-    if (!z.grow(fb + bb + lb + sb + yb + hb)) return -1;
+    const size_t spb = nsb ? a256(sizeof(int32_t) * (2 * (size_t)nsf + nsb + 16)) + a256(sizeof(SpecB) * nsb) +
+                                 2 * a256(sizeof(uint32_t) * SPEC_TSZ * (size_t)nsb) + 256
+                           : 0;
+    if (!z.grow(fb + bb + lb + sb + yb + hb + spb)) return -1;
     uint8_t *p = z.d;
     FInfo *d_fi = (FInfo *)p;
     p += fb;
@@ -1926,6 +2084,21 @@ extern "C" int jfs_launch_zstd_encode(const jfs_dev_block *d_blocks, int nblk, i
     uint8_t *d_bytes = p;
     p += yb;
     uint32_t *d_hist = (uint32_t *)p;
+    p += hb;
+    int32_t *d_slists = nullptr, *d_any = nullptr;
+    SpecB *d_sp = nullptr;
+    uint32_t *d_W = nullptr, *d_I = nullptr;
+    if (nsb) {
+        d_slists = (int32_t *)p;
+        p += a256(sizeof(int32_t) * (2 * (size_t)nsf + nsb + 16));
+        d_sp = (SpecB *)p;
+        p += a256(sizeof(SpecB) * nsb);
+        d_W = (uint32_t *)p;
+        p += a256(sizeof(uint32_t) * SPEC_TSZ * (size_t)nsb);
+        d_I = (uint32_t *)p;
+        p += a256(sizeof(uint32_t) * SPEC_TSZ * (size_t)nsb);
+        d_any = (int32_t *)p;
+    }
     if (hipMemcpyAsync(d_fi, fi.data(), sizeof(FInfo) * nblk, hipMemcpyHostToDevice, stream) != hipSuccess) return -1;
     if (nbk > 0 && hipMemcpyAsync(d_bi, bi.data(), sizeof(BInfo) * nbk, hipMemcpyHostToDevice, stream) != hipSuccess)
         return -1;
@@ -1936,7 +2109,48 @@ extern "C" int jfs_launch_zstd_encode(const jfs_dev_block *d_blocks, int nblk, i
     for (int f = 0; f < nblk; f++)
         if (fi[f].status < 0) hret[f] = -2;
     if (hipMemcpyAsync(d_ret, hret.data(), sizeof(int32_t) * nblk, hipMemcpyHostToDevice, stream) != hipSuccess) return -1;
+    std::vector<char> spec_f(nblk, 0);
+    for (int f : sf) spec_f[f] = 1;
     for (int pass = 0; pass <= nbk + 1 && !todo.empty(); pass++) {
+        // pass 0: the speculative block-parallel parse of the small batch's
+        // multi-block frames (a frame whose confirmation guess turns out wrong
+        // is parsed again frame-serially in the next pass)
+        if (pass == 0 && nsb) {
+            std::vector<int32_t> sl(sf);
+            sl.insert(sl.end(), sslot.begin(), sslot.end());
+            sl.insert(sl.end(), sblist.begin(), sblist.end());
+            if (hipMemcpyAsync(d_slists, sl.data(), sizeof(int32_t) * sl.size(), hipMemcpyHostToDevice, stream) !=
+                    hipSuccess ||
+                hipMemsetAsync(d_W, 0, sizeof(uint32_t) * SPEC_TSZ * (size_t)nsb, stream) != hipSuccess ||
+                hipMemsetAsync(d_sp, 0, sizeof(SpecB) * nsb, stream) != hipSuccess)
+                return -1;
+            const int32_t *d_sf = d_slists, *d_ss = d_slists + nsf, *d_sb = d_slists + 2 * nsf;
+            int maxnb = 0;
+            for (int f : sf) maxnb = std::max(maxnb, fi[f].nb);
+            bool settled = false;
+            for (int r = 0; r <= maxnb + 1; r++) {
+                if (hipMemsetAsync(d_any, 0, sizeof(int32_t), stream) != hipSuccess) return -1;
+                hipLaunchKernelGGL(zl1_spec_merge, dim3(nsf), dim3(256), 0, stream, d_fi, d_sf, d_ss, d_bi, d_W, d_I,
+                                   d_sp, d_any, r == 0 ? 1 : 0);
+                if (hipGetLastError() != hipSuccess) return -1;
+                if (r > 0) {
+                    int32_t h_any = 1;
+                    if (hipMemcpyAsync(&h_any, d_any, sizeof(int32_t), hipMemcpyDeviceToHost, stream) != hipSuccess ||
+                        hipStreamSynchronize(stream) != hipSuccess)
+                        return -1;
+                    if (!h_any) { settled = true; break; }
+                }
+                for (const auto &g : sgrp) {
+                    const size_t tsz = (size_t)1 << g.first;
+                    const int g0 = g.second.first, cnt = g.second.second;
+                    hipLaunchKernelGGL(zl1_spec_parse<true>, dim3(cnt), dim3(64), tsz * 2 + tsz / 2, stream, d_fi,
+                                       d_sb + g0, d_bi, d_seq, d_I + (size_t)g0 * SPEC_TSZ, d_W + (size_t)g0 * SPEC_TSZ,
+                                       d_sp + g0);
+                    if (hipGetLastError() != hipSuccess) return -1;
+                }
+            }
+            if (!settled) return -1;  // (cannot happen: nb + 1 rounds settle any frame)
+        }
         // parse launches: one per (table width, hashLog) so each gets exactly its LDS
         std::vector<int32_t> lists, blist;
         struct Grp { bool wide; uint32_t hlog; int off, cnt; };
@@ -1946,6 +2160,7 @@ extern "C" int jfs_launch_zstd_encode(const jfs_dev_block *d_blocks, int nblk, i
                 Grp g{wide != 0, hl, (int)lists.size(), 0};
                 for (int f : todo) {
                     const bool w = fi[f].n >= 65536;
+                    if (pass == 0 && spec_f[f]) continue;  // parsed above
                     if (w == (wide != 0) && fi[f].hlog == hl && fi[f].nb > 0) {
                         lists.push_back(f);
                         g.cnt++;
