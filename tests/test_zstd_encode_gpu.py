@@ -180,6 +180,23 @@ def test_zstd_encode_golden_l1_cases(gpu):
         assert x == c["csize"] and _sha(f) == c["comp_sha"], (c["kind"], c["size"], x, c["csize"])
 
 
+def test_zstd_encode_golden_l1_cases_frame_serial(gpu):
+    """The same cases in a batch of more than JFS_ZL1_SPEC_MAX (2,048) blocks:
+    the frame-serial parse (one wave per frame) instead of the small-batch
+    speculative block-parallel one -- byte-identical either way."""
+    import json
+    from tests.zstd_l1_cases import make_case
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "zstd_l1_golden.json")))
+    cs = g["cases"]
+    big = [c for c in cs if c["kind"] == "T" and c["size"] == 4 << 20][0]
+    cs = cs + [big] * 64  # 64 x 32 blocks: past the speculative path's limit
+    srcs = [make_case(c["kind"], c["seed"], c["size"]) for c in cs]
+    assert sum((len(x) + (128 << 10) - 1) // (128 << 10) for x in srcs) > 2048
+    r, frames = encode_device(srcs, gpu, src_mis=1, dst_mis=4)
+    for c, x, f in zip(cs, r, frames):
+        assert x == c["csize"] and _sha(f) == c["comp_sha"], (c["kind"], c["size"], x, c["csize"])
+
+
 def test_zstd_encode_matches_oracle_seeded(gpu, oracle):
     """Seeded inputs of every kind and size class (many frames per launch, every
     (table width, hashLog) parse group): identical to the CPU oracle."""
