@@ -28,6 +28,10 @@
 //                     section (Huffman table build / reuse decision, exact
 //                     sizes), the raw / RLE / compressed choice, and the
 //                     block bytes written in place.
+// Small batches (<= JFS_ZL1_SPEC_MAX blocks of multi-block frames) replace the
+// frame-serial parse by zl1_spec_merge / zl1_spec_parse: every block parses at
+// once from the prefix maxima of the other blocks' write sets, again until no
+// block's inputs change -- the serial parse's result, by induction.
 // A block that ends up raw or RLE does not pass its repeat offsets on
 // (ZSTD_confirmRepcodesAndEntropyTables); the parse predicts that (RLE blocks
 // are known exactly, others are assumed compressed) and the literal kernel
