@@ -20,6 +20,7 @@ typedef JFS_GLOBAL uint32_t g_u32;
 typedef JFS_GLOBAL const uint32_t gc_u32;
 typedef JFS_GLOBAL uint4 g_u4;
 typedef JFS_GLOBAL const uint4 gc_u4;
+typedef JFS_GLOBAL const uint2 gc_u2;
 typedef JFS_GLOBAL const jfs_dev_block gc_blk;
 
 extern "C" {

@@ -44,23 +44,30 @@ __device__ unsigned long long g_eprof[12];
 #define EPC(k) do { } while (0)
 #define EP_FLUSH() do { } while (0)
 #endif
-#ifndef JFS_LZ4E_PSEARCH
-#define JFS_LZ4E_PSEARCH 1  // lane-parallel search over the skip schedule (serial loop on shared hashes)
-#endif
 constexpr int64_t kMaxInput = 0x7E000000;
 constexpr int64_t kSegMinInput = 65536 + 12 - 1;  // byU32 table (smaller blocks: byU16, serial kernel only)
-constexpr int OB = 2048;  // output staging ring (the put_* paths assume OB >= 2 * OFLUSH + slack)
-constexpr int OBMASK = OB - 1;
-constexpr int OFLUSH = 1024;
-constexpr int SW = 2048;  // source window (LDS), slides in SW/2 steps
-constexpr int SWMASK = SW - 1;
-constexpr int SWSTEP = SW / 2;  // = 64 lanes x 16 bytes
-
+// LDS of one block's wave.  Smem<false> (20 KiB, 8 blocks per CU): byU32
+// entries = position + check bits (byU16 view: the same 16 KiB), 2 KiB output
+// ring, 2 KiB source window.  Smem<true> ("compact", 10 KiB, 16 blocks per
+// CU; byU32 blocks of the large-batch kernel only): 17-bit position entries
+// (u16 + a bit plane, see ctab_*), no check bits, 512-byte output ring,
+// 1 KiB source window.
+template <bool C>
 struct Smem {
-    alignas(16) uint32_t table[4096];  // byU32 view; byU16 view is the same 16 KiB
+    static constexpr bool kCompact = C;
+    static constexpr int OB = C ? 512 : 2048;  // output staging ring (the put_* paths assume OB >= 2 * OFLUSH + slack)
+    static constexpr int OBMASK = OB - 1;
+    static constexpr int OFLUSH = C ? 128 : 1024;
+    static constexpr int SW = C ? 1024 : 2048;  // source window (LDS), slides in SW/2 steps
+    static constexpr int SWMASK = SW - 1;
+    static constexpr int SWSTEP = SW / 2;       // = 64 lanes x PIECE bytes
+    static constexpr int PIECE = SWSTEP / 64;
+    static constexpr int SPAN = C ? 448 : 512;  // search batch reach (bytes past its first position)
+    alignas(16) uint32_t table[C ? 2048 + 128 : 4096];
     alignas(16) uint8_t ob[OB];
     alignas(16) uint8_t sw[SW];
 };
+static_assert(sizeof(Smem<true>) == 10240, "compact layout: 16 blocks per CU");
 
 struct Enc {
     const gc_u8 *src;
@@ -70,12 +77,13 @@ struct Enc {
     int64_t F;   // flushed up to
     uint32_t dmis;
     // source window: covers "aligned offsets" q in [wq, wq + SW), q = p + smis
-    // for source position p; pf = this lane's 16 bytes of [wq + SW, wq + SW + SWSTEP)
+    // for source position p; pf = this lane's PIECE bytes of [wq + SW, wq + SW + SWSTEP)
     const gc_u4 *sa;  // src rounded down to 16 bytes
     int64_t smis, wq, nq;
     uint4 pf;
     int pb;        // position bits of a byU32 table entry (check bits above)
     uint32_t pmask;
+    int64_t rlast;  // compact table: position of the last refresh (ctab_refresh)
 };
 
 __device__ __forceinline__ uint32_t ld32u(const gc_u8 *p) {
@@ -89,66 +97,89 @@ __device__ __forceinline__ uint32_t ld32u(const gc_u8 *p) {
 }
 
 // ---- source window ---------------------------------------------------------
-__device__ __forceinline__ uint4 sw_chunk(const Enc &e, int64_t q) {  // 16 bytes at aligned offset q
+template <class SM>
+__device__ __forceinline__ uint4 sw_chunk(const Enc &e, int64_t q) {  // PIECE bytes at aligned offset q
     uint4 v = make_uint4(0, 0, 0, 0);
-    if (q < e.nq) v = e.sa[q >> 4];
+    if (q < e.nq) {
+        if constexpr (SM::PIECE == 16) {
+            v = e.sa[q >> 4];
+        } else {
+            const uint2 w = ((const gc_u2 *)e.sa)[q >> 3];
+            v.x = w.x;
+            v.y = w.y;
+        }
+    }
     return v;
 }
-__device__ __forceinline__ void sw_put(Smem &s, int64_t q, const uint4 &v) {
-    *(uint4 *)(s.sw + (uint32_t)(q & SWMASK)) = v;
+template <class SM>
+__device__ __forceinline__ void sw_put(SM &s, int64_t q, const uint4 &v) {
+    if constexpr (SM::PIECE == 16) *(uint4 *)(s.sw + (uint32_t)(q & SM::SWMASK)) = v;
+    else *(uint2 *)(s.sw + (uint32_t)(q & SM::SWMASK)) = make_uint2(v.x, v.y);
 }
 // (re)fill the window to start at aligned offset wq (multiple of SWSTEP)
-__device__ __forceinline__ void sw_fill(Smem &s, Enc &e, int64_t wq) {
+template <class SM>
+__device__ __forceinline__ void sw_fill(SM &s, Enc &e, int64_t wq) {
     const int l = lane_id();
-    const uint4 a = sw_chunk(e, wq + 16 * l), b = sw_chunk(e, wq + SWSTEP + 16 * l);
-    e.pf = sw_chunk(e, wq + SW + 16 * l);
-    sw_put(s, wq + 16 * l, a);
-    sw_put(s, wq + SWSTEP + 16 * l, b);
+    constexpr int P = SM::PIECE;
+    const uint4 a = sw_chunk<SM>(e, wq + P * l), b = sw_chunk<SM>(e, wq + SM::SWSTEP + P * l);
+    e.pf = sw_chunk<SM>(e, wq + SM::SW + P * l);
+    sw_put(s, wq + P * l, a);
+    sw_put(s, wq + SM::SWSTEP + P * l, b);
     e.wq = wq;
     __builtin_amdgcn_wave_barrier();
 }
 // make source bytes [p, p + len) readable from the window (len <= 16)
-__device__ __forceinline__ void sw_need(Smem &s, Enc &e, int64_t p, int len) {
+template <class SM>
+__device__ __forceinline__ void sw_need(SM &s, Enc &e, int64_t p, int len) {
     const int64_t q = p + e.smis;
-    if (q + len <= e.wq + SW) return;
-    if (q + len <= e.wq + SW + SWSTEP && q >= e.wq + SWSTEP) {
+    if (q + len <= e.wq + SM::SW) return;
+    if (q + len <= e.wq + SM::SW + SM::SWSTEP && q >= e.wq + SM::SWSTEP) {
         // slide by one step: the prefetched chunk replaces the oldest half
         const int l = lane_id();
-        sw_put(s, e.wq + SW + 16 * l, e.pf);
-        e.wq += SWSTEP;
-        e.pf = sw_chunk(e, e.wq + SW + 16 * l);
+        sw_put(s, e.wq + SM::SW + SM::PIECE * l, e.pf);
+        e.wq += SM::SWSTEP;
+        e.pf = sw_chunk<SM>(e, e.wq + SM::SW + SM::PIECE * l);
         __builtin_amdgcn_wave_barrier();
         return;
     }
-    sw_fill(s, e, (q & ~(int64_t)(SWSTEP - 1)) - SWSTEP > 0 ? (q & ~(int64_t)(SWSTEP - 1)) - SWSTEP : 0);
+    // refill: the step holding the last needed byte becomes the window's second half
+    constexpr int64_t ST = SM::SWSTEP;
+    const int64_t w = ((q + len - 1) & ~(ST - 1)) - ST;
+    sw_fill(s, e, w > 0 ? w : 0);
 }
+template <class SM>
 __device__ __forceinline__ bool sw_has(const Enc &e, int64_t p, int len) {
     const int64_t q = p + e.smis;
-    return q >= e.wq && q + len <= e.wq + SW;
+    return q >= e.wq && q + len <= e.wq + SM::SW;
 }
-__device__ __forceinline__ uint32_t sw_rd32(const Smem &s, const Enc &e, int64_t p) {
+template <class SM>
+__device__ __forceinline__ uint32_t sw_rd32(const SM &s, const Enc &e, int64_t p) {
     const uint32_t q = (uint32_t)(p + e.smis);
     const uint32_t a = q & ~3u, sh = q & 3u;
-    const uint32_t w0 = *(const uint32_t *)(s.sw + (a & SWMASK)), w1 = *(const uint32_t *)(s.sw + ((a + 4) & SWMASK));
+    const uint32_t w0 = *(const uint32_t *)(s.sw + (a & SM::SWMASK)), w1 = *(const uint32_t *)(s.sw + ((a + 4) & SM::SWMASK));
     return __builtin_amdgcn_alignbyte(w1, w0, sh);
 }
-__device__ __forceinline__ uint64_t sw_rd64(const Smem &s, const Enc &e, int64_t p) {
+template <class SM>
+__device__ __forceinline__ uint64_t sw_rd64(const SM &s, const Enc &e, int64_t p) {
     const uint32_t q = (uint32_t)(p + e.smis);
     const uint32_t a = q & ~3u, sh = q & 3u;
-    const uint32_t w0 = *(const uint32_t *)(s.sw + (a & SWMASK)), w1 = *(const uint32_t *)(s.sw + ((a + 4) & SWMASK)),
-                   w2 = *(const uint32_t *)(s.sw + ((a + 8) & SWMASK));
+    const uint32_t w0 = *(const uint32_t *)(s.sw + (a & SM::SWMASK)),
+                   w1 = *(const uint32_t *)(s.sw + ((a + 4) & SM::SWMASK)),
+                   w2 = *(const uint32_t *)(s.sw + ((a + 8) & SM::SWMASK));
     return (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32);
 }
 // 8 bytes at p through the window (slides it forward as needed)
-__device__ __forceinline__ uint64_t src64(Smem &s, Enc &e, int64_t p) {
+template <class SM>
+__device__ __forceinline__ uint64_t src64(SM &s, Enc &e, int64_t p) {
     sw_need(s, e, p, 8);
-    if (sw_has(e, p, 8)) return sw_rd64(s, e, p);
+    if (sw_has<SM>(e, p, 8)) return sw_rd64(s, e, p);
     const uint32_t lo = ld32u(e.src + p), hi = ld32u(e.src + p + 4);  // (window just reset below p)
     return (uint64_t)lo | ((uint64_t)hi << 32);
 }
 // 4 bytes at an arbitrary earlier position (window if present, else HBM)
-__device__ __forceinline__ uint32_t src32(const Smem &s, const Enc &e, int64_t p) {
-    if (sw_has(e, p, 4)) return sw_rd32(s, e, p);
+template <class SM>
+__device__ __forceinline__ uint32_t src32(const SM &s, const Enc &e, int64_t p) {
+    if (sw_has<SM>(e, p, 4)) return sw_rd32(s, e, p);
     return ld32u(e.src + p);
 }
 
@@ -161,57 +192,139 @@ __device__ __forceinline__ uint32_t check_of(const Enc &e, uint32_t v) {
     return ((v * 0x9E3779B1u) >> e.pb) << e.pb;  // top (32 - pb) bits
 }
 
-__device__ __forceinline__ uint32_t tget(const Smem &s, uint32_t h, bool u16) {
+// ---- hash table ------------------------------------------------------------
+// Smem<false>: byU32 entries (position | check bits) or byU16 entries.
+// Smem<true> (byU32 only): entry h = the low 17 bits of its position, 16 in
+// lo[h] = ((u16 *)table)[h] and bit 16 in the plane hb = table + 2048 (bit h &
+// 31 of hb[h >> 5]).  A lookup at P decodes it as the unique position == e
+// (mod 2^17) in (P - 2^17, P]; that is the true position while every entry
+// is at least P - 2^17 + 1, which ctab_refresh keeps (see there).  Raw values
+// below: the 17-bit entry (compact), the u32 / u16 entry (otherwise).
+template <class SM>
+__device__ __forceinline__ uint32_t tget(const SM &s, uint32_t h, bool u16) {
+    if constexpr (SM::kCompact)
+        return (uint32_t)((const uint16_t *)s.table)[h] | (((s.table[2048 + (h >> 5)] >> (h & 31)) & 1u) << 16);
     return u16 ? (uint32_t)((const uint16_t *)s.table)[h] : s.table[h];
 }
 // insert position pos whose first 4 bytes are v
-__device__ __forceinline__ void tput(Smem &s, const Enc &e, uint32_t h, uint32_t pos, uint32_t v, bool u16) {
+template <class SM>
+__device__ __forceinline__ void tput(SM &s, const Enc &e, uint32_t h, uint32_t pos, uint32_t v, bool u16) {
+    if constexpr (SM::kCompact) {
+        ((uint16_t *)s.table)[h] = (uint16_t)pos;
+        const uint32_t m = 1u << (h & 31);
+        if (pos & 0x10000u)
+            (void)__hip_atomic_fetch_or(&s.table[2048 + (h >> 5)], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        else
+            (void)__hip_atomic_fetch_and(&s.table[2048 + (h >> 5)], ~m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return;
+    }
     if (u16) ((uint16_t *)s.table)[h] = (uint16_t)pos;
     else s.table[h] = pos | check_of(e, v);
 }
-// can the entry (found for 4 bytes v) be a match?  (byU16: always ask HBM)
+// the search batch's temporary lane tags (a tag never outlives its batch:
+// lanes restore or overwrite it), their read-back, and the restore of an
+// entry read before the batch (compact: only the u16 half was tagged)
+template <class SM>
+__device__ __forceinline__ void ttag(SM &s, uint32_t h, uint32_t tag, bool u16) {
+    if (SM::kCompact || u16) ((uint16_t *)s.table)[h] = (uint16_t)tag;
+    else s.table[h] = tag;
+}
+template <class SM>
+__device__ __forceinline__ uint32_t ttag_rd(const SM &s, uint32_t h, bool u16) {
+    if (SM::kCompact || u16) return (uint32_t)((const uint16_t *)s.table)[h];
+    return s.table[h];
+}
+template <class SM>
+__device__ __forceinline__ void trestore(SM &s, uint32_t h, uint32_t E, bool u16) {
+    if (SM::kCompact || u16) ((uint16_t *)s.table)[h] = (uint16_t)E;
+    else s.table[h] = E;
+}
+// candidate position of raw entry E looked up at position P
+template <class SM>
+__device__ __forceinline__ int64_t tcand(const Enc &e, uint32_t E, int64_t P, bool u16) {
+    if constexpr (SM::kCompact) return P - (int64_t)(((uint32_t)P - E) & 0x1FFFFu);
+    return u16 ? (int64_t)E : (int64_t)(E & e.pmask);
+}
+// can the entry (found for 4 bytes v) be a match?  (byU16, compact: always ask HBM)
+template <class SM>
 __device__ __forceinline__ bool may_match(const Enc &e, uint32_t ent, uint32_t v, bool u16) {
+    if constexpr (SM::kCompact) return true;
     return u16 || (ent & ~e.pmask) == check_of(e, v);
+}
+// Compact table upkeep, before any lookup or insert at pos (wave-uniform):
+// once pos is 32 KiB past the last refresh R, every entry older than
+// pos - 65535 (stale for LZ4's distance check at every later position) is
+// rewritten as pos - 65536 (stale as well).  Between refreshes every entry is
+// >= R - 65536 and every lookup / insert is below R + 32768 + SPAN + 8, so
+// entries span less than 2^17 and decode exactly, here relative to
+// R + 49152 and in the lookups relative to their own position.
+template <class SM>
+__device__ __forceinline__ void ctab_refresh(SM &s, Enc &e, int64_t pos) {
+    if constexpr (SM::kCompact) {
+        if (pos - e.rlast < 32768) return;
+        const int l = lane_id();
+        const uint32_t ref = (uint32_t)(e.rlast + 49152), sent = (uint32_t)(pos - 65536) & 0x1FFFFu;
+        uint16_t *lo = (uint16_t *)s.table;
+        uint32_t *hb = s.table + 2048;
+        __builtin_amdgcn_wave_barrier();
+        for (int k = 0; k < 64; ++k) {
+            const uint32_t h = 64u * (uint32_t)k + (uint32_t)l;
+            const uint32_t E = (uint32_t)lo[h] | (((hb[h >> 5] >> (h & 31)) & 1u) << 16);
+            const int64_t t = (int64_t)ref - (int64_t)((ref - E) & 0x1FFFFu);
+            const uint32_t ne = t + 65535 < pos ? sent : E;
+            lo[h] = (uint16_t)ne;
+            const uint64_t m = __ballot((ne >> 16) & 1u);
+            if (l == 0) *(uint2 *)(hb + 2 * k) = make_uint2((uint32_t)m, (uint32_t)(m >> 32));
+        }
+        __builtin_amdgcn_wave_barrier();
+        e.rlast = pos;
+    }
 }
 
 // staging slot of output position x (mirrors HBM 16-byte alignment)
-__device__ __forceinline__ uint32_t obidx(const Enc &e, int64_t x) { return (uint32_t)((x + e.dmis) & OBMASK); }
+template <class SM>
+__device__ __forceinline__ uint32_t obidx(const Enc &e, int64_t x) { return (uint32_t)((x + e.dmis) & SM::OBMASK); }
 
-__device__ __forceinline__ void oflush2(Smem &s, Enc &e, int64_t to) {
+template <class SM>
+__device__ __forceinline__ void oflush2(SM &s, Enc &e, int64_t to) {
     const int l = lane_id();
     if (to > e.cap) to = e.cap;
     int64_t F = e.F;
     if (to <= F) return;
     int64_t a = F + (int64_t)((16u - ((e.dmis + (uint32_t)F) & 15u)) & 15u);
     if (a > to) a = to;
-    if (l < a - F) e.dst[F + l] = s.ob[obidx(e, F + l)];
+    if (l < a - F) e.dst[F + l] = s.ob[obidx<SM>(e, F + l)];
     int64_t b = a + ((to - a) & ~(int64_t)15);
-    for (int64_t x = a + 16 * l; x < b; x += 1024) *(g_u4 *)(e.dst + x) = *(const uint4 *)(s.ob + obidx(e, x));
-    if (l < to - b) e.dst[b + l] = s.ob[obidx(e, b + l)];
+    for (int64_t x = a + 16 * l; x < b; x += 1024) *(g_u4 *)(e.dst + x) = *(const uint4 *)(s.ob + obidx<SM>(e, x));
+    if (l < to - b) e.dst[b + l] = s.ob[obidx<SM>(e, b + l)];
     e.F = to;
 }
 
-__device__ __forceinline__ void maybe_flush(Smem &s, Enc &e, int64_t keep_from) {
+template <class SM>
+__device__ __forceinline__ void maybe_flush(SM &s, Enc &e, int64_t keep_from) {
     // flush everything below min(op, keep_from) once enough is pending
     int64_t lim = e.op < keep_from ? e.op : keep_from;
-    if (lim - e.F >= OFLUSH) {
+    if (lim - e.F >= SM::OFLUSH) {
         int64_t to = ((lim + e.dmis) & ~(int64_t)15) - e.dmis;
         oflush2(s, e, to);
     }
 }
 
 // one byte written by lane 0 (uniform position)
-__device__ __forceinline__ void put1(Smem &s, Enc &e, uint32_t v) {
-    if (lane_id() == 0) s.ob[obidx(e, e.op)] = (uint8_t)v;
+template <class SM>
+__device__ __forceinline__ void put1(SM &s, Enc &e, uint32_t v) {
+    if (lane_id() == 0) s.ob[obidx<SM>(e, e.op)] = (uint8_t)v;
     e.op++;
 }
 
-__device__ __forceinline__ void put_len(Smem &s, Enc &e, uint32_t len) {
+template <class SM>
+__device__ __forceinline__ void put_len(SM &s, Enc &e, uint32_t len) {
     // 255-run then remainder; lanes write the run in parallel
     const int l = lane_id();
     uint32_t runs = len / 255;
     for (uint32_t k = 0; k < runs; k += 64) {
-        if (k + l < runs) s.ob[obidx(e, e.op + l)] = 255;
+        if (e.op + 64 + 16 - e.F > SM::OB) oflush2(s, e, ((e.op + e.dmis) & ~(int64_t)15) - e.dmis);  // room for 64
+        if (k + l < runs) s.ob[obidx<SM>(e, e.op + l)] = 255;
         e.op += (runs - k < 64 ? runs - k : 64);
         maybe_flush(s, e, INT64_MAX);
     }
@@ -259,7 +372,8 @@ __device__ void copy_direct(Enc &e, int64_t dpos, int64_t spos, int64_t len) {
 }
 
 // copy literals src[from, from+len) into the output
-__device__ __forceinline__ void put_lits(Smem &s, Enc &e, int64_t from, int64_t len, int64_t keep_from,
+template <class SM>
+__device__ __forceinline__ void put_lits(SM &s, Enc &e, int64_t from, int64_t len, int64_t keep_from,
                                          int32_t pre = -1) {
     const int l = lane_id();
     if (len >= 2048) {  // long run: flush the ring (token and length bytes), copy HBM -> HBM
@@ -271,7 +385,7 @@ __device__ __forceinline__ void put_lits(Smem &s, Enc &e, int64_t from, int64_t 
     }
     for (int64_t k = 0; k < len; k += 64) {
         maybe_flush(s, e, keep_from);
-        if (e.op + 64 + 16 - e.F > OB) {
+        if (e.op + 64 + 16 - e.F > SM::OB) {
             // token pending too far back: flush past it (the token is patched in
             // HBM); the 16 bytes of slack hold the offset bytes that follow the
             // run before the next flush, so the ring never wraps onto unflushed bytes
@@ -279,15 +393,16 @@ __device__ __forceinline__ void put_lits(Smem &s, Enc &e, int64_t from, int64_t 
             oflush2(s, e, to);
         }
         int64_t i = k + l;
-        if (i < len) s.ob[obidx(e, e.op + l)] = (k == 0 && pre >= 0) ? (uint8_t)pre : e.src[from + i];
+        if (i < len) s.ob[obidx<SM>(e, e.op + l)] = (k == 0 && pre >= 0) ? (uint8_t)pre : e.src[from + i];
         e.op += (len - k < 64 ? len - k : 64);
     }
 }
 
 // set the token byte at output position tp
-__device__ __forceinline__ void put_token(Smem &s, Enc &e, int64_t tp, uint32_t v) {
+template <class SM>
+__device__ __forceinline__ void put_token(SM &s, Enc &e, int64_t tp, uint32_t v) {
     if (lane_id() == 0) {
-        if (tp >= e.F) s.ob[obidx(e, tp)] = (uint8_t)v;
+        if (tp >= e.F) s.ob[obidx<SM>(e, tp)] = (uint8_t)v;
         else if (tp < e.cap) e.dst[tp] = (uint8_t)v;
     }
 }
@@ -377,7 +492,7 @@ __device__ __forceinline__ int seg_conv(const SegCtl &c, int b, int upto) {
 // The hash table at search position P: for every hash, the latest position
 // before P that the parse inserted (map byte == rv); only the last 65,535
 // positions matter (older entries fail the distance check, like position 0).
-__device__ void seg_table(Smem &s, const Enc &e, const uint8_t *mapr, uint8_t rv, int64_t P) {
+__device__ void seg_table(Smem<false> &s, const Enc &e, const uint8_t *mapr, uint8_t rv, int64_t P) {
     const int l = lane_id();
     for (int k = l; k < 4096; k += 64) s.table[k] = 0;
     __builtin_amdgcn_wave_barrier();
@@ -409,12 +524,13 @@ __device__ void seg_table(Smem &s, const Enc &e, const uint8_t *mapr, uint8_t rv
 // from the segment's start state up to the first search position at or past
 // the segment's end, recording the positions it inserts (map) and its
 // sequences instead of output bytes.
-template <bool SEG>
+template <bool SEG, bool C>
 __global__ __launch_bounds__(64) void lz4_encode_kernel_t(const jfs_dev_block *__restrict__ blocks, int nblk,
                                                          int32_t *__restrict__ ret, const int32_t *__restrict__ todo,
-                                                         SegCtl c) {
-    static_assert(!SEG || JFS_LZ4E_PSEARCH, "segment mode needs the lane-parallel search");
-    __shared__ Smem s;
+                                                         SegCtl c, int only) {
+    static_assert(!(SEG && C), "segment mode keeps the check-bit table");
+    using SM = Smem<C>;
+    __shared__ SM s;
     int b, j = 0;
     if constexpr (SEG) {
         j = blockIdx.x;
@@ -428,6 +544,10 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel_t(const jfs_dev_block *_
     }
     const int l = lane_id();
     const jfs_dev_block d = ((const gc_blk *)blocks)[b];
+    if (only) {  // 1: the byU32 blocks only (the compact kernel's), 2: the others only
+        const bool big = d.src_len >= kSegMinInput && d.src_len <= kMaxInput;
+        if (big != (only == 1)) return;
+    }
     EP_DECL
     Enc e;
     e.src = (const gc_u8 *)d.src;
@@ -442,6 +562,7 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel_t(const jfs_dev_block *_
     e.nq = e.n + e.smis;
     e.wq = 0;
     e.pf = make_uint4(0, 0, 0, 0);
+    e.rlast = 0;
     const gc_u8 *src = e.src;
     const int64_t n = e.n;
     int32_t result;
@@ -461,7 +582,7 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel_t(const jfs_dev_block *_
         e.pmask = e.pb >= 32 ? 0xFFFFFFFFu : ((1u << e.pb) - 1u);
         sw_fill(s, e, 0);
         // empty table: every entry is position 0 (LZ4's zeroed table), with its check bits
-        const uint32_t init = u16 ? 0u : (n >= 4 ? check_of(e, sw_rd32(s, e, 0)) : 0u);
+        const uint32_t init = (u16 || C) ? 0u : (n >= 4 ? check_of(e, sw_rd32(s, e, 0)) : 0u);
         const int64_t mflimitP1 = n - 12 + 1, matchlimit = n - 5;
         int64_t ip = 0, anchor = 0;
         // segment mode: start state, insertion map, sequence list
@@ -515,7 +636,7 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel_t(const jfs_dev_block *_
                 for (int k = l; k < 4096; k += 64) s.table[k] = init;
             }
         } else {
-            for (int k = l; k < 4096; k += 64) s.table[k] = init;
+            for (int k = l; k < (int)(sizeof(s.table) / 4); k += 64) s.table[k] = init;
         }
         __builtin_amdgcn_wave_barrier();
         if (n >= 13) {
@@ -525,8 +646,6 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel_t(const jfs_dev_block *_
                 if (SEG && l == 0 && rec_lo == 0) mapw[0] = rv;
                 ip = 1;
             }
-            uint64_t fv = src64(s, e, ip);  // 8 bytes at the next search position
-            uint32_t fh = hash_of(fv, u16);
             for (;;) {
                 int64_t match;
                 // ---- search (skip schedule: step = searchMatchNb++ >> 6)
@@ -538,7 +657,6 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel_t(const jfs_dev_block *_
                 int64_t pre_ip = -1, pre_m = -1;
                 uint32_t p_ca = 0, p_cb = 1, p_xa = 0, p_xb = 1;
                 int32_t p_lit = -1;
-#if JFS_LZ4E_PSEARCH
                 // Lane-parallel: lane j takes the j-th next position of the
                 // schedule; every lane reads its table entry before any insert
                 // of the batch, which is the serial order exactly when no two
@@ -555,11 +673,12 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel_t(const jfs_dev_block *_
                         hand_k0 = k0;
                         break;
                     }
+                    ctab_refresh(s, e, pk);
                     const int32_t k = k0 + l;
                     const int32_t sk = k == 0 ? 1 : (63 + k) >> 6;
                     const uint32_t inc = dpp_scan_add((uint32_t)sk);
                     const int64_t P = pk + (int64_t)(inc - (uint32_t)sk), Pn = pk + (int64_t)inc;
-                    const bool span = P - pk <= 512;
+                    const bool span = P - pk <= SM::SPAN;
                     const uint64_t endm = __ballot(span && Pn > mflimitP1), spm = __ballot(span);
                     const int jend = endm ? (int)__builtin_ctzll(endm) : 64;
                     const int jspan = ~spm ? (int)__builtin_ctzll(~spm) : 64;
@@ -585,24 +704,18 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel_t(const jfs_dev_block *_
                     // lane m of any such pair has no predecessor in the batch, so
                     // lanes [0, m] are exact and the batch is cut after m.
                     const uint32_t tag = (uint32_t)l + 1u;
-                    if (on) {
-                        if (u16) ((uint16_t *)s.table)[h] = (uint16_t)tag;
-                        else s.table[h] = tag;
-                    }
+                    if (on) ttag(s, h, tag, u16);
                     __builtin_amdgcn_wave_barrier();
                     uint32_t cm = 64u;
                     if (on) {
-                        const uint32_t t = tget(s, h, u16);
+                        const uint32_t t = ttag_rd(s, h, u16);
                         if (t != tag) cm = umin32((uint32_t)l, t - 1u);
                     }
                     const int ncut = (int)dwave_min(cm) + 1;  // 65: no shared hash
                     const int nb = ncut < nl ? ncut : nl;     // lanes [0, nb) are exact
-                    if (on && l >= nb) {  // beyond the cut: pre-batch entries back (same hash, same entry)
-                        if (u16) ((uint16_t *)s.table)[h] = (uint16_t)E;
-                        else s.table[h] = E;
-                    }
-                    const int64_t cand = u16 ? (int64_t)E : (int64_t)(E & e.pmask);
-                    bool pass = l < nb && (u16 || cand + 65535 >= P) && may_match(e, E, cv, u16);
+                    if (on && l >= nb) trestore(s, h, E, u16);  // beyond the cut: pre-batch entries back (same hash, same entry)
+                    const int64_t cand = tcand<SM>(e, E, P, u16);
+                    bool pass = l < nb && (u16 || cand + 65535 >= P) && may_match<SM>(e, E, cv, u16);
                     const uint64_t pm0 = __ballot(pass);
                     if (pm0) {
                         EPC(9);
@@ -625,8 +738,7 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel_t(const jfs_dev_block *_
                             tput(s, e, h, (uint32_t)P, cv, u16);
                             if (SEG && P >= rec_lo) mapw[P] = rv;
                         }
-                        else if (u16) ((uint16_t *)s.table)[h] = (uint16_t)E;
-                        else s.table[h] = E;
+                        else trestore(s, h, E, u16);
                     }
                     __builtin_amdgcn_wave_barrier();
                     if (hm) {
@@ -638,34 +750,6 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel_t(const jfs_dev_block *_
                     if (nb == nl && endm && jend <= jspan && jend <= jstop) { last = true; break; }  // the schedule passed mflimit
                     pk += (int64_t)readlane(inc, nb - 1);
                     k0 += nb;
-                }
-                if (false)
-#endif
-                {
-                    int64_t fip = ip;
-                    int32_t step = 1, snb = 1 << 6;
-                    for (;;) {
-                        const uint32_t h = fh;
-                        const int64_t cur = fip;
-                        const uint32_t cv = (uint32_t)fv;
-                        const uint32_t ent = tget(s, h, u16);
-                        ip = fip;
-                        fip += step;
-                        step = snb++ >> 6;
-                        if (fip > mflimitP1) { last = true; break; }
-                        match = u16 ? ent : (ent & e.pmask);
-                        fv = src64(s, e, fip);
-                        fh = hash_of(fv, u16);
-                        tput(s, e, h, (uint32_t)cur, cv, u16);
-                        EPC(7);
-                        if (!u16 && match + 65535 < cur) continue;
-                        if (!may_match(e, ent, cv, u16)) continue;
-                        EP(0);
-                        EPC(9);
-                        const bool hit = src32(s, e, match) == cv;
-                        EP(1);
-                        if (hit) break;
-                    }
                 }
                 EP(0);
                 if (last) break;
@@ -759,8 +843,9 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel_t(const jfs_dev_block *_
                     if (ip >= mflimitP1) break;
                     // bytes at ip - 2 and ip: one window check, both reads issued together
                     uint64_t v2, vi;
+                    ctab_refresh(s, e, ip);
                     sw_need(s, e, ip + 2, 8);
-                    if (sw_has(e, ip - 2, 12)) {
+                    if (sw_has<SM>(e, ip - 2, 12)) {
                         v2 = sw_rd64(s, e, ip - 2);
                         vi = sw_rd64(s, e, ip);
                     } else {
@@ -770,13 +855,13 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel_t(const jfs_dev_block *_
                     tput(s, e, hash_of(v2, u16), (uint32_t)(ip - 2), (uint32_t)v2, u16);
                     const uint32_t h = hash_of(vi, u16);
                     const uint32_t ent = tget(s, h, u16);
-                    const uint32_t mi = u16 ? ent : (ent & e.pmask);
+                    const int64_t mi = tcand<SM>(e, ent, ip, u16);
                     tput(s, e, h, (uint32_t)ip, (uint32_t)vi, u16);
                     if (SEG && l == 0) {
                         if (ip - 2 >= rec_lo) mapw[ip - 2] = rv;
                         if (ip >= rec_lo) mapw[ip] = rv;
                     }
-                    bool rm = (u16 || (int64_t)mi + 65535 >= ip) && may_match(e, ent, (uint32_t)vi, u16);
+                    bool rm = (u16 || mi + 65535 >= ip) && may_match<SM>(e, ent, (uint32_t)vi, u16);
                     if (rm) {  // the 4-byte check and the first 64 extension bytes in one round trip
                         const int64_t ax = ip + 4 + l, dlt = ip - (int64_t)mi;
                         uint32_t xa = 0, xb = 1;
@@ -803,8 +888,6 @@ __global__ __launch_bounds__(64) void lz4_encode_kernel_t(const jfs_dev_block *_
                 if (SEG && ovf) break;
                 if (anchor >= mflimitP1) break;
                 ++ip;
-                fv = src64(s, e, ip);
-                fh = hash_of(fv, u16);
                 EP(0);
             }
         }
@@ -1075,8 +1158,12 @@ using jfs::lz4e::SegCtl;
 
 extern "C" int jfs_launch_lz4_encode(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, hipStream_t stream) {
     if (nblk <= 0) return 0;
-    hipLaunchKernelGGL(jfs::lz4e::lz4_encode_kernel_t<false>, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, d_ret,
-                       (const int32_t *)nullptr, SegCtl{});
+    // byU32 blocks (>= 64 KiB + 11) on the compact-table kernel (16 per CU),
+    // the rest on the check-bit kernel; each grid skips the other's blocks
+    hipLaunchKernelGGL((jfs::lz4e::lz4_encode_kernel_t<false, true>), dim3(nblk), dim3(64), 0, stream, d_blocks, nblk,
+                       d_ret, (const int32_t *)nullptr, SegCtl{}, 1);
+    hipLaunchKernelGGL((jfs::lz4e::lz4_encode_kernel_t<false, false>), dim3(nblk), dim3(64), 0, stream, d_blocks, nblk,
+                       d_ret, (const int32_t *)nullptr, SegCtl{}, 2);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -1189,16 +1276,16 @@ extern "C" int jfs_launch_lz4_encode_seg(const jfs_dev_block *d_blocks, int nblk
     if (S > 0) {
         for (int r = 1; r <= R; ++r) {
             c.round = r;
-            hipLaunchKernelGGL(lz4_encode_kernel_t<true>, dim3((unsigned)S), dim3(64), 0, st, d_blocks, nblk, d_ret,
-                               (const int32_t *)nullptr, c);
+            hipLaunchKernelGGL((lz4_encode_kernel_t<true, false>), dim3((unsigned)S), dim3(64), 0, st, d_blocks, nblk,
+                               d_ret, (const int32_t *)nullptr, c, 0);
             if (r >= 2) hipLaunchKernelGGL(eseg_cmp_kernel, dim3(nchunk, (unsigned)B), dim3(256), 0, st, c);
         }
         hipLaunchKernelGGL(eseg_size_kernel, dim3((unsigned)S), dim3(64), 0, st, c, R);
         hipLaunchKernelGGL(eseg_emit_kernel, dim3((unsigned)S), dim3(64), 0, st, d_blocks, d_ret, c, R);
     }
     // blocks below the segment size, unsettled or overflowed: the serial parse
-    hipLaunchKernelGGL(lz4_encode_kernel_t<false>, dim3(nblk), dim3(64), 0, st, d_blocks, nblk, d_ret,
-                       (const int32_t *)c.todo, SegCtl{});
+    hipLaunchKernelGGL((lz4_encode_kernel_t<false, false>), dim3(nblk), dim3(64), 0, st, d_blocks, nblk, d_ret,
+                       (const int32_t *)c.todo, SegCtl{}, 0);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

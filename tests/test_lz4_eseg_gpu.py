@@ -113,3 +113,55 @@ def test_eseg_many_blocks_and_batch_api(gpu, oracle):
     res = c.CompressBatch(pairs)
     for (d, s), (n, err) in zip(pairs, res):
         assert err is None and bytes(d[:n]) == oracle.lz4_compress(s)[1]
+
+
+def _encode_device(srcs):
+    """jfs_lz4_compress_device results (bytes / 0): the large-batch path, whose
+    byU32 blocks take the compact-table kernel (lz4_encode.hip, Smem<true>)."""
+    dev = torch.device("cuda:0")
+    caps = [D.lz4_bound(len(s)) for s in srcs]
+    soff = np.cumsum([0] + [(len(s) + 255) // 256 * 256 for s in srcs])
+    doff = np.cumsum([0] + [(c + 255) // 256 * 256 for c in caps])
+    raw = torch.zeros(int(soff[-1]) + 256, dtype=torch.uint8)
+    for i, s in enumerate(srcs):
+        if s:
+            raw[int(soff[i]):int(soff[i]) + len(s)] = torch.frombuffer(bytearray(s), dtype=torch.uint8)
+    raw = raw.to(dev)
+    comp = torch.zeros(int(doff[-1]) + 256, dtype=torch.uint8, device=dev)
+    desc = D.make_desc(raw, soff[:-1], [len(s) for s in srcs], comp, doff[:-1], caps)
+    ret = torch.zeros(len(srcs), dtype=torch.int32, device=dev)
+    D.lz4_compress(desc, ret)
+    torch.cuda.synchronize()
+    r = ret.cpu().numpy()
+    host = comp.cpu().numpy()
+    return [bytes(host[int(doff[i]):int(doff[i]) + int(r[i])]) if r[i] > 0 else int(r[i]) for i in range(len(srcs))]
+
+
+def test_compact_table_kernel_exact(gpu, oracle):
+    """The large-batch kernel keeps 17-bit position entries (u16 + a bit plane)
+    refreshed every 32 KiB, a 512-byte output ring and a 1 KiB source window
+    (16 blocks per CU); its output must stay LZ4_compress_default's: matches at
+    exactly 65,535 / 65,536 bytes back, entries going stale across long
+    matches and long skip-schedule jumps, a long literal run right before a
+    long match (the ring's room), the byU16/byU32 switch at 65,547."""
+    srcs = []
+    r = gen_block("R", 61, 65535)
+    srcs.append(r + r + r[:3000])                       # distance 65,535: matches allowed
+    r = gen_block("R", 62, 65536)
+    srcs.append(r + r + r[:3000])                       # distance 65,536: too far
+    r = gen_block("R", 63, 65537)
+    srcs.append(r + gen_block("T", 64, 40000) + r)      # stale entries, then text
+    for lit in (430, 470, 500, 1990, 2040):
+        b = bytearray(gen_block("T", 40 + lit, 300000))
+        b[100000:100000 + lit] = gen_block("R", lit, lit)
+        b[100000 + lit:100000 + lit + 5000] = bytes(5000)
+        srcs.append(bytes(b))
+    for i, z in enumerate((70000, 140000, 300000)):    # long matches jump past refreshes
+        srcs.append(gen_block("T", 70 + i, 200000) + bytes(z) + gen_block("T", 70 + i, 150000))
+    srcs += [_mixed(80 + i, (4 << 20) - 13 * i, 20) for i in range(3)]
+    srcs += [gen_block("R", 90, 1 << 20), gen_block("Z", 91, 1 << 20), gen_block("T", 92, 65547),
+             gen_block("T", 93, 65546), gen_block("T", 94, 3 * 131072 + 5), gen_block("T", 95, 16 << 20),
+             gen_block("R", 96, 300000) + gen_block("T", 96, 300000)]
+    got = _encode_device(srcs)
+    for i, s in enumerate(srcs):
+        assert got[i] == oracle.lz4_compress(s)[1], (i, len(s))
