@@ -45,7 +45,10 @@ inline int64_t align16(int64_t x) { return (x + 15) & ~(int64_t)15; }
 // One pinned host + device staging area: chunk k of a batch uses slot
 // k % NSLOT, so chunk k+1's H2D and chunk k-1's D2H run while chunk k's
 // kernel runs.
-constexpr int NSLOT = 3;
+#ifndef JFS_NSLOT
+#define JFS_NSLOT 3
+#endif
+constexpr int NSLOT = JFS_NSLOT;
 // disk-cache checksum piece (pkg/chunk/disk_cache_file.go:139-152: csBlock)
 constexpr int64_t CSUM_SEG = 32 << 10;
 

@@ -1158,8 +1158,22 @@ using jfs::lz4e::SegCtl;
 
 extern "C" int jfs_launch_lz4_encode(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, hipStream_t stream) {
     if (nblk <= 0) return 0;
-    // byU32 blocks (>= 64 KiB + 11) on the compact-table kernel (16 per CU),
-    // the rest on the check-bit kernel; each grid skips the other's blocks
+    // More blocks than the 20 KiB kernel holds at once (8 per CU): byU32
+    // blocks (>= 64 KiB + 11) on the compact-table kernel (16 per CU), the
+    // rest on the check-bit kernel, each grid skipping the other's blocks.
+    // Smaller batches all take the check-bit kernel: resident either way, its
+    // parse is 19 % faster (no HBM compare per candidate).
+    static int ncu = [] {
+        int dev = 0, v = 0;
+        (void)hipGetDevice(&dev);
+        return hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0 ? v : 256;
+    }();
+    const char *force = getenv("JFS_LZ4E_COMPACT");  // "1" / "0": always / never (tests, experiments)
+    if (force ? force[0] == '0' : nblk <= 8 * ncu) {
+        hipLaunchKernelGGL((jfs::lz4e::lz4_encode_kernel_t<false, false>), dim3(nblk), dim3(64), 0, stream, d_blocks,
+                           nblk, d_ret, (const int32_t *)nullptr, SegCtl{}, 0);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     hipLaunchKernelGGL((jfs::lz4e::lz4_encode_kernel_t<false, true>), dim3(nblk), dim3(64), 0, stream, d_blocks, nblk,
                        d_ret, (const int32_t *)nullptr, SegCtl{}, 1);
     hipLaunchKernelGGL((jfs::lz4e::lz4_encode_kernel_t<false, false>), dim3(nblk), dim3(64), 0, stream, d_blocks, nblk,

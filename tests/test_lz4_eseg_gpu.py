@@ -7,6 +7,7 @@ uses the result only once a round changes nothing; blocks that do not settle
 Checked against the CPU oracle (oracle/lz4_oracle.c, pinned by liblz4 1.9.3
 golden vectors) and against the serial GPU kernel, on text, zero, random and
 mixed blocks whose content changes at the segment boundaries."""
+import os
 import random
 
 import numpy as np
@@ -162,6 +163,10 @@ def test_compact_table_kernel_exact(gpu, oracle):
     srcs += [gen_block("R", 90, 1 << 20), gen_block("Z", 91, 1 << 20), gen_block("T", 92, 65547),
              gen_block("T", 93, 65546), gen_block("T", 94, 3 * 131072 + 5), gen_block("T", 95, 16 << 20),
              gen_block("R", 96, 300000) + gen_block("T", 96, 300000)]
-    got = _encode_device(srcs)
+    os.environ["JFS_LZ4E_COMPACT"] = "1"  # small batches take the check-bit kernel by default
+    try:
+        got = _encode_device(srcs)
+    finally:
+        del os.environ["JFS_LZ4E_COMPACT"]
     for i, s in enumerate(srcs):
         assert got[i] == oracle.lz4_compress(s)[1], (i, len(s))
