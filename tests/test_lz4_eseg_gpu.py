@@ -116,11 +116,11 @@ def test_eseg_many_blocks_and_batch_api(gpu, oracle):
         assert err is None and bytes(d[:n]) == oracle.lz4_compress(s)[1]
 
 
-def _encode_device(srcs):
+def _encode_device(srcs, caps=None):
     """jfs_lz4_compress_device results (bytes / 0): the large-batch path, whose
     byU32 blocks take the compact-table kernel (lz4_encode.hip, Smem<true>)."""
     dev = torch.device("cuda:0")
-    caps = [D.lz4_bound(len(s)) for s in srcs]
+    caps = caps or [D.lz4_bound(len(s)) for s in srcs]
     soff = np.cumsum([0] + [(len(s) + 255) // 256 * 256 for s in srcs])
     doff = np.cumsum([0] + [(c + 255) // 256 * 256 for c in caps])
     raw = torch.zeros(int(soff[-1]) + 256, dtype=torch.uint8)
@@ -170,3 +170,33 @@ def test_compact_table_kernel_exact(gpu, oracle):
         del os.environ["JFS_LZ4E_COMPACT"]
     for i, s in enumerate(srcs):
         assert got[i] == oracle.lz4_compress(s)[1], (i, len(s))
+
+
+def test_compact_table_kernel_golden_and_limited_output(gpu, golden):
+    """liblz4 1.9.3's own bytes (golden sha256) and its limited-output results
+    (0 when the block does not fit in dst_cap) through the compact kernel."""
+    import hashlib
+    cache, srcs, caps, want = {}, [], [], []
+    for b in golden["lz4"]["blocks"]:
+        srcs.append(gen_block(b["cls"], b["seed"], b["size"]))
+        caps.append(D.lz4_bound(b["size"]))
+        want.append(("sha", b["csize"], b["comp_sha"]))
+    for e in golden["lz4"]["limited"]:
+        key = (e["cls"], e["seed"], e["size"])
+        if key not in cache:
+            cache[key] = gen_block(*key)
+        srcs.append(cache[key])
+        caps.append(e["cap"])
+        want.append(("ret", e["ret"], None))
+    os.environ["JFS_LZ4E_COMPACT"] = "1"
+    try:
+        got = _encode_device(srcs, caps)
+    finally:
+        del os.environ["JFS_LZ4E_COMPACT"]
+    for i, (kind, n, sh) in enumerate(want):
+        if kind == "sha":
+            assert isinstance(got[i], bytes) and len(got[i]) == n and hashlib.sha256(got[i]).hexdigest() == sh, i
+        elif n == 0:
+            assert got[i] == 0, (i, caps[i])
+        else:
+            assert isinstance(got[i], bytes) and len(got[i]) == n, (i, caps[i])
