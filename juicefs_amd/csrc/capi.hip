@@ -1223,6 +1223,10 @@ struct Pending {
     jfs_iov iov;
     int64_t res;
     bool done;
+    // the caller's own wake-up: a release wakes only the callers it answers
+    // (one shared condition woke all ~200 waiting callers per released chunk,
+    // each re-taking the queue mutex that the gathering worker needs)
+    std::condition_variable cv;
 };
 
 // Gather window (microseconds): a worker that finds work waits until no new
@@ -1307,12 +1311,12 @@ class Coalescer {
         std::vector<DevCtx *> &ds = devices();
         if (ds.empty()) return JFS_ERR_NO_DEVICE;
         start(ds);
-        Pending p{algo, dir, iov, 0, false};
+        Pending p{algo, dir, iov, 0, false, {}};
         std::unique_lock<std::mutex> lk(mu_);
         q_.push_back(&p);
         arrivals_++;
         cv_work_.notify_all();
-        cv_done_.wait(lk, [&] { return p.done; });
+        p.cv.wait(lk, [&] { return p.done; });
         return p.res;
     }
 
@@ -1322,7 +1326,7 @@ class Coalescer {
     // pipelined chunks of at most chunk_limit() staging bytes.
     static constexpr int kMaxBlocks = 4096;
     std::mutex mu_;
-    std::condition_variable cv_work_, cv_done_;
+    std::condition_variable cv_work_;
     std::deque<Pending *> q_;
     uint64_t arrivals_ = 0;
     bool gathering_ = false;  // one worker gathers at a time; the others run batches
@@ -1422,16 +1426,14 @@ class Coalescer {
                     std::vector<char> prel(np, 0);
                     for (int k = 0; k < np; k++) piov[k] = iov[idx[k]];
                     const std::function<void(int, int)> release = [&](int s, int e) {
-                        {
-                            std::lock_guard<std::mutex> lk(mu_);
-                            for (int k = s; k < e; k++) {
-                                batch[idx[k]]->res = pout[k];
-                                batch[idx[k]]->done = true;
-                                released[idx[k]] = 1;
-                                prel[k] = 1;
-                            }
+                        std::lock_guard<std::mutex> lk(mu_);
+                        for (int k = s; k < e; k++) {
+                            batch[idx[k]]->res = pout[k];
+                            batch[idx[k]]->done = true;
+                            batch[idx[k]]->cv.notify_one();
+                            released[idx[k]] = 1;
+                            prel[k] = 1;
                         }
-                        cv_done_.notify_all();
                     };
                     if (run_batch(d, L, algo, dir, np, piov.data(), pout.data(), nullptr, nullptr, cb, &release) !=
                         JFS_OK) {
@@ -1466,9 +1468,9 @@ class Coalescer {
                     if (released[i]) continue;
                     batch[i]->res = out[i];
                     batch[i]->done = true;
+                    batch[i]->cv.notify_one();
                 }
             }
-            cv_done_.notify_all();
         }
     }
 };
