@@ -44,12 +44,11 @@ inline int64_t align16(int64_t x) { return (x + 15) & ~(int64_t)15; }
 
 // One pinned host + device staging area: chunk k of a batch uses slot
 // k % NSLOT, so chunk k+1's H2D and chunk k-1's D2H run while chunk k's
-// kernel runs.  Four slots let a long decode stage its first full chunk while
-// the three ramp chunks are still in flight (with three it waited for ramp
-// chunk 0's copy-out): 4,096 x 4 MiB host-to-host 42.0 -> 42.8 GiB/s, and with
-// the smaller first full chunk below 43.4 (3 interleaved runs each).
+// kernel runs.  (Four slots measured 42.8 vs 42.0 GiB/s on a lone 4,096-block
+// host-to-host decode, but 28 vs 41 right after a configs[0] round trip had
+// grown the staging: kept at three.)
 #ifndef JFS_NSLOT
-#define JFS_NSLOT 4
+#define JFS_NSLOT 3
 #endif
 constexpr int NSLOT = JFS_NSLOT;
 // disk-cache checksum piece (pkg/chunk/disk_cache_file.go:139-152: csBlock)
