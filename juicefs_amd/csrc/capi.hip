@@ -64,8 +64,13 @@ int64_t staging_max_bytes() {
     return v;
 }
 
+// The output D2H of a (non-encrypted) chunk goes in up to NPIECE pieces, each
+// with its own event, so the host copy-out of a piece overlaps the D2H of the
+// next -- at the end of a batch only the last piece's copy-out is left.
+constexpr int NPIECE = 4;
 struct Slot {
     hipEvent_t ev_in = nullptr, ev_k = nullptr, ev = nullptr;  // H2D done, kernel done, D2H done
+    hipEvent_t ev_p[NPIECE] = {};                              // output piece p landed
     uint8_t *h = nullptr;
     int64_t h_cap = 0;
     uint8_t *d = nullptr;
@@ -303,6 +308,8 @@ void init_devices() {
                 ok = ok && hipEventCreateWithFlags(&sl.ev_in, hipEventDisableTiming) == hipSuccess;
                 ok = ok && hipEventCreateWithFlags(&sl.ev_k, hipEventDisableTiming) == hipSuccess;
                 ok = ok && hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming) == hipSuccess;
+                for (hipEvent_t &e : sl.ev_p)
+                    ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
             }
         }
         if (!ok) {
@@ -755,6 +762,11 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
     const int64_t zib = zplan ? (int64_t)jfs_zstd_info_bytes() : 0;
     // aead extras per block: descriptor, second result, 64 bytes of key (32) + nonce (12)
     const int64_t aeb = ae ? (int64_t)sizeof(jfs_aead_block) + 4 + 64 : 0;
+    // output pieces of a chunk (see NPIECE): blocks [piece_b(c, p), piece_b(c, p + 1))
+    auto npiece = [&](const Chunk &c) { return std::max(1, std::min(NPIECE, c.e - c.s)); };
+    auto piece_b = [&](const Chunk &c, int p) {
+        return c.s + (int)((int64_t)(c.e - c.s) * p / npiece(c));
+    };
     auto layout = [&](const Chunk &c, uint8_t *base, uint8_t **in, uint8_t **outp, jfs_dev_block **desc, int32_t **ret,
                       uint8_t **zinfo) {
         const int64_t desc_bytes = align16((int64_t)(c.e - c.s) * (int64_t)sizeof(jfs_dev_block));
@@ -1081,15 +1093,22 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
             return JFS_ERR_HIP;
         if (dir == COMPRESS && fetch_crc(c, sl) != JFS_OK) return JFS_ERR_HIP;
         if (fetch_csum(c, sl) != JFS_OK) return JFS_ERR_HIP;
-        if (hipMemcpyAsync(h_out, d_out, (size_t)c.tout, hipMemcpyDeviceToHost, dev->s_out) != hipSuccess)
-            return JFS_ERR_HIP;
+        for (int p = 0; p < npiece(c); p++) {  // blocks [piece_b(c, p), piece_b(c, p + 1))
+            const int b0 = piece_b(c, p), b1 = piece_b(c, p + 1);
+            const int64_t o0 = out_off[b0], o1 = b1 < c.e ? out_off[b1] : c.tout;
+            if (o1 > o0 && hipMemcpyAsync(h_out + o0, d_out + o0, (size_t)(o1 - o0), hipMemcpyDeviceToHost,
+                                          dev->s_out) != hipSuccess)
+                return JFS_ERR_HIP;
+            if (hipEventRecord(sl.ev_p[p], dev->s_out) != hipSuccess) return JFS_ERR_HIP;
+        }
         if (hipEventRecord(sl.ev, dev->s_out) != hipSuccess) return JFS_ERR_HIP;
         return JFS_OK;
     };
     auto finish = [&](const Chunk &c) -> int64_t {
         Slot &sl = ln.slot[c.slot];
         const double t0 = host_trace() ? now_ms() : 0.0;
-        if (hipEventSynchronize(sl.ev) != hipSuccess) return JFS_ERR_HIP;
+        // (results, CRCs and checksums land before the first output piece)
+        if (hipEventSynchronize(ae ? sl.ev : sl.ev_p[0]) != hipSuccess) return JFS_ERR_HIP;
         const double t1 = host_trace() ? now_ms() : 0.0;
         uint8_t *h_in, *h_out, *h_zi;
         jfs_dev_block *h_desc;
@@ -1134,10 +1153,13 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
                 }
             }
         } else {
-            for (int i = c.s; i < c.e; i++) {
-                const int64_t r = finish_result(algo, dir, h_ret[i - c.s]);
-                if (r > 0) jobs.push_back({iov[i].dst, h_out + out_off[i], r});
-                out[i] = r;
+            for (int i = c.s; i < c.e; i++) out[i] = finish_result(algo, dir, h_ret[i - c.s]);
+            for (int p = 0; p < npiece(c); p++) {  // each piece's copy-out as soon as it landed
+                if (p > 0 && hipEventSynchronize(sl.ev_p[p]) != hipSuccess) return JFS_ERR_HIP;
+                std::vector<CopyJob> pj;
+                for (int i = piece_b(c, p); i < piece_b(c, p + 1); i++)
+                    if (out[i] > 0) pj.push_back({iov[i].dst, h_out + out_off[i], out[i]});
+                par_copy(pj);
             }
         }
         if (crc_out) {
