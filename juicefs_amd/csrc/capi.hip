@@ -67,7 +67,10 @@ int64_t staging_max_bytes() {
 // The output D2H of a (non-encrypted) chunk goes in up to NPIECE pieces, each
 // with its own event, so the host copy-out of a piece overlaps the D2H of the
 // next -- at the end of a batch only the last piece's copy-out is left.
-constexpr int NPIECE = 4;
+#ifndef JFS_NPIECE
+#define JFS_NPIECE 4
+#endif
+constexpr int NPIECE = JFS_NPIECE;
 struct Slot {
     hipEvent_t ev_in = nullptr, ev_k = nullptr, ev = nullptr;  // H2D done, kernel done, D2H done
     hipEvent_t ev_p[NPIECE] = {};                              // output piece p landed
