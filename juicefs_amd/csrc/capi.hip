@@ -1024,17 +1024,29 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
         int32_t *h_ret, *d_ret;
         layout(c, sl.h, &h_in, &h_out, &h_desc, &h_ret, &h_zi);
         layout(c, sl.d, &d_in, &d_out, &d_desc, &d_ret, &d_zi);
-        std::vector<CopyJob> jobs;
         for (int i = c.s; i < c.e; i++) {
             const int k = i - c.s;
-            if (iov[i].src_len > 0) jobs.push_back({h_in + in_off[i], iov[i].src, iov[i].src_len});
             h_desc[k].src = d_in + in_off[i];
             h_desc[k].dst = d_out + out_off[i];
             h_desc[k].src_len = (int32_t)iov[i].src_len;
             h_desc[k].dst_cap = (int32_t)std::min<int64_t>(cap[i], INT32_MAX);
         }
         const double t0 = host_trace() ? now_ms() : 0.0;
-        par_copy(jobs);
+        // Stage the inputs in pieces (NPIECE), each piece's H2D issued as soon as
+        // it is staged so that it overlaps the staging of the next (the
+        // encrypted path stages everything first: launch_aead issues its H2D).
+        for (int p = 0; p < npiece(c); p++) {
+            const int b0 = piece_b(c, p), b1 = piece_b(c, p + 1);
+            std::vector<CopyJob> jobs;
+            for (int i = b0; i < b1; i++)
+                if (iov[i].src_len > 0) jobs.push_back({h_in + in_off[i], iov[i].src, iov[i].src_len});
+            par_copy(jobs);
+            if (ae) continue;
+            const int64_t o0 = in_off[b0], o1 = b1 < c.e ? in_off[b1] : c.tin;
+            if (o1 > o0 && hipMemcpyAsync(d_in + o0, h_in + o0, (size_t)(o1 - o0), hipMemcpyHostToDevice, dev->s_in) !=
+                               hipSuccess)
+                return JFS_ERR_HIP;
+        }
         if (host_trace())
             fprintf(stderr, "[jfs host] t=%.2f chunk %d-%d stage-in %.1f MiB %.2f ms\n", now_ms(), c.s, c.e,
                     c.tin / 1048576.0, now_ms() - t0);
@@ -1054,7 +1066,6 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
             if (!sl.ensure_zstd(ztot)) return JFS_ERR_NO_MEMORY;
             if (jfs_zstd_split_ok(n, ztot) && !sl.ensure_split(jfs_zstd_split_bytes(n, ztot))) return JFS_ERR_NO_MEMORY;
         }
-        if (hipMemcpyAsync(d_in, h_in, (size_t)c.tin, hipMemcpyHostToDevice, dev->s_in) != hipSuccess) return JFS_ERR_HIP;
         if (hipMemcpyAsync(d_desc, h_desc, (size_t)n * sizeof(jfs_dev_block), hipMemcpyHostToDevice, dev->s_in) !=
             hipSuccess)
             return JFS_ERR_HIP;
