@@ -766,7 +766,9 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
     // aead extras per block: descriptor, second result, 64 bytes of key (32) + nonce (12)
     const int64_t aeb = ae ? (int64_t)sizeof(jfs_aead_block) + 4 + 64 : 0;
     // output pieces of a chunk (see NPIECE): blocks [piece_b(c, p), piece_b(c, p + 1))
-    auto npiece = [&](const Chunk &c) { return std::max(1, std::min(NPIECE, c.e - c.s)); };
+    // (small chunks -- the coalescer's 16-block ones -- stay whole: a piece's
+    // host copy is a thread-pool round of its own)
+    auto npiece = [&](const Chunk &c) { return c.e - c.s >= 64 ? std::min(NPIECE, c.e - c.s) : 1; };
     auto piece_b = [&](const Chunk &c, int p) {
         return c.s + (int)((int64_t)(c.e - c.s) * p / npiece(c));
     };
