@@ -51,6 +51,7 @@ inline int64_t align16(int64_t x) { return (x + 15) & ~(int64_t)15; }
 #define JFS_NSLOT 3
 #endif
 constexpr int NSLOT = JFS_NSLOT;
+static_assert(NSLOT >= 2, "the staging pipeline overlaps a chunk's copies with the next chunk's");
 // disk-cache checksum piece (pkg/chunk/disk_cache_file.go:139-152: csBlock)
 constexpr int64_t CSUM_SEG = 32 << 10;
 
@@ -71,6 +72,7 @@ int64_t staging_max_bytes() {
 #define JFS_NPIECE 4
 #endif
 constexpr int NPIECE = JFS_NPIECE;
+static_assert(NPIECE >= 1, "at least one output piece per chunk (finish() waits on ev_p[npiece - 1])");
 struct Slot {
     hipEvent_t ev_in = nullptr, ev_k = nullptr, ev = nullptr;  // H2D done, kernel done, D2H done
     hipEvent_t ev_p[NPIECE] = {};                              // output piece p landed
@@ -473,7 +475,7 @@ int64_t chunk_limit() {
 int host_ramp_len() {
     static int v = [] {
         const char *e = getenv("JFS_HOST_RAMP");
-        return e ? std::max(0, atoi(e)) : 3;
+        return e ? std::min(8, std::max(0, atoi(e))) : 3;  // 32 << k stays well inside int
     }();
     return v;
 }
@@ -1347,6 +1349,44 @@ int64_t spread_min_bytes() {
     return v;
 }
 
+// The lanes a coalescer worker runs a gathered burst on: its own lane, and
+// (spreading) one idle lane of each other device, at most
+// `parts - 1` of them.  Lock order, so that no two workers can deadlock: the
+// own lane is taken first and blocking, while the worker holds nothing else;
+// other devices' lanes are only ever try-locked, so no thread ever waits while
+// holding a lane that another thread waits for.  (Round 4 try-locked the
+// foreign lanes first and then blocked on its own: two workers could each
+// hold the other's lane.)  Host-only logic: jfs_test_spread_locking runs it on
+// fake devices.
+struct SpreadLanes {
+    std::unique_lock<std::mutex> own;
+    std::vector<DevCtx *> hdev;
+    std::vector<Lane *> hlane;
+    std::vector<std::unique_lock<std::mutex>> hlock;
+    void release() {
+        hlock.clear();
+        hlane.clear();
+        hdev.clear();
+        if (own.owns_lock()) own.unlock();
+    }
+};
+
+void spread_acquire(DevCtx *dev, Lane &ln, const std::vector<DevCtx *> &all, int parts, SpreadLanes &sl) {
+    sl.own = std::unique_lock<std::mutex>(ln.mu);
+    for (DevCtx *d : all) {
+        if (d == dev || (int)sl.hdev.size() + 1 >= parts) continue;
+        for (int k = 0; k < NLANE; k++) {
+            std::unique_lock<std::mutex> t(d->lane[k].mu, std::try_to_lock);
+            if (t.owns_lock()) {
+                sl.hdev.push_back(d);
+                sl.hlane.push_back(&d->lane[k]);
+                sl.hlock.push_back(std::move(t));
+                break;
+            }
+        }
+    }
+}
+
 class Coalescer {
    public:
     static Coalescer &get() {
@@ -1436,26 +1476,13 @@ class Coalescer {
                 // Other devices with an idle lane take a size-balanced share of
                 // the gathered burst: their lanes are locked here
                 // and released after their parts finish.
-                std::vector<DevCtx *> hdev;
-                std::vector<Lane *> hlane;
-                std::vector<std::unique_lock<std::mutex>> hlock;
                 std::vector<int64_t> cost(n);
                 int64_t tot = 0;
                 for (int i = 0; i < n; i++) tot += (cost[i] = block_cost(iov[i]));
-                if (n >= 2 && tot >= spread_min_bytes()) {
-                    for (DevCtx *d : devices()) {
-                        if (d == dev || (int)hdev.size() + 1 >= n) continue;
-                        for (int k = 0; k < NLANE; k++) {
-                            std::unique_lock<std::mutex> t(d->lane[k].mu, std::try_to_lock);
-                            if (t.owns_lock()) {
-                                hdev.push_back(d);
-                                hlane.push_back(&d->lane[k]);
-                                hlock.push_back(std::move(t));
-                                break;
-                            }
-                        }
-                    }
-                }
+                SpreadLanes sl;
+                spread_acquire(dev, ln, devices(), n >= 2 && tot >= spread_min_bytes() ? n : 1, sl);
+                std::vector<DevCtx *> &hdev = sl.hdev;
+                std::vector<Lane *> &hlane = sl.hlane;
                 const int G = 1 + (int)hdev.size();
                 std::vector<int32_t> where(n, 0);
                 plan_deal(cost.data(), n, G, where.data());
@@ -1497,12 +1524,9 @@ class Coalescer {
                 };
                 std::vector<std::thread> th;
                 for (int g = 1; g < G; g++) th.emplace_back([&, g] { run_part(hdev[g - 1], *hlane[g - 1], pidx[g]); });
-                {
-                    std::lock_guard<std::mutex> llk(ln.mu);
-                    run_part(dev, ln, pidx[0]);
-                }
+                run_part(dev, ln, pidx[0]);
                 for (auto &t : th) t.join();
-                hlock.clear();
+                sl.release();
                 if (host_trace())
                     fprintf(stderr, "[jfs coalescer] t=%.2f dev %d lane %d algo %d dir %d: %zu calls on %d device(s), gathered %.2f ms, ran %.2f ms\n",
                             now_ms(), dev->id, (int)(&ln - dev->lane), algo, dir, batch.size(), G, t0 - t_gather,
@@ -1877,6 +1901,45 @@ int64_t jfs_decompress_batch_csum(int algo, int nblk, const jfs_iov *iov, int64_
 void jfs_deal_plan(const int64_t *cost, int n, int ndev, int32_t *out_dev) {
     if (!cost || !out_dev || n <= 0) return;
     plan_deal(cost, n, ndev, out_dev);
+}
+
+int64_t jfs_test_spread_locking(int ndev, int iters, int timeout_ms) {
+    if (ndev < 1 || ndev > 32 || iters < 1) return -2;
+    // fake devices (no GPU state: only their lane mutexes are used)
+    struct Run {
+        std::vector<DevCtx *> devs;
+        std::atomic<int> finished{0};
+        std::atomic<int64_t> spread{0};
+    };
+    auto *r = new Run;  // leaked on a deadlock (the stuck threads still use it)
+    for (int d = 0; d < ndev; d++) {
+        r->devs.push_back(new DevCtx);
+        r->devs.back()->id = d;
+    }
+    const int nthr = ndev * NLANE;
+    for (int t = 0; t < nthr; t++) {
+        std::thread([r, t, iters, ndev] {
+            DevCtx *dev = r->devs[t / NLANE];
+            Lane &ln = dev->lane[t % NLANE];
+            for (int i = 0; i < iters; i++) {
+                SpreadLanes sl;
+                spread_acquire(dev, ln, r->devs, ndev + 1, sl);
+                if (!sl.hdev.empty()) r->spread.fetch_add(1);
+                std::this_thread::yield();
+                sl.release();
+            }
+            r->finished.fetch_add(1);
+        }).detach();
+    }
+    const auto t_end = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
+    while (r->finished.load() < nthr) {
+        if (std::chrono::steady_clock::now() > t_end) return -1;  // deadlocked
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
+    const int64_t sp = r->spread.load();
+    for (DevCtx *d : r->devs) delete d;
+    delete r;
+    return sp;
 }
 
 // The device-resident entry points launch on the caller's current device; it

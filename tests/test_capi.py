@@ -171,3 +171,16 @@ def test_deal_plan_size_balanced(lib):
     cost = [4 << 20, 64 << 10, 4 << 20, 64 << 10]
     w = plan(cost, 2)
     assert w[0] != w[2]
+
+
+def test_spread_lock_order_no_deadlock(lib):
+    """the coalescer's burst spreading takes the worker's own
+    lane first (blocking) and other devices' lanes only by try_lock.  Run that
+    acquisition concurrently on fake devices (host only, no GPU): every worker
+    of every device spreading at once must finish, and the spread branch (a
+    foreign lane taken) must actually be exercised."""
+    for ndev in (2, 3, 8):
+        r = lib.jfs_test_spread_locking(ndev, 2000, 20000)
+        assert r != -1, f"spread lane acquisition deadlocked with {ndev} devices"
+        assert r > 0, "no burst took a foreign lane: the multi-device branch did not run"
+    assert lib.jfs_test_spread_locking(0, 1, 10) == -2
