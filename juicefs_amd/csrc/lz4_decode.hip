@@ -1673,7 +1673,13 @@ __device__ __forceinline__ void parser_wave(Smem &s, Ctx &c PROF_ARG) {
     }
 }
 
+#ifndef JFS_LZ4_CPRIO
+#define JFS_LZ4_CPRIO 1  // s_setprio of the copier wave (the critical one of the pair)
+#endif
 __device__ __forceinline__ void copier_wave(Smem &s, Ctx &c, int32_t *retp PROF_ARG) {
+#if JFS_LZ4_CPRIO
+    __builtin_amdgcn_s_setprio(JFS_LZ4_CPRIO);
+#endif
     Ser st;
     st.ip = 0;
     st.op = 0;
