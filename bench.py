@@ -53,12 +53,15 @@ ZSTD_FRAMES = []  # configs[3]'s distinct frames (host copies) for its CPU leg
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 METRIC = "device-resident GiB/s (de)compress, 4 MiB blocks, LZ4+Zstd, 1/2/4/8 MI355X"
 KERNEL_SOURCES = ("juicefs_amd/csrc/lz4_decode.hip", "juicefs_amd/csrc/wave.cuh", "juicefs_amd/csrc/jfs_internal.h")
+ZSTD_KERNEL_SOURCES = ("juicefs_amd/csrc/zstd_decode.hip", "juicefs_amd/csrc/zstd_split.inc",
+                       "juicefs_amd/csrc/wave.cuh", "juicefs_amd/csrc/jfs_internal.h")
 
 
-def kernel_src_sha256() -> str:
-    """Stamp of the LZ4 decode kernel sources (profiles/traffic.json carries it)."""
+def kernel_src_sha256(sources=KERNEL_SOURCES) -> str:
+    """Stamp of a kernel's sources (profiles/traffic*.json carry it): the LZ4
+    decode kernel by default, ZSTD_KERNEL_SOURCES for the Zstd decoder."""
     h = hashlib.sha256()
-    for p in KERNEL_SOURCES:
+    for p in sources:
         with open(os.path.join(ROOT, p), "rb") as f:
             h.update(f.read())
     return h.hexdigest()
@@ -87,6 +90,7 @@ def parse():
     p.add_argument("--extra-blocks", type=int, default=1024, help="blocks in the Zstd compress sample")
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="wall budget per CPU baseline leg")
     p.add_argument("--traffic-file", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    p.add_argument("--zstd-traffic-file", default=os.path.join(ROOT, "profiles", "traffic_zstd.json"))
     return p.parse_args()
 
 
@@ -356,6 +360,19 @@ def oneshot_concurrency(comp_blocks, raw_blocks, U, n_dec=200, n_enc=20, rounds=
         return {"calls": n * k, "p50_ms": pct(flat, 0.5), "p99_ms": pct(flat, 0.99),
                 "value": n * k * U / wall / 2**30, "unit": "GiB/s", "errors": errs, "device_batches": b1 - b0}
 
+    def bursts(n, k, fn, check, nb=5):
+        """nb bursts of run(n, k): the median value / p50 / p99 over the bursts
+        (one burst alone swings with what the coalescer gathers), each burst's
+        record (device batches = how many device batches its calls formed)."""
+        rs = [run(n, k, fn, check) for _ in range(nb)]
+        med = lambda key: sorted(r[key] for r in rs)[len(rs) // 2]
+        return {"calls": n * k, "bursts": len(rs), "value": med("value"), "p50_ms": med("p50_ms"),
+                "p99_ms": med("p99_ms"), "unit": "GiB/s", "errors": sum(r["errors"] for r in rs),
+                "device_batches": [r["device_batches"] for r in rs],
+                "calls_per_device_batch": [round(n * k / max(r["device_batches"], 1), 1) for r in rs],
+                "per_burst": [{"value": round(r["value"], 3), "p50_ms": round(r["p50_ms"], 2),
+                               "p99_ms": round(r["p99_ms"], 2)} for r in rs]}
+
     nc = len(comp_blocks)
     kmax = max(rounds, 5)
     ddst = {}  # one output buffer per (thread, call): checked after the run
@@ -390,8 +407,8 @@ def oneshot_concurrency(comp_blocks, raw_blocks, U, n_dec=200, n_enc=20, rounds=
     warm = [run(n_dec, rounds, dec, dchk)["device_batches"] for _ in range(2)]
     warm += [run(n_enc, rounds, enc, echk)["device_batches"]]
     out = {"decompress_lone": run(1, 5, dec, dchk), "compress_lone": run(1, 3, enc, echk),
-           f"decompress_{n_dec}_concurrent": run(n_dec, rounds, dec, dchk),
-           f"compress_{n_enc}_concurrent": run(n_enc, rounds, enc, echk),
+           f"decompress_{n_dec}_concurrent": bursts(n_dec, rounds, dec, dchk),
+           f"compress_{n_enc}_concurrent": bursts(n_enc, rounds, enc, echk),
            "warmup_device_batches": warm,
            "path": "LZ4 one-call API (jfs_compress / jfs_decompress) from concurrent host threads, host buffers, "
                    "1 GPU; value = uncompressed GiB/s over the wall time of all calls"}
@@ -414,8 +431,8 @@ def oneshot_concurrency(comp_blocks, raw_blocks, U, n_dec=200, n_enc=20, rounds=
         return z.Decompress(zout[(t, r)], zframes[(t + r) % len(zframes)])[0]
     zdchk = lambda t, r, n: n == U and zout[(t, r)] == raw_blocks[(t + r) % len(zframes)]
     out["zstd"] = {"compress_lone": run(1, 3, zenc, zechk), "decompress_lone": run(1, 5, zdec, zdchk),
-                   f"compress_{n_enc}_concurrent": run(n_enc, rounds, zenc, zechk),
-                   f"decompress_{n_enc}_concurrent": run(n_enc, rounds, zdec, zdchk),
+                   f"compress_{n_enc}_concurrent": bursts(n_enc, rounds, zenc, zechk),
+                   f"decompress_{n_enc}_concurrent": bursts(n_enc, rounds, zdec, zdchk),
                    "path": "Zstd one-call API (compress.go ZStandard: GPU encoder, level-1 class; GPU decoder)"}
     return out
 
@@ -632,13 +649,16 @@ def configs3_zstd(a, S, world, rank, dev):
     global ZSTD_FRAMES
     ZSTD_FRAMES = [zb.comp[i * zb.slot:i * zb.slot + int(zb.csize[i])].cpu().numpy().tobytes()
                    for i in range(min(16, a.blocks))]
+    traffic, traffic_src = measured_traffic(a.zstd_traffic_file, a.blocks, U, ZSTD_KERNEL_SOURCES)
     return {"config": f"Zstd level-{a.level} decode, {a.blocks}x4MiB frames in HBM per GPU (BASELINE configs[3])",
             "value": S.whole_job_gib_s(world, a.blocks, U, a.zstd_steps, el), "unit": "GiB/s",
             "ms_per_step": el / a.zstd_steps * 1e3, "steps": a.zstd_steps, "n_gpus": world,
             "kernel_ms": kms, "ratio": a.blocks * U / zb.comp_bytes,
             "roofline": {"bound": "hbm", "achieved": (zb.comp_bytes + a.blocks * U) / (kms / 1e3) / 1e9,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": (zb.comp_bytes + a.blocks * U) / (kms / 1e3) / 1e9 / HBM_PEAK_GBS},
+                         "frac": (zb.comp_bytes + a.blocks * U) / (kms / 1e3) / 1e9 / HBM_PEAK_GBS,
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "algorithmic_bytes_per_launch": zb.comp_bytes + a.blocks * U},
             "data": "synthetic text-like, 256 distinct blocks compressed by the host libzstd, replicated",
             "verified": "every frame's output compared with its source"}
 
@@ -741,16 +761,17 @@ def other_classes(a, S, world, rank, dev, nblk=1024):
     return out
 
 
-def measured_traffic(path, nblk, U):
-    """HBM bytes per launch from profiles/traffic.json, only if it was
-    measured on these kernel sources at this workload."""
+def measured_traffic(path, nblk, U, sources=KERNEL_SOURCES):
+    """HBM bytes per launch from profiles/traffic.json (traffic_zstd.json for
+    the Zstd decoder), only if it was measured on these kernel sources at this
+    workload."""
     try:
         tj = json.load(open(path))
     except Exception:
         return None, "no traffic file"
     if tj.get("blocks") != nblk or tj.get("block_bytes") != U:
         return None, "traffic file is for another workload"
-    if tj.get("kernel_src_sha256") != kernel_src_sha256():
+    if tj.get("kernel_src_sha256") != kernel_src_sha256(sources):
         return None, "traffic file is stale (kernel sources changed since it was measured)"
     stamp = tj.get("git_head") or f"kernel sources sha256 {tj.get('kernel_src_sha256', '')[:12]}"
     return tj.get("hbm_bytes_per_launch"), f"rocprofv3 PMC FETCH_SIZE/WRITE_SIZE ({stamp})"

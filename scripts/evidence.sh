@@ -17,17 +17,16 @@ tail -1 $O/smoke.log
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $T/pf -o pf --output-format csv -- python scripts/prof_run.py 4096 1 T > $O/pf.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $T/pw -o pw --output-format csv -- python scripts/prof_run.py 4096 1 T > $O/pw.log 2>&1
 python scripts/traffic.py $(find $T/pf -name '*counter_collection.csv' | head -1) $(find $T/pw -name '*counter_collection.csv' | head -1) lz4_decode_kernel 4096 4194304 $O/traffic.json > /dev/null
-timeout -k 10 900 python bench.py --traffic-file $O/traffic.json > $O/bench.json 2> $O/bench.err
+# HBM traffic of the Zstd decode kernels (one launch each pass, frames from the cache)
+timeout -k 10 300 python scripts/prof_run.py 4096 0 T zstd > /dev/null 2>&1
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $T/zpf -o zpf --output-format csv -- python scripts/prof_run.py 4096 1 T zstd > $O/zpf.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $T/zpw -o zpw --output-format csv -- python scripts/prof_run.py 4096 1 T zstd > $O/zpw.log 2>&1
+python scripts/traffic_zstd.py $(find $T/zpf -name '*counter_collection.csv' | head -1) $(find $T/zpw -name '*counter_collection.csv' | head -1) 4096 4194304 $O/traffic_zstd.json > /dev/null
+timeout -k 10 900 python bench.py --traffic-file $O/traffic.json --zstd-traffic-file $O/traffic_zstd.json > $O/bench.json 2> $O/bench.err
 tail -c 400 $O/bench.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $T/kt_lz4 -o kt --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-extras --no-host-path --traffic-file $O/traffic.json > $O/kt_lz4.log 2>&1
 find $T/kt_lz4 -name '*kernel_stats.csv' -exec cp {} $O/lz4_kernel_stats.csv \;
-timeout -k 10 300 python scripts/prof_run.py 4096 0 T zstd > /dev/null 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $T/kt_zstd -o kt --output-format csv -- python scripts/prof_run.py 4096 3 T zstd > $O/kt_zstd.log 2>&1
 find $T/kt_zstd -name '*kernel_stats.csv' -exec cp {} $O/zstd_kernel_stats.csv \;
-# HBM traffic of the Zstd decode kernels (one launch each pass, frames from the cache)
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $T/zpf -o zpf --output-format csv -- python scripts/prof_run.py 4096 1 T zstd > $O/zpf.log 2>&1
-timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $T/zpw -o zpw --output-format csv -- python scripts/prof_run.py 4096 1 T zstd > $O/zpw.log 2>&1
-find $T/zpf -name '*counter_collection.csv' -exec cp {} $O/zstd_fetch.csv \;
-find $T/zpw -name '*counter_collection.csv' -exec cp {} $O/zstd_write.csv \;
 du -sh $O
 echo evidence-done

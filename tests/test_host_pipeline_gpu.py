@@ -1,7 +1,8 @@
 """Host batch path (capi.hip run_batch): many chunks pipelined over two
 streams.  A child process with a 16 MiB staging chunk pushes ~60 blocks
 through several chunks per call, mixed sizes and codecs; every result must
-match a single-chunk run and the CPU oracle (LZ4 bytes exact, Zstd round trip)."""
+match a single-chunk run and the CPU oracle (LZ4 and Zstd level-1 bytes exact,
+both round trips)."""
 import os
 import subprocess
 import sys
@@ -32,6 +33,8 @@ for c in (lz, zs):
         if c is lz:
             m, ref = o.lz4_compress(s)
             assert bytes(d[:n]) == ref
+        else:  # byte-identical to libzstd 1.4.9 level 1 (the restatement the oracle pins)
+            assert bytes(d[:n]) == o.zstd_compress_l1(s)
     outs = [bytearray(len(s)) for s in srcs]
     back = c.DecompressBatch(list(zip(outs, frames)))
     for s, b, (n, e) in zip(srcs, outs, back):
