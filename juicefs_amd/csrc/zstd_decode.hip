@@ -2281,6 +2281,9 @@ __global__ __launch_bounds__(64) void zseqa_kernel(const jfs_dev_block *__restri
 // (in stream order over the workgroup's inputs), decodes their sequences
 // with wave 1 keeping the tables and bitstreams in LDS, then resolves the
 // symbolic repeat offsets in block order.
+#ifndef JFS_ZSEQ_DPRIO
+#define JFS_ZSEQ_DPRIO 0
+#endif
 __global__ __launch_bounds__(128) void zseqb_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
                                                     ZInfo *__restrict__ info, uint16_t *__restrict__ tabs_all,
                                                     uint4 *__restrict__ items_all) {
@@ -2297,6 +2300,9 @@ __global__ __launch_bounds__(128) void zseqb_kernel(const jfs_dev_block *__restr
         }
         return;
     }
+#if JFS_ZSEQ_DPRIO
+    __builtin_amdgcn_s_setprio(JFS_ZSEQ_DPRIO);  // the decoder wave is the critical one of the pair
+#endif
     int gn = 0;
     uint32_t e0 = 1, e1 = 4, e2 = 8;  // repeat offsets carried through phase C (reset at each frame)
     for (int f = 0; f < ZSEQ_INPUTS; ++f) {
@@ -2457,7 +2463,16 @@ __global__ __launch_bounds__(64) void zseq_kernel(const jfs_dev_block *__restric
 // ---------------------------------------------------------------------------
 // kernel 3: execute items
 // ---------------------------------------------------------------------------
+#ifndef JFS_ZEXEC_V2
+#define JFS_ZEXEC_V2 1  // batches as in the LZ4 copier (lz4_decode.hip batch()): zeroed span + OR'd 16-byte steps
+#endif
+#if JFS_ZEXEC_V2
+// V2 needs no far-source buffer: the ring takes its 4 KiB (sources up to 8 KiB
+// back stay in LDS; fewer far matches, rarer waits for flushed output)
+constexpr int R = 8192;
+#else
 constexpr int R = 4096;
+#endif
 constexpr int RMASK = R - 1;
 constexpr int LW = 2048;          // literal staging window
 constexpr int FLUSH_T = 1024;
@@ -2466,8 +2481,13 @@ constexpr int CH = 256;           // output chunk of the parallel gather (4 byte
 
 constexpr int FB = 64;           // far-source prefetch bytes per lane (16 B alignment slack)
 constexpr int FBUSE = FB - 16;
-constexpr int BSPAN = R / 2;     // max output span of one lane-parallel batch
+constexpr int BSPAN = 2048;      // max output span of one lane-parallel batch
+static_assert(BSPAN <= R / 2, "a batch span and the unflushed tail fit the ring");
+#if JFS_ZEXEC_V2
+constexpr int LONGI = 64;        // items with a literal run or match longer than this go whole-wave
+#else
 constexpr int LONGI = 1024;      // items longer than this are copied by the whole wave
+#endif
 #ifndef JFS_ZEXEC_LEVELS
 #define JFS_ZEXEC_LEVELS 0  // 1: near matches in dependency rounds (binary search over lanes); measured slower (119 vs 114 ms)
 #endif
@@ -2479,6 +2499,15 @@ constexpr int LONGI = 1024;      // items longer than this are copied by the who
 // CU's 160 KiB, so a launch is one round (at 10,304 bytes it was 15 per CU and
 // the 256 leftover frames ran as a second round).  Over-reads past lw and
 // farbuf (dword/alignbyte tails) only fetch bytes that are never used.
+#if JFS_ZEXEC_V2
+struct XSmem {
+    alignas(16) uint8_t ring[R];
+    union {
+        alignas(16) uint8_t lw[LW];  // literal window (x.lw0 is reset after a checksum)
+        uint64_t xxh[4];             // frame checksum (between batches)
+    };
+};
+#else
 struct XSmem {
     alignas(16) uint8_t ring[R];
     alignas(16) uint8_t lw[LW];
@@ -2487,6 +2516,7 @@ struct XSmem {
         uint64_t xxh[4];                      // frame checksum (between batches)
     };
 };
+#endif
 static_assert(sizeof(XSmem) * 16 <= 160 * 1024, "16 zexec workgroups per CU");
 
 struct X {
@@ -2689,6 +2719,208 @@ __device__ __forceinline__ void cp_ring(XSmem &s, const X &x, int32_t src, int32
     }
 }
 
+#if JFS_ZEXEC_V2
+// ---------------------------------------------------------------------------
+// V2 batch: the LZ4 copier's scheme (lz4_decode.hip batch()).
+// The batch's ring span is zeroed, then every write is an LDS atomic OR of
+// whole dwords (lanes sharing a boundary dword cannot clobber each other), in
+// fixed 16-byte steps: literal runs from the staged literal window, far matches
+// from HBM (24 bytes loaded per 16-byte step), then near matches: source
+// substitution (a match whose source lies inside another pending match of the
+// batch reads that match's source), one lane-parallel round for matches whose
+// source is final (before the batch, or inside one literal run of it), and the
+// rest by the whole wave in lane (= output) order.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t zbal(bool b) { return __builtin_amdgcn_ballot_w64(b); }
+
+__device__ __forceinline__ void zor(XSmem &s, uint32_t a, uint32_t v) {  // a % 4 == 0
+    __hip_atomic_fetch_or(reinterpret_cast<uint32_t *>(s.ring) + (a >> 2), v, __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// bytes [ha, ha + m) (1 <= m <= 16, ha = da & 3) of the 20-byte span w0..w4 to ring slot da
+__device__ __forceinline__ void zput16(XSmem &s, uint32_t da, int32_t m, uint32_t w0, uint32_t w1, uint32_t w2,
+                                       uint32_t w3, uint32_t w4) {
+    const int32_t ha = (int32_t)(da & 3u), e8 = 8 * (ha + m);
+    const uint32_t D0 = da & ~3u;
+    auto lm = [](int32_t b) -> uint32_t {  // low min(max(b, 0), 32) bits
+        const uint32_t sh = (uint32_t)(b < 0 ? 0 : b > 32 ? 32 : b);
+        return (uint32_t)((0xFFFFFFFFull << sh) >> 32);
+    };
+    zor(s, D0, w0 & lm(e8) & ~lm(8 * ha));
+    zor(s, (D0 + 4) & RMASK, w1 & lm(e8 - 32));
+    zor(s, (D0 + 8) & RMASK, w2 & lm(e8 - 64));
+    zor(s, (D0 + 12) & RMASK, w3 & lm(e8 - 96));
+    zor(s, (D0 + 16) & RMASK, w4 & lm(e8 - 128));
+}
+// m (1..16) bytes from LDS byte address sa (RING: ring slot space) to ring slot da
+template <bool RING>
+__device__ __forceinline__ void zcopy16(XSmem &s, uint32_t sa, uint32_t da, int32_t m) {
+    const uint8_t *lds = (const uint8_t *)&s;
+    const uint32_t ha = da & 3u;
+    const uint32_t sb = sa - ha, S0 = sb & ~3u, sh = sb & 3u;
+    uint32_t r[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        const uint32_t a = RING ? ((S0 + 4 * j) & RMASK) : (S0 + 4 * j);
+        r[j] = *(const uint32_t *)(lds + a);
+    }
+    zput16(s, da, m, __builtin_amdgcn_alignbyte(r[1], r[0], sh), __builtin_amdgcn_alignbyte(r[2], r[1], sh),
+           __builtin_amdgcn_alignbyte(r[3], r[2], sh), __builtin_amdgcn_alignbyte(r[4], r[3], sh),
+           __builtin_amdgcn_alignbyte(r[5], r[4], sh));
+}
+// zero ring bytes of output [O0, O1) (bytes below O0 in the first dword are kept)
+__device__ __forceinline__ void zzero_span(XSmem &s, const X &x, int32_t O0, int32_t O1) {
+    const int l = lane_id();
+    const uint32_t a = slot(x, O0), h = a & 3u;
+    const int32_t A = O0 + (int32_t)((4u - h) & 3u);
+    if (l == 0 && h) {
+        const uint32_t keep = (1u << (8 * h)) - 1u;
+        __hip_atomic_fetch_and(reinterpret_cast<uint32_t *>(s.ring) + (a >> 2), keep, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    for (int32_t q = A + 4 * l; q < O1; q += 256) *(uint32_t *)(s.ring + slot(x, q)) = 0u;
+}
+typedef uint32_t zu32x4 __attribute__((ext_vector_type(4), aligned(4)));
+typedef uint32_t zu32x2 __attribute__((ext_vector_type(2), aligned(4)));
+// far source: the 6 dwords from the dword holding HBM address a.  A dword
+// wholly below the output's first dword (lo) holds no source byte (only bytes
+// the write mask drops) and is not read: it reads as 0.
+__device__ __forceinline__ void zfar_load(uintptr_t a, uintptr_t lo, uint32_t (&d)[6]) {
+    const uintptr_t b = a & ~(uintptr_t)3;
+    lo &= ~(uintptr_t)3;
+    const bool under = b < lo;
+    const uintptr_t q = under ? lo : b;
+    const zu32x4 v = *(JFS_GLOBAL const zu32x4 *)q;
+    const zu32x2 w = *(JFS_GLOBAL const zu32x2 *)(q + 16);
+    d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w; d[4] = w.x; d[5] = w.y;
+    if (zbal(under)) {
+        if (under) { d[5] = d[4]; d[4] = d[3]; d[3] = d[2]; d[2] = d[1]; d[1] = d[0]; d[0] = 0; }
+    }
+}
+// whole-wave copy of len bytes to output op from op - D (all inside the ring),
+// in chunks of at most D bytes so that self-overlapping matches repeat their period
+__device__ __forceinline__ void zwave_near(XSmem &s, const X &x, int32_t op, int32_t D, int32_t len) {
+    const int l = lane_id();
+    const int32_t step = D < 64 ? D : 64;
+    for (int32_t k = 0; k < len; k += step) {
+        const int32_t i = k + l;
+        if (l < step && i < len) s.ring[slot(x, op + i)] = s.ring[slot(x, op + i - D)];
+    }
+}
+
+__device__ __forceinline__ void x_batch2(XSmem &s, X &x, bool act, int32_t o, uint32_t ll, uint32_t ml, uint32_t off,
+                                         int32_t lit, int32_t O0, int32_t O1) {
+    // sources below hz come from HBM: the ring slots of [hz, O1) are intact
+    // (zzero_span may clear up to 3 bytes past O1)
+    const int32_t hz = O1 + 4 - R;
+    uint64_t tq0 = ZP_NOW();
+    if (O0 - x.F >= FLUSH_T) xflush_line(s, x, O0, false);
+    zzero_span(s, x, O0, O1);
+    const int32_t ms = o + (int32_t)ll, msrc = ms - (int32_t)off;
+    const bool hasm = act && ml > 0;
+    const bool far = hasm && msrc < hz;
+    // a far source (< hz + LONGI) must be flushed and its stores complete
+    if (zbal(far) && hz + LONGI > x.Fw) {
+        wait_vm();
+        x.Fw = x.F;
+        if (hz + LONGI > x.Fw) x.bug = 105;
+    }
+    uint32_t fd[6] = {0, 0, 0, 0, 0, 0};
+    const uint32_t fha = slot(x, ms) & 3u;
+    if (zbal(far)) {
+        if (far) zfar_load((uintptr_t)(x.dst + msrc) - fha, (uintptr_t)x.dst, fd);
+    }
+    uint64_t tq1 = ZP_NOW();
+    // literal runs (source: the staged literal window)
+    const uint32_t lwoff = (uint32_t)((const uint8_t *)s.lw - (const uint8_t *)&s) + (uint32_t)(lit - (int32_t)x.lw0);
+    for (uint32_t k = 0; zbal(act && k < ll); k += 16) {
+        if (act && k < ll) {
+            const int32_t m = ll - k < 16u ? (int32_t)(ll - k) : 16;
+            zcopy16<false>(s, lwoff + k, slot(x, o + (int32_t)k), m);
+        }
+    }
+    uint64_t tq2 = ZP_NOW();
+    // far matches
+    if (zbal(far)) {
+        for (uint32_t k = 0; zbal(far && k < ml); k += 16) {
+            if (far && k < ml) {
+                const int32_t m = ml - k < 16u ? (int32_t)(ml - k) : 16;
+                const uint32_t da = slot(x, ms + (int32_t)k);  // da & 3 == fha
+                const uint32_t sh = (uint32_t)((uintptr_t)(x.dst + msrc + (int32_t)k) - fha) & 3u;
+                zput16(s, da, m, __builtin_amdgcn_alignbyte(fd[1], fd[0], sh), __builtin_amdgcn_alignbyte(fd[2], fd[1], sh),
+                       __builtin_amdgcn_alignbyte(fd[3], fd[2], sh), __builtin_amdgcn_alignbyte(fd[4], fd[3], sh),
+                       __builtin_amdgcn_alignbyte(fd[5], fd[4], sh));
+            }
+            const bool more = far && k + 16 < ml;
+            if (zbal(more)) {
+                if (more) zfar_load((uintptr_t)(x.dst + msrc + (int32_t)k + 16) - fha, (uintptr_t)x.dst, fd);
+            }
+        }
+    }
+    uint64_t tq3 = ZP_NOW();
+    XP_ADD(1, tq1 - tq0);
+    XP_ADD(2, tq2 - tq1);
+    XP_ADD(3, tq3 - tq2);
+    XP_ADD(5, 1);
+    // source substitution: out[x] == out[x - off_i] for every byte a match i
+    // writes, so a pending match whose whole source lies inside another
+    // pending match of this batch can read that match's source instead
+    bool pend = hasm && !far;
+    int32_t src = msrc;
+    const uint64_t am = zbal(act);
+    const int first = am ? (int)__builtin_ctzll(am) : 0;
+    const uint32_t key = act ? (uint32_t)ms : ((int)lane_id() < first ? 0u : 0xFFFFFFFFu);  // non-decreasing
+    bool litsrc = false;  // the source lies wholly inside one literal run of this batch (written above)
+    {
+        const uint32_t mek = pend ? (uint32_t)(ms + (int32_t)ml) : 0u;
+        const bool want = pend && off >= ml && src >= O0;
+        if (zbal(want)) {
+            int lo = 0;  // last lane with key <= src
+#pragma unroll
+            for (int stp = 32; stp; stp >>= 1) {
+                const uint32_t v = (uint32_t)__shfl((int)key, lo + stp, 64);
+                lo = v <= (uint32_t)src ? lo + stp : lo;
+            }
+            const uint32_t vms = (uint32_t)__shfl((int)key, lo, 64);
+            const uint32_t vme = (uint32_t)__shfl((int)mek, lo, 64);
+            const int32_t voff = __shfl((int)off, lo, 64);
+            const uint32_t nms = (uint32_t)__shfl((int)key, lo + 1 < 64 ? lo + 1 : 63, 64);
+            const bool ok = want && vms <= (uint32_t)src && (uint32_t)(src + (int32_t)ml) <= vme && voff > 0 &&
+                            src - voff >= hz;
+            // past the end of lane lo's match and before the next lane's match:
+            // inside the next item's literal run, already in the ring
+            litsrc = want && vms <= (uint32_t)src && (uint32_t)src >= vme && lo < 63 &&
+                     (uint32_t)(src + (int32_t)ml) <= nms;
+            src = ok ? src - voff : src;
+        }
+    }
+    int32_t pos = ms, rem = (int32_t)ml, D = ms - src;
+    const int32_t send = src + (int32_t)ml < ms ? src + (int32_t)ml : ms;
+    {
+        // one round: every ready lane copies its first (<= 16 byte) step; what
+        // is left is copied by the whole wave in lane order (= output order,
+        // so every source is complete when its match's turn comes)
+        const bool go = pend && (send <= O0 || litsrc);
+        if (zbal(go)) {
+            if (go) {
+                const int32_t m = rem < 16 ? (rem < D ? rem : D) : (D < 16 ? D : 16);
+                zcopy16<true>(s, slot(x, pos - D), slot(x, pos), m);
+                pos += m;
+                rem -= m;
+                if (rem <= 0) pend = false;
+            }
+        }
+        for (uint64_t pmk = zbal(pend); pmk; pmk &= pmk - 1) {
+            const int j = (int)__builtin_ctzll(pmk);
+            zwave_near(s, x, (int32_t)readlane((uint32_t)pos, j), (int32_t)readlane((uint32_t)D, j),
+                       (int32_t)readlane((uint32_t)rem, j));
+        }
+    }
+    XP_ADD(4, ZP_NOW() - tq3);
+}
+#endif
+
+#if !JFS_ZEXEC_V2
 __device__ __forceinline__ void x_batch(XSmem &s, X &x, bool act, int32_t o, uint32_t ll, uint32_t ml, uint32_t off,
                                         int32_t lit, int32_t O0, int32_t O1) {
     const int l = lane_id();
@@ -2817,6 +3049,8 @@ __device__ __forceinline__ void x_batch(XSmem &s, X &x, bool act, int32_t o, uin
     XP_ADD(4, ZP_NOW() - tq3);
 }
 
+#endif  // !JFS_ZEXEC_V2
+
 // whole-wave copy of one long match (ring or HBM sources)
 __device__ __forceinline__ void x_match(XSmem &s, X &x, uint32_t off, int32_t len) {
     const int l = lane_id();
@@ -2853,16 +3087,22 @@ __device__ __forceinline__ void x_run(XSmem &s, X &x, uint32_t n, uint32_t ll, u
     const int32_t O0run = x.op;
     const int32_t o = O0run + (int32_t)(incl - len);
     const int32_t lit = (int32_t)*lp + (int32_t)(lincl - lln);
+#if JFS_ZEXEC_V2
+    const bool lng = in && (ll > (uint32_t)LONGI || ml > (uint32_t)LONGI);
+#else
     const bool lng = in && len > (uint32_t)LONGI;
+#endif
     uint32_t j = 0;
     while (j < n) {
         const int32_t oj = (int32_t)readlane((uint32_t)o, (int)j), lj = (int32_t)readlane((uint32_t)lit, (int)j);
         if (readlane(lng ? 1u : 0u, (int)j)) {  // one long item, whole wave
+            const uint64_t tl0 = ZP_NOW();
             const uint32_t jll = readlane(ll, (int)j), jml = readlane(ml, (int)j), joff = readlane(off, (int)j);
             x.op = oj;
             x_lit(s, x, lj, (int32_t)jll);
             if (jml) x_match(s, x, joff, (int32_t)jml);
             j++;
+            XP_ADD(6, ZP_NOW() - tl0);
             continue;
         }
         // maximal batch from j: span, literal window and no long item
@@ -2874,8 +3114,14 @@ __device__ __forceinline__ void x_run(XSmem &s, X &x, uint32_t n, uint32_t ll, u
         const bool act = (uint32_t)l >= j && (uint32_t)l < eb;
         const int32_t O1 = (int32_t)readlane((uint32_t)endo, (int)eb - 1);
         const int32_t L1 = (int32_t)readlane((uint32_t)endl, (int)eb - 1);
+        const uint64_t tw0 = ZP_NOW();
         if (L1 > lj) lit_window(s, x, lj, L1 - lj);
+        XP_ADD(0, ZP_NOW() - tw0);
+#if JFS_ZEXEC_V2
+        x_batch2(s, x, act, o, ll, ml, off, lit, oj, O1);
+#else
         x_batch(s, x, act, o, ll, ml, off, lit, oj, O1);
+#endif
         x.op = O1;
         j = eb;
     }
@@ -2915,11 +3161,22 @@ __global__ __launch_bounds__(64) void zexec_kernel(const jfs_dev_block *__restri
     int32_t regen = 0, lused = 0;
     uint32_t rin0 = 1, rin1 = 4, rin2 = 8;  // repeat offsets at the start of the current block
     bool done = false;
+#if JFS_ZEXEC_V2
+    // items one chunk ahead: the next 64 are loaded while this chunk runs
+    uint4 ahead = make_uint4(0, 0, 0, 0);
+    if ((uint32_t)l < nit) ahead = it[l];
+#endif
     for (uint32_t base = 0; base < nit && !done; base += 64) {
         uint64_t tb0 = ZP_NOW();
+#if JFS_ZEXEC_V2
+        const uint4 mine = ahead;
+        ahead = make_uint4(0, 0, 0, 0);
+        if (base + 64 + l < nit) ahead = it[base + 64 + l];
+#else
         uint4 mine = make_uint4(0, 0, 0, 0);
         if (base + l < nit) mine = it[base + l];
         wait_vm();
+#endif
         XP_ADD(0, ZP_NOW() - tb0);
         uint32_t cnt = nit - base < 64 ? nit - base : 64;
         const uint64_t nonseq = __ballot((uint32_t)l >= cnt || (mine.w & 0xFF) != IT_SEQ);
@@ -2975,6 +3232,7 @@ __global__ __launch_bounds__(64) void zexec_kernel(const jfs_dev_block *__restri
                     wait_vm();
                     x.Fw = x.F;
                     uint64_t h = xxh64_dev(s, (const gc_u8 *)x.dst + x.fstart, x.op - x.fstart);
+                    x.lw0 = -(1LL << 40);  // s.xxh shares the literal window's bytes
                     if ((uint32_t)h != iz) { result = E_CORRUPT; done = true; break; }
                 }
             } else if (kind == IT_ERR) {

@@ -14,7 +14,7 @@ lib.jfs_zprof_reset()
 b.decompress(); torch.cuda.synchronize()
 buf = (ctypes.c_ulonglong * 8)()
 lib.jfs_zprof_read(buf)
-names = ["item_load", "flush+far_issue", "literals", "far_land", "matches", "batches", "match_rounds", "total"]
+names = ["item_load+litwin", "flush+far_issue", "literals", "far_land", "matches", "batches", "long_items(V2)", "total"]
 for i, nm in enumerate(names):
     print(f"{nm:12s} per frame {buf[i] / n:14.0f}")
 print(f"per batch: flush+far {buf[1] / max(buf[5], 1):.0f} literals {buf[2] / max(buf[5], 1):.0f} far_land {buf[3] / max(buf[5], 1):.0f} matches {buf[4] / max(buf[5], 1):.0f} ticks; match rounds per batch {buf[6] / max(buf[5], 1):.2f}")
