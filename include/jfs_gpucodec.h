@@ -103,6 +103,17 @@ int64_t jfs_compress_batch(int algo, int nblk, const jfs_iov *iov, int64_t *out_
 int64_t jfs_compress_batch_crc(int algo, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t *crc,
                                uint32_t device_mask);
 int64_t jfs_decompress_batch(int algo, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t device_mask);
+/* Mixed-codec batches (algo[i] per block: a chunk store reading objects written
+ * under different codecs).  Each codec's blocks form
+ * one jfs_{de,}compress_batch call; decode calls run at once, so the codecs
+ * share every device's lanes instead of queueing behind one another (encode
+ * calls run in turn: the encoders slow each other down).  Per-block
+ * results as jfs_{de,}compress_batch (JFS_ERR_INVALID for an unknown algo[i]);
+ * returns JFS_OK or the first whole-call error of a codec's call. */
+int64_t jfs_compress_batch_mixed(const int32_t *algo, int nblk, const jfs_iov *iov, int64_t *out_n,
+                                 uint32_t device_mask);
+int64_t jfs_decompress_batch_mixed(const int32_t *algo, int nblk, const jfs_iov *iov, int64_t *out_n,
+                                   uint32_t device_mask);
 /* jfs_decompress_batch plus, for each block with csum[i] != NULL, the disk-cache
  * checksum of the decoded block -- what cacheStore.add writes beside it
  * (pkg/chunk/disk_cache.go:536-537, checksum() of disk_cache_file.go:139-152):

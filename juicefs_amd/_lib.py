@@ -37,7 +37,7 @@ EXPORTS = [
     "jfs_lz4_split_counts", "jfs_zstd_split_counts", "jfs_lz4_compress_device_small", "jfs_lz4_eseg_counts", "jfs_cipher_from_name", "jfs_cipher_key_size", "jfs_aead_seal_device",
     "jfs_aead_open_device", "jfs_envelope_bound", "jfs_envelope_parse", "jfs_compress_seal_batch",
     "jfs_open_decompress_batch", "jfs_compress_batch_crc", "jfs_decompress_batch_csum", "jfs_deal_plan",
-    "jfs_test_spread_locking",
+    "jfs_test_spread_locking", "jfs_compress_batch_mixed", "jfs_decompress_batch_mixed",
 ]
 
 MODE_OFF, MODE_AUTO, MODE_FORCE = 0, 1, 2
@@ -129,6 +129,9 @@ def load() -> ctypes.CDLL:
     lib.jfs_decompress_batch_csum.restype = i64
     lib.jfs_deal_plan.argtypes = [ctypes.POINTER(i64), ctypes.c_int, ctypes.c_int, ctypes.POINTER(i32)]
     lib.jfs_deal_plan.restype = None
+    for f in (lib.jfs_compress_batch_mixed, lib.jfs_decompress_batch_mixed):
+        f.argtypes = [ctypes.POINTER(i32), ctypes.c_int, ctypes.POINTER(JfsIov), ctypes.POINTER(i64), u32]
+        f.restype = i64
     lib.jfs_test_spread_locking.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
     lib.jfs_test_spread_locking.restype = i64
     lib.jfs_compress_seal_batch.restype = i64

@@ -168,6 +168,46 @@ def csum_bytes(n: int) -> int:
     return (int((n - 1) / CSUM_BLOCK) + 1) * 4
 
 
+def CompressBatchMixed(entries, device_mask: int = 0):
+    """entries: list of (Compressor, dst, src) with any mix of codecs; the
+    codecs' batches run at once on the GPU(s) (jfs_compress_batch_mixed).
+    Returns [(n, err)] with each Compressor's own result semantics."""
+    return _batch_mixed(entries, device_mask, compress=True)
+
+
+def DecompressBatchMixed(entries, device_mask: int = 0):
+    """DecompressBatch over blocks of several codecs (jfs_decompress_batch_mixed)."""
+    return _batch_mixed(entries, device_mask, compress=False)
+
+
+def _batch_mixed(entries, device_mask: int, compress: bool):
+    lib = L.load()
+    nb = len(entries)
+    iov = (L.JfsIov * max(nb, 1))()
+    algos = (ctypes.c_int32 * max(nb, 1))()
+    keep = []
+    for i, (cd, dst, src) in enumerate(entries):
+        d, dn, kd = _addr(dst, True)
+        s, sn, ks = _addr(src, False)
+        keep.append((kd, ks))
+        iov[i].src, iov[i].src_len, iov[i].dst, iov[i].dst_cap = s, sn, d, dn
+        algos[i] = cd.algo
+    out = (ctypes.c_int64 * max(nb, 1))()
+    fn = lib.jfs_compress_batch_mixed if compress else lib.jfs_decompress_batch_mixed
+    rc = fn(algos, nb, iov, out, device_mask)
+    if rc != 0:
+        raise _err(rc, 0, 0, "batch")
+    res = []
+    for i in range(nb):
+        r, algo = int(out[i]), int(algos[i])
+        if r < 0:
+            n = r if (algo == L.ALGO_LZ4 and not compress and r > L.JFS_ERR_BASE) else 0
+            res.append((n, _err(r, iov[i].dst_cap, iov[i].src_len, "compress" if compress else "decompress")))
+        else:
+            res.append((r, None))
+    return res
+
+
 def _batch(algo: int, pairs, device_mask: int, compress: bool, with_crc: bool = False, with_csum: bool = False):
     """pairs: list of (dst, src).  Returns list of (n, err)."""
     lib = L.load()

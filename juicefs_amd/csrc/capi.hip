@@ -1882,6 +1882,77 @@ int64_t jfs_compress_batch(int algo, int nblk, const jfs_iov *iov, int64_t *out_
     return batch_call(algo, COMPRESS, nblk, iov, out_n, device_mask);
 }
 
+// Mixed-codec batches: the blocks of each codec form one batch call.  Decode
+// calls run at once (a device has two lanes, so an LZ4 and a Zstd batch share
+// every device instead of queueing one behind the other: config 4 decode
+// 13.2 -> 21.9 GiB/s); encode calls run in turn (see below).
+static int64_t batch_mixed(int dir, const int32_t *algo, int nblk, const jfs_iov *iov, int64_t *out_n,
+                           uint32_t device_mask) {
+    if (nblk < 0 || (nblk > 0 && (!algo || !iov || !out_n))) return JFS_ERR_INVALID;
+    std::vector<int> idx[3];
+    for (int i = 0; i < nblk; i++) {
+        const int a = algo[i];
+        if (a != JFS_ALGO_NONE && a != JFS_ALGO_LZ4 && a != JFS_ALGO_ZSTD) {
+            out_n[i] = JFS_ERR_INVALID;
+            continue;
+        }
+        idx[a].push_back(i);
+    }
+    struct Group {
+        int algo;
+        std::vector<jfs_iov> iov;
+        std::vector<int64_t> out;
+        int64_t rc = JFS_OK;
+    };
+    std::vector<Group> gs;
+    for (int a = 0; a < 3; a++) {
+        if (idx[a].empty()) continue;
+        Group g;
+        g.algo = a;
+        for (int i : idx[a]) g.iov.push_back(iov[i]);
+        g.out.assign(idx[a].size(), 0);
+        gs.push_back(std::move(g));
+    }
+    auto run = [&](Group &g) {
+        g.rc = batch_call(g.algo, dir, (int)g.iov.size(), g.iov.data(), g.out.data(), device_mask);
+    };
+    static const bool enc_together = [] {
+        const char *e = getenv("JFS_MIXED_ENCODE_TOGETHER");
+        return e && atoi(e) != 0;
+    }();
+    if (dir == DECOMPRESS || enc_together) {
+        std::vector<std::thread> th;
+        for (size_t k = 1; k < gs.size(); k++) th.emplace_back(run, std::ref(gs[k]));
+        if (!gs.empty()) run(gs[0]);
+        for (auto &t : th) t.join();
+    } else {
+        // encoders one codec after the other: measured on config 4's mix, the
+        // LZ4 serial-parse kernels beside the Zstd encoder's host-synchronised
+        // parse rounds ran 0.93 GiB/s against 1.47 in turn
+        for (Group &g : gs) run(g);
+    }
+    int64_t rc = JFS_OK;
+    for (Group &g : gs) {
+        if (g.rc != JFS_OK) {
+            rc = g.rc;
+            continue;
+        }
+        const std::vector<int> &ix = idx[g.algo];
+        for (size_t k = 0; k < ix.size(); k++) out_n[ix[k]] = g.out[k];
+    }
+    return rc;
+}
+
+int64_t jfs_compress_batch_mixed(const int32_t *algo, int nblk, const jfs_iov *iov, int64_t *out_n,
+                                 uint32_t device_mask) {
+    return batch_mixed(COMPRESS, algo, nblk, iov, out_n, device_mask);
+}
+
+int64_t jfs_decompress_batch_mixed(const int32_t *algo, int nblk, const jfs_iov *iov, int64_t *out_n,
+                                   uint32_t device_mask) {
+    return batch_mixed(DECOMPRESS, algo, nblk, iov, out_n, device_mask);
+}
+
 int64_t jfs_compress_batch_crc(int algo, int nblk, const jfs_iov *iov, int64_t *out_n, uint32_t *crc,
                                uint32_t device_mask) {
     if (nblk > 0 && !crc) return JFS_ERR_INVALID;

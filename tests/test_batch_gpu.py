@@ -261,3 +261,50 @@ def test_decompress_batch_disk_cache_checksums(gpu, oracle):
         if name != "none":
             n, e, cs = res[-1]
             assert e is not None and cs is None
+
+
+def test_mixed_codec_batches(gpu, oracle):
+    """jfs_{de,}compress_batch_mixed (SURVEY.md 8(d) config 4 shape): LZ4, Zstd
+    and "none" blocks of 64 KiB - 4 MiB in one call; every compressed block is
+    byte-identical to the oracle of its codec (liblz4 1.9.3 / libzstd 1.4.9
+    level 1), every block round-trips, an unknown codec fails alone."""
+    rng = np.random.default_rng(5)
+    sizes = np.exp(rng.uniform(np.log(64 << 10), np.log(4 << 20), 24)).astype(np.int64)
+    raws = [gen_block("TZR"[i % 3] if i % 4 else "T", 7100 + i, int(n)) for i, n in enumerate(sizes)]
+    cds = [(C.LZ4(), C.ZStandard(), C.noOp())[i % 3] for i in range(len(raws))]
+    ents = [(cd, bytearray(cd.CompressBound(len(r))), r) for cd, r in zip(cds, raws)]
+    res = C.CompressBatchMixed(ents)
+    comp = []
+    for (cd, buf, r), (n, e) in zip(ents, res):
+        assert e is None and n > 0, e
+        got = bytes(buf[:n])
+        if isinstance(cd, C.LZ4):
+            assert got == oracle.lz4_compress(r)[1]
+        elif isinstance(cd, C.ZStandard):
+            assert got == oracle.zstd_compress_l1(r)
+        else:
+            assert got == r
+        comp.append(got)
+    outs = [(cd, bytearray(len(r)), c) for cd, r, c in zip(cds, raws, comp)]
+    back = C.DecompressBatchMixed(outs)
+    for (cd, buf, _), (n, e), r in zip(outs, back, raws):
+        assert e is None and n == len(r) and bytes(buf) == r
+    # an unknown codec id fails alone; its neighbours still decode
+    lib = L.load()
+    import ctypes
+    nb = 3
+    iov = (L.JfsIov * nb)()
+    keep = []
+    for i in range(nb):
+        src = comp[i]
+        dst = bytearray(len(raws[i]))
+        keep.append((src, dst))
+        iov[i].src = ctypes.cast(ctypes.c_char_p(src), ctypes.c_void_p)
+        iov[i].src_len = len(src)
+        iov[i].dst = ctypes.addressof((ctypes.c_char * len(dst)).from_buffer(dst))
+        iov[i].dst_cap = len(dst)
+    algos = (ctypes.c_int32 * nb)(cds[0].algo, 7, cds[2].algo)
+    out = (ctypes.c_int64 * nb)()
+    assert lib.jfs_decompress_batch_mixed(algos, nb, iov, out, 0) == 0
+    assert out[0] == len(raws[0]) and out[1] == L.JFS_ERR_INVALID and out[2] == len(raws[2])
+    assert bytes(keep[0][1]) == raws[0] and bytes(keep[2][1]) == raws[2]
