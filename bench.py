@@ -57,6 +57,12 @@ ZSTD_KERNEL_SOURCES = ("juicefs_amd/csrc/zstd_decode.hip", "juicefs_amd/csrc/zst
                        "juicefs_amd/csrc/wave.cuh", "juicefs_amd/csrc/jfs_internal.h")
 
 
+
+def _mark(name):
+    """(JFS_HOST_TRACE) a leg marker on stderr, on the library's trace clock"""
+    if os.environ.get("JFS_HOST_TRACE"):
+        print(f"[bench] t={time.monotonic() * 1e3:.2f} leg {name}", file=sys.stderr, flush=True)
+
 def kernel_src_sha256(sources=KERNEL_SOURCES) -> str:
     """Stamp of a kernel's sources (profiles/traffic*.json carry it): the LZ4
     decode kernel by default, ZSTD_KERNEL_SOURCES for the Zstd decoder."""
@@ -547,6 +553,7 @@ def dealer_legs(batch, U, a):
     lib.jfs_stats_reset()
     out = {"host_path": host_path_rate(comp, raws, U, a.host_blocks, device_mask=0)}
     if not a.no_mixed:
+        _mark("mixed_host_path")
         out["mixed_host_path"] = mixed_host_path(raws, a.mixed_blocks, device_mask=0)
     ds = (L.JfsDeviceStat * 64)()
     nd = lib.jfs_device_stats(ds, 64)
@@ -858,23 +865,28 @@ def main():
     extras = not a.no_extras
     if extras and a.codec == "lz4":
         try:
+            _mark("configs_3")
             out["configs_3"] = configs3_zstd(a, S, world, rank, dev)
         except Exception as e:  # report, never fake
             out["configs_3"] = {"error": repr(e)}
         try:
+            _mark("configs_2")
             out["configs_2"] = configs2_roundtrip(a, S, world, rank, dev)
         except Exception as e:
             out["configs_2"] = {"error": repr(e)}
         try:
+            _mark("checksum_aead")
             out["checksum_aead"] = checksum_and_aead(batch, S, world, dev)
         except Exception as e:
             out["checksum_aead"] = {"error": repr(e)}
         try:
+            _mark("lz4_other_classes")
             out["lz4_other_classes"] = other_classes(a, S, world, rank, dev)
         except Exception as e:
             out["lz4_other_classes"] = {"error": repr(e)}
     if extras and a.codec == "lz4" and world > 1 and not a.no_host_path:
         try:
+            _mark("host_path_ranked")
             out["host_path_ranked"] = ranked_host_path(S, world, rank, local, dev, a.c0_blocks // 4, U)
         except Exception as e:
             out["host_path_ranked"] = {"error": repr(e)}
@@ -883,6 +895,7 @@ def main():
         # = all), round-robin per block; the other ranks wait at the barrier
         if rank == 0:
             try:
+                _mark("dealer_all_gpus")
                 out["dealer_all_gpus"] = dealer_legs(batch, U, a)
             except Exception as e:
                 out["dealer_all_gpus"] = {"error": repr(e)}
@@ -915,6 +928,7 @@ def main():
                                        "note": "one GPU Zstd encode launch; frames verified by the GPU decoder"}
             except Exception as e:  # report, never fake
                 ex["zstd_compress"] = {"error": repr(e)}
+            _mark("compress")
             out["compress"] = ex
             if not a.no_cpu_baseline:
                 try:
@@ -925,19 +939,23 @@ def main():
             if not a.no_host_path:
                 raw_blocks = [batch.raw[i * U:(i + 1) * U].cpu().numpy().tobytes() for i in range(ns)]
                 try:
+                    _mark("configs_0")
                     out["configs_0"] = configs0_roundtrip(dev, a.c0_blocks, U)
                 except Exception as e:
                     out["configs_0"] = {"error": repr(e)}
                 try:
+                    _mark("host_path")
                     out["host_path"] = host_path_rate(comp_blocks, raw_blocks, U, a.host_blocks)
                 except Exception as e:
                     out["host_path"] = {"error": repr(e)}
                 try:
+                    _mark("oneshot_concurrency")
                     out["oneshot_concurrency"] = oneshot_concurrency(comp_blocks, raw_blocks, U)
                 except Exception as e:
                     out["oneshot_concurrency"] = {"error": repr(e)}
                 if not a.no_mixed:
                     try:
+                        _mark("mixed_host_path")
                         out["mixed_host_path"] = mixed_host_path(raw_blocks, a.mixed_blocks)
                     except Exception as e:
                         out["mixed_host_path"] = {"error": repr(e)}

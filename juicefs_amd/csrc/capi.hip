@@ -42,6 +42,21 @@ constexpr int64_t LZ4_MAX_INPUT = 0x7E000000;
 
 inline int64_t align16(int64_t x) { return (x + 15) & ~(int64_t)15; }
 
+// JFS_HOST_TRACE=1: per-chunk host timings on stderr (diagnostics)
+bool host_trace() {
+    static bool v = getenv("JFS_HOST_TRACE") != nullptr;
+    return v;
+}
+double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+// (trace) a staging or scratch allocation: hipFree waits for the whole device
+void trace_alloc(const char *what, int64_t bytes, double t0) {
+    if (host_trace())
+        fprintf(stderr, "[jfs host] t=%.2f alloc %s %.1f MiB %.2f ms\n", now_ms(), what, bytes / 1048576.0,
+                now_ms() - t0);
+}
+
 // One pinned host + device staging area: chunk k of a batch uses slot
 // k % NSLOT, so chunk k+1's H2D and chunk k-1's D2H run while chunk k's
 // kernel runs.  (Four slots measured 42.8 vs 42.0 GiB/s on a lone 4,096-block
@@ -90,6 +105,7 @@ struct Slot {
 
     bool ensure_split(int64_t bytes) {
         if (bytes <= sp_cap) return true;
+        const double t0 = host_trace() ? now_ms() : 0.0;
         if (sp) (void)hipFree(sp);
         sp = nullptr;
         sp_cap = 0;
@@ -97,18 +113,21 @@ struct Slot {
         while (want < bytes) want <<= 1;
         if (hipMalloc((void **)&sp, (size_t)want) != hipSuccess) return false;
         sp_cap = want;
+        trace_alloc("split", want, t0);
         return true;
     }
 
     bool ensure_zstd(const uint64_t *t) {  // t: items, literal bytes, table cells
         auto grow = [](auto **p, uint64_t *cap, uint64_t want, size_t elem) {
             if (*cap >= want) return true;
+            const double t0 = host_trace() ? now_ms() : 0.0;
             if (*p) (void)hipFree(*p);
             *p = nullptr;
             *cap = 0;
             const uint64_t n = want + want / 4;
             if (hipMalloc((void **)p, (size_t)(n * elem)) != hipSuccess) return false;
             *cap = n;
+            trace_alloc("zstd", (int64_t)(n * elem), t0);
             return true;
         };
         return grow(&z_items, &z_items_cap, t[0], 16) && grow(&z_lit, &z_lit_cap, t[1], 1) &&
@@ -121,6 +140,7 @@ struct Slot {
         int64_t want = 64ll << 20;
         while (want < bytes) want <<= 1;
         if (bytes > staging_max_bytes()) return false;
+        const double t0 = host_trace() ? now_ms() : 0.0;
         if (bytes > h_cap) {
             if (h) (void)hipHostFree(h);
             if (hipHostMalloc((void **)&h, (size_t)want, hipHostMallocDefault) != hipSuccess) {
@@ -129,6 +149,7 @@ struct Slot {
                 return false;
             }
             h_cap = want;
+            trace_alloc("pinned", want, t0);
         }
         if (bytes > d_cap) {
             if (d) (void)hipFree(d);
@@ -138,6 +159,7 @@ struct Slot {
                 return false;
             }
             d_cap = want;
+            trace_alloc("device", want, t0);
         }
         return true;
     }
@@ -157,6 +179,7 @@ struct Lane {
     std::mutex mu;  // serialises use of this lane's slots
     Slot slot[NSLOT];
     hipStream_t s_k = nullptr;  // this lane's kernels, in chunk order
+    std::atomic<int> kind{-1};  // algo * 2 + dir of the batch it last ran (acquire_lane)
     // free the pinned host and HBM staging (caller holds mu)
     void release_staging() {
         for (Slot &sl : slot) {
@@ -193,14 +216,19 @@ struct DevCtx {
     std::atomic<uint64_t> batches{0}, blocks{0};  // per-device counters (jfs_device_stats)
 
     // a lane for a batch call: a free one if any, else wait for one
-    Lane &acquire_lane(std::unique_lock<std::mutex> &lk) {
-        for (int k = 0; k < NLANE; k++) {
-            std::unique_lock<std::mutex> t(lane[k].mu, std::try_to_lock);
-            if (t.owns_lock()) {
-                lk = std::move(t);
-                return lane[k];
+    // (kind = algo * 2 + dir, or -1: a free lane that last ran the same kind
+    // first, since its staging and scratch already fit such batches -- a lane
+    // that must grow them waits on hipFree, i.e. on the whole device)
+    Lane &acquire_lane(std::unique_lock<std::mutex> &lk, int kind = -1) {
+        for (int pass = kind < 0 ? 1 : 0; pass < 2; pass++)
+            for (int k = 0; k < NLANE; k++) {
+                if (pass == 0 && lane[k].kind.load(std::memory_order_relaxed) != kind) continue;
+                std::unique_lock<std::mutex> t(lane[k].mu, std::try_to_lock);
+                if (t.owns_lock()) {
+                    lk = std::move(t);
+                    return lane[k];
+                }
             }
-        }
         Lane &l = lane[next_lane.fetch_add(1) % NLANE];
         lk = std::unique_lock<std::mutex>(l.mu);
         return l;
@@ -608,15 +636,6 @@ void par_copy(std::vector<CopyJob> &jobs) {
     pool.run(pc);
 }
 
-// JFS_HOST_TRACE=1: per-chunk host timings on stderr (diagnostics)
-bool host_trace() {
-    static bool v = getenv("JFS_HOST_TRACE") != nullptr;
-    return v;
-}
-double now_ms() {
-    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
-
 // LZ4 encode batches of at most this many blocks take the segment-parallel
 // parse (lz4_encode.hip, lz4_eseg): latency of a few segment parses instead of
 // one whole-block parse per wave
@@ -680,6 +699,7 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
     DevGuard guard;
     (void)hipSetDevice(dev->id);
     dev->last_use_ms = steady_ms();
+    ln.kind.store(algo * 2 + dir, std::memory_order_relaxed);
     dev->batches.fetch_add(1, std::memory_order_relaxed);
     dev->blocks.fetch_add((uint64_t)nblk, std::memory_order_relaxed);
     if (OpStats *st = op_stats(algo, dir)) st->batches.fetch_add(1, std::memory_order_relaxed);
@@ -1052,8 +1072,8 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
                 return JFS_ERR_HIP;
         }
         if (host_trace())
-            fprintf(stderr, "[jfs host] t=%.2f chunk %d-%d stage-in %.1f MiB %.2f ms\n", now_ms(), c.s, c.e,
-                    c.tin / 1048576.0, now_ms() - t0);
+            fprintf(stderr, "[jfs host] t=%.2f lane %d algo %d dir %d chunk %d-%d stage-in %.1f MiB %.2f ms\n",
+                    now_ms(), (int)(&ln - dev->lane), algo, dir, c.s, c.e, c.tin / 1048576.0, now_ms() - t0);
         const int n = c.e - c.s;
         uint64_t ztot[6] = {0, 0, 0, 0, 0, 0};
         if (ae) return launch_aead(c, sl, h_in, h_out, h_desc, h_ret, d_in, d_out, d_desc, d_ret);
@@ -1206,6 +1226,30 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
         return JFS_OK;
     };
     const int nch = (int)ch.size();
+    // Size every slot for all of its chunks (staging, LZ4 small-batch scratch)
+    // before the first launch: growing a slot mid-batch frees the old buffer,
+    // and hipFree waits for the whole device -- the batch's own chunks in
+    // flight (64 ms of a 273 ms 1,024-block decode).  A size that cannot be
+    // had is left to the chunk's own ensure(), which reports it.
+    {
+        int64_t need[NSLOT] = {}, need_sp[NSLOT] = {};
+        for (const Chunk &c : ch) {
+            need[c.slot] = std::max(need[c.slot], chunk_bytes(c));
+            const int n = c.e - c.s;
+            if (algo == JFS_ALGO_LZ4 && dir == DECOMPRESS && !ae && n <= split_max()) {
+                std::vector<int32_t> lens(n), caps(n);
+                for (int k = 0; k < n; k++) {
+                    lens[k] = (int32_t)iov[c.s + k].src_len;
+                    caps[k] = (int32_t)std::min<int64_t>(cap[c.s + k], INT32_MAX);
+                }
+                need_sp[c.slot] = std::max(need_sp[c.slot], jfs_lz4_split_scratch_bytes(n, lens.data(), caps.data()));
+            }
+        }
+        for (int s = 0; s < NSLOT; s++) {
+            if (need[s] > 0) (void)ln.slot[s].ensure(need[s]);
+            if (need_sp[s] > 0) (void)ln.slot[s].ensure_split(need_sp[s]);
+        }
+    }
     int64_t rc = JFS_OK;
     int done = 0;  // chunks [0, done) finished
     auto finish_next = [&]() -> int64_t {
@@ -1606,7 +1650,7 @@ int64_t deal(int algo, int dir, const std::vector<int> &todo, const std::vector<
         p.crc.assign(p.iov.size(), 0u);
         uint32_t *pc = crc ? p.crc.data() : nullptr;
         std::unique_lock<std::mutex> lk;
-        Lane &ln = ds[g]->acquire_lane(lk);
+        Lane &ln = ds[g]->acquire_lane(lk, algo * 2 + dir);
         if (ae_all) {
             Aead a{ae_all->cipher, ae_all->seal, p.orig.data(), p.key.data(), p.nonce.data(),
                    ae_all->sp ? p.sp.data() : nullptr, ae_all->hdr ? p.hdr.data() : nullptr};
