@@ -512,7 +512,9 @@ bool host_ramp() { return host_ramp_len() > 0; }
 // LZ4 compress chunks: the serial-parse encoder holds 8 blocks per CU and a
 // launch lasts one block's parse (~0.5 s) whatever its size, so a 2 GiB chunk
 // (256 blocks at ~8 MiB staged each) fills an eighth of the GPU; 4 GiB chunks
-// (512 blocks) with two chunk kernels side by side fill half of it.
+// (512 blocks) with two chunk kernels side by side fill half of it.  The
+// same holds for Zstd compress (one frame's serial parse, ~0.7 s at 4 MiB):
+// a mixed 64 KiB-4 MiB batch in 1 GiB chunks paid its longest chain per chunk.
 // JFS_HOST_CHUNK_MB_LZ4C overrides.
 int64_t chunk_limit_lz4c() {
     static int64_t v = [] {
@@ -722,7 +724,8 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
     };
     std::vector<Chunk> ch;
     {
-        const int64_t limit = algo == JFS_ALGO_LZ4 && dir == COMPRESS && !ae ? chunk_limit_lz4c() : chunk_limit();
+        const int64_t limit =
+            (algo == JFS_ALGO_LZ4 || algo == JFS_ALGO_ZSTD) && dir == COMPRESS && !ae ? chunk_limit_lz4c() : chunk_limit();
         // Decode ramp: the first output cannot leave before chunk 0's H2D and
         // kernel are done, and the one-workgroup-per-block kernels take a
         // block's whole latency (~20 ms) whatever the chunk size; so a long
