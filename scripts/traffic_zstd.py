@@ -13,24 +13,29 @@ sys.path.insert(0, ROOT)
 
 
 def per_kernel(path, counter):
-    """{kernel short name: KiB summed over its dispatches} for jfs::zstdd kernels"""
-    d = {}
+    """{kernel short name: KiB per decode launch} for jfs::zstdd kernels: the
+    sum over the profiled run's dispatches divided by its number of launches
+    (zexec_kernel runs once per launch)"""
+    d, launches = {}, set()
     for r in csv.DictReader(open(path)):
         k = r["Kernel_Name"]
         if "zstdd::" not in k or r["Counter_Name"] != counter:
             continue
         name = k.split("zstdd::")[1].split("(")[0]
         d[name] = d.get(name, 0.0) + float(r["Counter_Value"])
-    if not d:
+        if name == "zexec_kernel":
+            launches.add(r["Dispatch_Id"])
+    if not d or not launches:
         raise SystemExit(f"no jfs::zstdd {counter} rows in {path}")
-    return d
+    return {k: v / len(launches) for k, v in d.items()}, len(launches)
 
 
 fpath, wpath, nblk, bb = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
-f, w = per_kernel(fpath, "FETCH_SIZE"), per_kernel(wpath, "WRITE_SIZE")
+(f, nf), (w, nw) = per_kernel(fpath, "FETCH_SIZE"), per_kernel(wpath, "WRITE_SIZE")
 fk, wk = sum(f.values()), sum(w.values())
 out = {
     "blocks": nblk, "block_bytes": bb, "kernels": "every jfs::zstdd kernel of one jfs_zstd_decompress_device launch",
+    "launches_profiled": [nf, nw],
     "fetch_size_kb": fk, "write_size_kb": wk,
     "per_kernel_kb": {k: {"fetch": f.get(k, 0.0), "write": w.get(k, 0.0)} for k in sorted(set(f) | set(w))},
     "hbm_bytes_raw": (fk + wk) * 1024.0,
