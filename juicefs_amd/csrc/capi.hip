@@ -1356,8 +1356,12 @@ Gather gather_window(int dir) {
             if (end && *end == ',') g[COMPRESS_DIR] = std::max(0ll, strtoll(end + 1, nullptr, 10));
         }
     });
+    static const int64_t mx = [] {  // JFS_GATHER_MAX_X: max = gap x this (default 16)
+        const char *e = getenv("JFS_GATHER_MAX_X");
+        return e ? std::max(1ll, atoll(e)) : 16ll;
+    }();
     const int64_t gap = g[dir == DECOMPRESS_DIR ? DECOMPRESS_DIR : COMPRESS_DIR];
-    return {gap, gap * 16};
+    return {gap, gap * mx};
 }
 
 // Work of one block for the dealer: the bytes it stages in and out.
