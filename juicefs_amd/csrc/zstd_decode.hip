@@ -1149,6 +1149,9 @@ struct ASmem {  // zseqa: table-build scratch
     int16_t norm[64];
     uint8_t symat[512], mark[512], ksym[512];
 };
+#ifndef JFS_ZSEQ_STATE32
+#define JFS_ZSEQ_STATE32 1  // state pass: the three next-state reads from one 32-bit field of the window
+#endif
 #ifndef JFS_ZSEQ_AB
 #define JFS_ZSEQ_AB 1  // decoder: serial state pass + lane-parallel value pass per period
 #endif
@@ -1975,9 +1978,20 @@ __device__ __forceinline__ void zdecode(SeqSmem &sm, int gn, uint32_t &r0, uint3
                         const uint32_t nbl = kl31 + (uint32_t)__builtin_clz(nsl);
                         const uint32_t nbm = km31 + (uint32_t)__builtin_clz(nsm);
                         const uint32_t nbo = ko31 + (uint32_t)__builtin_clz(nso);
+#if JFS_ZSEQ_STATE32
+                        // the three state reads (<= 9 + 9 + 8 bits) all lie in the
+                        // window's top 32 bits: one extraction, three field reads
+                        const uint32_t x = (uint32_t)(h2 >> 32);
+                        const uint32_t ol = 32u - nbl, om = ol - nbm, oo = om - nbo;
+                        sll = ((nsl << nbl) - szl) + __builtin_amdgcn_ubfe(x, ol, nbl);
+                        sml = ((nsm << nbm) - szm) + __builtin_amdgcn_ubfe(x, om, nbm);
+                        sof = ((nso << nbo) - szo) + __builtin_amdgcn_ubfe(x, oo, nbo);
+                        c2 = (int32_t)(32u - oo);
+#else
                         sll = ((nsl << nbl) - szl) + zw_get(h2, c2, nbl);
                         sml = ((nsm << nbm) - szm) + zw_get(h2, c2, nbm);
                         sof = ((nso << nbo) - szo) + zw_get(h2, c2, nbo);
+#endif
                     }
                     left -= c + c2;
                     ++i;
