@@ -1956,13 +1956,17 @@ __device__ __forceinline__ void zdecode(SeqSmem &sm, int gn, uint32_t &r0, uint3
     }
     const uint32_t szl = 1u << all, szo = 1u << alof, szm = 1u << alml;
     const uint32_t kl31 = (uint32_t)all - 31u, ko31 = (uint32_t)alof - 31u, km31 = (uint32_t)alml - 31u;
+    // 0: running or ended before, 1: stream overflow, 2: last sequence with
+    // the stream exactly consumed (BEND), 3: last sequence, bits left (ERR);
+    // the item is stored once per period, after the unrolled sequences
+    uint32_t fin = 0;
     for (int p = 0;; ++p) {
         const int32_t i0 = i;
 #pragma unroll
         for (int k = 0; k < ZK2; ++k) {
             if (run) {
                 if (left < m8) {  // overflow
-                    it[2 + i] = make_uint4(0, 0, (uint32_t)E_CORRUPT, IT_ERR);
+                    fin = 1;
                     run = false;
                 } else {
                     const uint32_t cl = tl[sll], co = to[sof], cm = tm[sml];
@@ -1996,11 +2000,15 @@ __device__ __forceinline__ void zdecode(SeqSmem &sm, int gn, uint32_t &r0, uint3
                     left -= c + c2;
                     ++i;
                     if (i == d.nseq) {
-                        it[2 + i] = left == m8 ? make_uint4(0, 0, 0, IT_BEND) : make_uint4(0, 0, (uint32_t)E_CORRUPT, IT_ERR);
+                        fin = left == m8 ? 2u : 3u;
                         run = false;
                     }
                 }
             }
+        }
+        if (fin) {
+            it[2 + i] = fin == 2 ? make_uint4(0, 0, 0, IT_BEND) : make_uint4(0, 0, (uint32_t)E_CORRUPT, IT_ERR);
+            fin = 0;
         }
         if (l < ZNB) {
             sm.rcnt[p & 1][l] = i - i0;
