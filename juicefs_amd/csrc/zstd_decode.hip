@@ -1848,6 +1848,9 @@ __device__ __forceinline__ uint32_t zsub(uint32_t x, uint32_t a0, uint32_t a1, u
     return y > dd ? y - dd : 1u;
 }
 __device__ __forceinline__ void zvalues(SeqSmem &sm, int gn, int b) {
+#ifdef JFS_SKIP_ZVALUES  // diagnostics: the state pass alone (wrong output)
+    return;
+#endif
     const int l = lane_id();
     const int j = l & (ZNB - 1);
     static_assert(ZNB == 16 && ZK2 == 8, "value pass layout: 16 blocks x 4 records per round, two rounds");
