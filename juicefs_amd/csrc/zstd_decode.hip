@@ -3103,12 +3103,13 @@ __device__ __forceinline__ void x_match(XSmem &s, X &x, uint32_t off, int32_t le
 
 // Execute items [0, n) of a checked run (lane j holds item j): split into
 // lane-parallel batches; long items are copied by the whole wave.
+// (incl / lincl: inclusive prefix sums over the lanes of len and lln as
+// below, computed by the caller)
 __device__ __forceinline__ void x_run(XSmem &s, X &x, uint32_t n, uint32_t ll, uint32_t ml, uint32_t off,
-                                      int64_t *lp) {
+                                      int64_t *lp, uint32_t incl, uint32_t lincl) {
     const int l = lane_id();
     const bool in = (uint32_t)l < n;
     const uint32_t len = in ? ll + ml : 0u, lln = in ? ll : 0u;
-    const uint32_t incl = dpp_scan_add(len), lincl = dpp_scan_add(lln);
     const int32_t O0run = x.op;
     const int32_t o = O0run + (int32_t)(incl - len);
     const int32_t lit = (int32_t)*lp + (int32_t)(lincl - lln);
@@ -3226,11 +3227,17 @@ __global__ __launch_bounds__(64) void zexec_kernel(const jfs_dev_block *__restri
                 const uint64_t bad = __ballot(in && (fdst || flit || foff));
                 const uint32_t nexec = bad ? (uint32_t)__builtin_ctzll(bad) : r;
                 const int32_t code = (int32_t)readlane(fdst ? (uint32_t)E_DSTSMALL : (uint32_t)E_CORRUPT, (int)(nexec & 63));
-                const uint32_t el = (uint32_t)l < nexec ? len : 0u, ell = (uint32_t)l < nexec ? lln : 0u;
-                const uint32_t tot = readlane(dpp_scan_add(el), 63), totll = readlane(dpp_scan_add(ell), 63);
-                if (nexec) x_run(s, x, nexec, ll, ml, off, &lp);
+                // the run's prefix sums serve the copies too; only a run cut
+                // short by a bad item needs them again over its first nexec lanes
+                uint32_t xincl = incl, xlincl = lincl;
+                if (nexec < r) {
+                    const uint32_t el = (uint32_t)l < nexec ? len : 0u, ell = (uint32_t)l < nexec ? lln : 0u;
+                    xincl = dpp_scan_add(el);
+                    xlincl = dpp_scan_add(ell);
+                }
+                const uint32_t totll = readlane(xlincl, 63);
+                if (nexec) x_run(s, x, nexec, ll, ml, off, &lp, xincl, xlincl);
                 lused += (int32_t)totll;
-                (void)tot;
                 if (bad) { result = code; done = true; break; }
                 k += r - 1;
             } else if (kind == IT_BSTART) {
