@@ -2202,6 +2202,15 @@ extern "C" int jfs_launch_zstd_encode(const jfs_dev_block *d_blocks, int nblk, i
                 }
                 if (g.cnt) grps.push_back(g);
             }
+        // Longest chain first: a launch lasts its longest frame's serial parse,
+        // and workgroups start in index order (a 4 MiB frame queued behind
+        // 1,000 small ones starts late), so each group lists its frames by
+        // decreasing size and the groups launch largest frame first.
+        for (const Grp &g : grps)
+            std::stable_sort(lists.begin() + g.off, lists.begin() + g.off + g.cnt,
+                             [&](int32_t a, int32_t b) { return fi[a].n > fi[b].n; });
+        std::stable_sort(grps.begin(), grps.end(),
+                         [&](const Grp &a, const Grp &b) { return fi[lists[a.off]].n > fi[lists[b.off]].n; });
         const int flist_off = (int)lists.size();
         for (int f : todo) lists.push_back(f);
         for (int f : todo)
