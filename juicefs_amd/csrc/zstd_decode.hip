@@ -767,6 +767,9 @@ __global__ __launch_bounds__(PLAN_T) void zplan_kernel(ZInfo *__restrict__ info,
 // ---------------------------------------------------------------------------
 // kernel 2: entropy decode (wave 0 literals, wave 1 sequences)
 // ---------------------------------------------------------------------------
+#ifndef JFS_ZLIT_QUAD
+#define JFS_ZLIT_QUAD 1  // Huffman streams: four symbols per step (two per refill, one aligned word store)
+#endif
 struct LitSmem {
     uint16_t huf[4096];  // sym | nb << 8
     uint8_t stage[256];
@@ -934,6 +937,35 @@ __device__ __forceinline__ int32_t lit_block(LitSmem &sm, const gc_u8 *in, const
         } else {
             const int64_t start = o, end = o + mycnt;
             uint32_t acc = 0;
+#if JFS_ZLIT_QUAD
+            // one symbol: peek, table, consume (no refill: a refill leaves >= 32
+            // bits in the container, two symbols take <= 24)
+            auto sym = [&]() -> uint32_t {
+                const uint32_t e = sm.huf[br_peek(r, maxbits)];
+                r.left -= (int32_t)(e >> 8);
+                return e & 0xFFu;
+            };
+            // head: up to the first 4-byte-aligned output position
+            for (; o < end && (o & 3); o++) {
+                acc |= sym() << (8 * (o & 3));
+                br_refill(r);
+                if (((o + 1) & 3) == 0) { put_word(lb, start, o + 1, acc); acc = 0; }
+            }
+            // body: four symbols, two refills and one aligned word store per step
+            for (; o + 4 <= end; o += 4) {
+                uint32_t w = sym();
+                w |= sym() << 8;
+                br_refill(r);
+                w |= sym() << 16;
+                w |= sym() << 24;
+                br_refill(r);
+                *(g_u32 *)(lb + o) = w;
+            }
+            for (; o < end; o++) {
+                acc |= sym() << (8 * (o & 3));
+                br_refill(r);
+            }
+#else
             for (; o < end; o++) {
                 uint32_t v = br_peek(r, maxbits);
                 uint32_t e = sm.huf[v];
@@ -941,6 +973,7 @@ __device__ __forceinline__ int32_t lit_block(LitSmem &sm, const gc_u8 *in, const
                 br_skip(r, (int)(e >> 8));
                 if (((o + 1) & 3) == 0) { put_word(lb, start, o + 1, acc); acc = 0; }
             }
+#endif
             if (o & 3) {
                 for (int64_t q = (o & ~3LL) > start ? (o & ~3LL) : start; q < o; q++) lb[q] = (uint8_t)(acc >> (8 * (q & 3)));
             }
