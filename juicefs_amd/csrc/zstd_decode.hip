@@ -767,6 +767,9 @@ __global__ __launch_bounds__(PLAN_T) void zplan_kernel(ZInfo *__restrict__ info,
 // ---------------------------------------------------------------------------
 // kernel 2: entropy decode (wave 0 literals, wave 1 sequences)
 // ---------------------------------------------------------------------------
+#ifndef JFS_ZLIT_FASTPEEK
+#define JFS_ZLIT_FASTPEEK 1  // zlit body steps away from the stream start peek without the start check
+#endif
 #ifndef JFS_ZLIT_QUAD
 #define JFS_ZLIT_QUAD 1  // Huffman streams: four symbols per step (two per refill, one aligned word store)
 #endif
@@ -951,13 +954,32 @@ __device__ __forceinline__ int32_t lit_block(LitSmem &sm, const gc_u8 *in, const
                 br_refill(r);
                 if (((o + 1) & 3) == 0) { put_word(lb, start, o + 1, acc); acc = 0; }
             }
-            // body: four symbols, two refills and one aligned word store per step
+            // body: four symbols, two refills and one aligned word store per
+            // step; while the stream has 4 x maxbits bits above its start no
+            // read can reach below it, and the peek needs no start check
+            const int32_t fastlim = 8 * r.m + 4 * maxbits;
+            const uint32_t pmask = (1u << maxbits) - 1u;
+            auto fsym = [&]() -> uint32_t {
+                const int32_t lo = r.left - maxbits;
+                const uint32_t e = sm.huf[(uint32_t)(r.c >> (uint32_t)(lo - 8 * r.cb)) & pmask];
+                r.left -= (int32_t)(e >> 8);
+                return e & 0xFFu;
+            };
             for (; o + 4 <= end; o += 4) {
-                uint32_t w = sym();
-                w |= sym() << 8;
-                br_refill(r);
-                w |= sym() << 16;
-                w |= sym() << 24;
+                uint32_t w;
+                if (JFS_ZLIT_FASTPEEK && r.left >= fastlim) {
+                    w = fsym();
+                    w |= fsym() << 8;
+                    br_refill(r);
+                    w |= fsym() << 16;
+                    w |= fsym() << 24;
+                } else {
+                    w = sym();
+                    w |= sym() << 8;
+                    br_refill(r);
+                    w |= sym() << 16;
+                    w |= sym() << 24;
+                }
                 br_refill(r);
                 *(g_u32 *)(lb + o) = w;
             }
