@@ -1204,6 +1204,9 @@ struct ASmem {  // zseqa: table-build scratch
     int16_t norm[64];
     uint8_t symat[512], mark[512], ksym[512];
 };
+#ifndef JFS_ZSEQ_XALIGN
+#define JFS_ZSEQ_XALIGN 1  // state pass: the next-state bit field by one alignbit from the window dwords
+#endif
 #ifndef JFS_ZSEQ_STATE32
 #define JFS_ZSEQ_STATE32 1  // state pass: the three next-state reads from one 32-bit field of the window
 #endif
@@ -2028,14 +2031,29 @@ __device__ __forceinline__ void zdecode(SeqSmem &sm, int gn, uint32_t &r0, uint3
                     run = false;
                 } else {
                     const uint32_t cl = tl[sll], co = to[sof], cm = tm[sml];
+#if JFS_ZSEQ_XALIGN
+                    const int32_t cbw = ((left - 96) >> 5) << 2;  // as zw_fill
+                    const uint32_t *w4 = (const uint32_t *)(ring + (cbw & (ZRB2 - 1)));
+                    const uint32_t d0 = w4[0], d1 = w4[1], d2 = w4[2], d3 = w4[3];
+                    const int32_t tw = left - 8 * cbw - 64;  // [32, 64)
+#else
                     uint64_t hi;
                     uint32_t lo;
                     zw_fill(ring, left, hi, lo);
+#endif
                     sm.rec[p & 1][k][l] = make_uint2((uint32_t)left, sll | (sof << 10) | (sml << 20));
                     const int32_t c = (int32_t)((sm.lut_ll[cl & 63] >> 24) + (sm.lut_ml[cm & 63] >> 24) + (co & 63));
                     int32_t c2 = 0;
                     if (i + 1 < d.nseq) {
+#if JFS_ZSEQ_XALIGN
+                        // the 32 bits below position left - c: bits [u, u + 32) of d0..d3
+                        const uint32_t u = (uint32_t)(tw + 32 - c), wsel = u >> 5;
+                        const uint32_t lo_d = wsel == 0 ? d0 : wsel == 1 ? d1 : d2;
+                        const uint32_t hi_d = wsel == 0 ? d1 : wsel == 1 ? d2 : d3;
+                        const uint64_t h2 = (uint64_t)__builtin_amdgcn_alignbit(hi_d, lo_d, u & 31u) << 32;
+#else
                         const uint64_t h2 = zw_shift(hi, lo, c);
+#endif
                         const uint32_t nsl = cl >> 6, nso = co >> 6, nsm = cm >> 6;
                         const uint32_t nbl = kl31 + (uint32_t)__builtin_clz(nsl);
                         const uint32_t nbm = km31 + (uint32_t)__builtin_clz(nsm);
@@ -2564,7 +2582,10 @@ constexpr int FBUSE = FB - 16;
 constexpr int BSPAN = 2048;      // max output span of one lane-parallel batch
 static_assert(BSPAN <= R / 2, "a batch span and the unflushed tail fit the ring");
 #if JFS_ZEXEC_V2
-constexpr int LONGI = 64;        // items with a literal run or match longer than this go whole-wave
+#ifndef JFS_ZLONGI
+#define JFS_ZLONGI 64
+#endif
+constexpr int LONGI = JFS_ZLONGI;  // items with a literal run or match longer than this go whole-wave
 #else
 constexpr int LONGI = 1024;      // items longer than this are copied by the whole wave
 #endif
