@@ -1204,6 +1204,9 @@ struct ASmem {  // zseqa: table-build scratch
     int16_t norm[64];
     uint8_t symat[512], mark[512], ksym[512];
 };
+#ifndef JFS_ZSEQ_NEXTALL
+#define JFS_ZSEQ_NEXTALL 1  // state pass: next states computed unconditionally (no per-sequence branch)
+#endif
 #ifndef JFS_ZSEQ_XALIGN
 #define JFS_ZSEQ_XALIGN 1  // state pass: the next-state bit field by one alignbit from the window dwords
 #endif
@@ -2044,7 +2047,9 @@ __device__ __forceinline__ void zdecode(SeqSmem &sm, int gn, uint32_t &r0, uint3
                     sm.rec[p & 1][k][l] = make_uint2((uint32_t)left, sll | (sof << 10) | (sml << 20));
                     const int32_t c = (int32_t)((sm.lut_ll[cl & 63] >> 24) + (sm.lut_ml[cm & 63] >> 24) + (co & 63));
                     int32_t c2 = 0;
-                    if (i + 1 < d.nseq) {
+                    // (the next states are computed for the last sequence too --
+                    // the lane stops right after -- so no branch per sequence)
+                    if (JFS_ZSEQ_NEXTALL || i + 1 < d.nseq) {
 #if JFS_ZSEQ_XALIGN
                         // the 32 bits below position left - c: bits [u, u + 32) of d0..d3
                         const uint32_t u = (uint32_t)(tw + 32 - c), wsel = u >> 5;
@@ -2066,7 +2071,7 @@ __device__ __forceinline__ void zdecode(SeqSmem &sm, int gn, uint32_t &r0, uint3
                         sll = ((nsl << nbl) - szl) + __builtin_amdgcn_ubfe(x, ol, nbl);
                         sml = ((nsm << nbm) - szm) + __builtin_amdgcn_ubfe(x, om, nbm);
                         sof = ((nso << nbo) - szo) + __builtin_amdgcn_ubfe(x, oo, nbo);
-                        c2 = (int32_t)(32u - oo);
+                        c2 = JFS_ZSEQ_NEXTALL && i + 1 >= d.nseq ? 0 : (int32_t)(32u - oo);
 #else
                         sll = ((nsl << nbl) - szl) + zw_get(h2, c2, nbl);
                         sml = ((nsm << nbm) - szm) + zw_get(h2, c2, nbm);
