@@ -1204,6 +1204,9 @@ struct ASmem {  // zseqa: table-build scratch
     int16_t norm[64];
     uint8_t symat[512], mark[512], ksym[512];
 };
+#ifndef JFS_ZSEQ_XB8
+#define JFS_ZSEQ_XB8 1  // state pass: extra-bit counts from byte tables (no shift after the lookup)
+#endif
 #ifndef JFS_ZSEQ_NEXTALL
 #define JFS_ZSEQ_NEXTALL 1  // state pass: next states computed unconditionally (no per-sequence branch)
 #endif
@@ -1220,6 +1223,7 @@ struct SeqSmem {  // zseqb
     alignas(16) uint8_t bring[ZNB][ZRB2 + 16];   // per-lane bitstream rings (+ a mirror of block slot 0)
     alignas(16) uint16_t arena[ZNB][TAB_CELLS];  // the group's tables (LL 0, OF 512, ML 768)
     uint32_t lut_ll[36], lut_ml[53];
+    uint8_t xb_ll[64], xb_ml[64];  // extra-bit counts alone (the state pass's chain)
     GBlk g[ZNB];
     int32_t pos[2][ZNB];  // decoder bit positions published at each period's barrier
     int32_t more[2];      // any lane still decoding (per period parity)
@@ -2045,7 +2049,11 @@ __device__ __forceinline__ void zdecode(SeqSmem &sm, int gn, uint32_t &r0, uint3
                     zw_fill(ring, left, hi, lo);
 #endif
                     sm.rec[p & 1][k][l] = make_uint2((uint32_t)left, sll | (sof << 10) | (sml << 20));
+#if JFS_ZSEQ_XB8
+                    const int32_t c = (int32_t)((uint32_t)sm.xb_ll[cl & 63] + (uint32_t)sm.xb_ml[cm & 63] + (co & 63));
+#else
                     const int32_t c = (int32_t)((sm.lut_ll[cl & 63] >> 24) + (sm.lut_ml[cm & 63] >> 24) + (co & 63));
+#endif
                     int32_t c2 = 0;
                     // (the next states are computed for the last sequence too --
                     // the lane stops right after -- so no branch per sequence)
@@ -2394,6 +2402,8 @@ __global__ __launch_bounds__(128) void zseqb_kernel(const jfs_dev_block *__restr
     const int l = lane_id();
     for (int i = l; i < 36; i += 64) sm.lut_ll[i] = LL_BASE[i] | ((uint32_t)LL_BITS[i] << 24);
     for (int i = l; i < 53; i += 64) sm.lut_ml[i] = ML_BASE[i] | ((uint32_t)ML_BITS[i] << 24);
+    sm.xb_ll[l] = l < 36 ? LL_BITS[l] : (uint8_t)0;  // (codes past the tables: 0; the stream check catches them)
+    sm.xb_ml[l] = l < 53 ? ML_BITS[l] : (uint8_t)0;
     if (threadIdx.x >= 64) {  // the mover wave: one group per command from wave 0
         for (;;) {
             zsync();
