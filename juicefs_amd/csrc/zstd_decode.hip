@@ -1260,6 +1260,9 @@ struct SeqSmem {
 };
 #endif
 
+#ifndef JFS_FSE_POSPAR
+#define JFS_FSE_POSPAR 1  // sequence FSE tables: position-parallel state assignment
+#endif
 // u16 cell = sym | ns << 6  (nb = al - highbit(ns), next-state base = (ns << nb) - 2^al)
 template <class P>
 __device__ __forceinline__ void build_seq_fse_g(P t, const int16_t *norm, int32_t maxsym, int32_t al,
@@ -1302,6 +1305,27 @@ __device__ __forceinline__ void build_seq_fse_g(P t, const int16_t *norm, int32_
         if (j < size && pj <= high) { symat[pj] = ksym[k]; k++; }
     }
     __builtin_amdgcn_wave_barrier();
+#if JFS_FSE_POSPAR
+    // position-parallel: 64 cells per step; a cell's state is its symbol's
+    // counter plus its rank among the step's cells of that symbol (one ballot
+    // per distinct symbol in the step); one coalesced store per step
+    uint32_t ns = nrm == -1 ? 1u : (uint32_t)nrm;  // lane s: symbol s's next state
+    for (int c = 0; c < size; c += 64) {
+        const int u = c + l;
+        const uint32_t sym = u < size ? (uint32_t)symat[u] : 0xFFu;
+        uint32_t cell = 0;
+        for (uint64_t todo = __builtin_amdgcn_ballot_w64(u < size); todo;) {
+            const uint32_t s = (uint32_t)__builtin_amdgcn_readlane((int)sym, (int)__builtin_ctzll(todo));
+            const uint64_t m = __builtin_amdgcn_ballot_w64(sym == s);
+            const uint32_t base = (uint32_t)__builtin_amdgcn_readlane((int)ns, (int)s);
+            const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            if (sym == s) cell = s | ((base + rk) << 6);
+            if ((uint32_t)l == s) ns += (uint32_t)__builtin_popcountll(m);
+            todo &= ~m;
+        }
+        if (u < size) t[u] = (uint16_t)cell;
+    }
+#else
     const bool act = l <= maxsym && nrm != 0;
     uint32_t ns = nrm == -1 ? 1u : (uint32_t)nrm;
     for (int u4 = 0; u4 < size; u4 += 4) {
@@ -1314,6 +1338,7 @@ __device__ __forceinline__ void build_seq_fse_g(P t, const int16_t *norm, int32_
             }
         }
     }
+#endif
     __builtin_amdgcn_wave_barrier();
 }
 
@@ -1355,6 +1380,52 @@ __device__ __forceinline__ int32_t seq_table_g(SM &sm, P tabs, uint32_t area, ui
     }
     return *have ? 0 : -1;
 }
+
+#ifndef JFS_ZSEQA_DEFER
+#define JFS_ZSEQA_DEFER 1  // zseqa parses table descriptions only; zbuild spreads all blocks' tables in parallel
+#endif
+#if JFS_ZSEQA_DEFER
+// A deferred table's normalized counts wait in the last 64 cells of its own
+// region (zbuild reads them into registers before spreading over the region);
+// ZDesc.rsv carries per field maxsym (6 bits at 6f) and the build kind
+// (2 bits at 18 + 2f: 1 stored counts, 2 predefined).
+__device__ __forceinline__ uint32_t zfield_cells(int f) { return f == 1 ? 256u : 512u; }
+template <class SM>
+__device__ __forceinline__ int32_t seq_table_defer(SM &sm, g_u16 *tabs, uint32_t area, uint32_t *cur, int32_t *al,
+                                                   int32_t *have, int32_t mode, const gc_u8 *s, int32_t p, int32_t n,
+                                                   int which, uint32_t *rs) {
+    int32_t maxsym = which == 0 ? 35 : which == 1 ? 31 : 52;
+    int32_t defal = which == 1 ? 5 : 6, defmax = which == 0 ? 35 : which == 1 ? 28 : 52;
+    int32_t maxal = which == 1 ? 8 : 9;
+    const int l = lane_id();
+    if (mode == 0) {
+        *rs |= ((uint32_t)defmax << (6 * which)) | (2u << (18 + 2 * which));
+        *cur = area; *al = defal; *have = 1;
+        return 0;
+    }
+    if (mode == 1) {
+        if (n < 1) return -1;
+        uint32_t v = rd8(s, p);
+        if ((int32_t)v > maxsym) return -1;
+        if (l == 0) tabs[area] = (uint16_t)(v | (1u << 6));
+        *cur = area; *al = 0; *have = 1;
+        return 1;
+    }
+    if (mode == 2) {
+        int32_t k = n < 256 ? n : 256;
+        stage_bytes(sm.stage, s, p, k);
+        int32_t ms = maxsym, a = 0;
+        int32_t c = read_ncount(sm.stage, k, sm.norm, &ms, &a, maxal);
+        if (c < 0 || c > n) return -1;
+        __builtin_amdgcn_wave_barrier();
+        if (l <= ms) tabs[area + zfield_cells(which) - 64 + l] = (uint16_t)sm.norm[l];
+        *rs |= ((uint32_t)ms << (6 * which)) | (1u << (18 + 2 * which));
+        *cur = area; *al = a; *have = 1;
+        return c;
+    }
+    return *have ? 0 : -1;
+}
+#endif
 
 __device__ __forceinline__ uint32_t rep_dec(uint32_t v) {  // libzstd: rep0 - 1, 0 becomes 1
     if (v & SYMB) return v + 1;
@@ -2420,13 +2491,20 @@ __global__ __launch_bounds__(64) void zseqa_kernel(const jfs_dev_block *__restri
             if (cblk >= cap_cblk || slot + 3 + (uint32_t)nseq > cap_items) { bug = 1; break; }
             const uint32_t area = cblk * TAB_STRIDE;
             cblk++;
+            uint32_t rs = 0;  // deferred builds (JFS_ZSEQA_DEFER)
             if (nseq > 0) {
                 if (ip + 1 > end) { put(0, 0, (uint32_t)E_SRCSIZE, IT_ERR); break; }
                 uint32_t modes = rd8(s, ip++);
                 if ((modes & 3) && strict_reserved) { put(0, 0, (uint32_t)E_CORRUPT, IT_ERR); break; }
+#if JFS_ZSEQA_DEFER
+                int32_t c = seq_table_defer(sm, tabs, area, &t_ll, &al_ll, &hv_ll, modes >> 6, s, ip, end - ip, 0, &rs);
+                if (c >= 0) { ip += c; c = seq_table_defer(sm, tabs, area + 512, &t_of, &al_of, &hv_of, (modes >> 4) & 3, s, ip, end - ip, 1, &rs); }
+                if (c >= 0) { ip += c; c = seq_table_defer(sm, tabs, area + 768, &t_ml, &al_ml, &hv_ml, (modes >> 2) & 3, s, ip, end - ip, 2, &rs); }
+#else
                 int32_t c = seq_table_g(sm, tabs, area, &t_ll, &al_ll, &hv_ll, modes >> 6, s, ip, end - ip, 0);
                 if (c >= 0) { ip += c; c = seq_table_g(sm, tabs, area + 512, &t_of, &al_of, &hv_of, (modes >> 4) & 3, s, ip, end - ip, 1); }
                 if (c >= 0) { ip += c; c = seq_table_g(sm, tabs, area + 768, &t_ml, &al_ml, &hv_ml, (modes >> 2) & 3, s, ip, end - ip, 2); }
+#endif
                 if (c < 0) { put(0, 0, (uint32_t)E_CORRUPT, IT_ERR); break; }
                 ip += c;
             }
@@ -2438,7 +2516,7 @@ __global__ __launch_bounds__(64) void zseqa_kernel(const jfs_dev_block *__restri
                 d.item = slot;
                 d.tll = t_ll; d.tof = t_of; d.tml = t_ml;
                 d.al = (uint32_t)al_ll | ((uint32_t)al_of << 8) | ((uint32_t)al_ml << 16) | ((uint32_t)first << 24);
-                d.rsv = 0;
+                d.rsv = rs;
                 *(JFS_GLOBAL ZDesc *)(tabs + area + TAB_CELLS) = d;
             }
             first = 0;
@@ -2452,6 +2530,45 @@ __global__ __launch_bounds__(64) void zseqa_kernel(const jfs_dev_block *__restri
     }
     ZS_ADD(0, ZP_NOW() - za);
 }
+
+#if JFS_ZSEQA_DEFER
+// zbuild: spreads the FSE tables zseqa left described.  Grid (inputs, ZBUILD_Q):
+// workgroup (i, q) takes tables q, q + Q, ... of input i (three per block).
+#ifndef JFS_ZBUILD_Q
+#define JFS_ZBUILD_Q 16
+#endif
+constexpr int ZBUILD_Q = JFS_ZBUILD_Q;
+__global__ __launch_bounds__(64) void zbuild_kernel(int nblk, const ZInfo *__restrict__ info,
+                                                    uint16_t *__restrict__ tabs_all) {
+    __shared__ uint8_t symat[512], mark[512], ksym[512];
+    const int l = lane_id();
+    const int bi = blockIdx.x;
+    if (bi >= nblk) return;
+    const ZInfo zi = info[bi];
+    if (zi.ovf || zi.n_items == 0xFFFFFFFFu) return;
+    g_u16 *tabs = (g_u16 *)tabs_all + zi.tab_off;
+    const uint32_t nt = 3 * zi.n_sblk;
+    for (uint32_t t = blockIdx.y; t < nt; t += ZBUILD_Q) {
+        const uint32_t j = t / 3, f = t - 3 * j;
+        g_u16 *area = tabs + (uint64_t)j * TAB_STRIDE;
+        const uint32_t rs = ((const JFS_GLOBAL ZDesc *)(area + TAB_CELLS))->rsv;
+        const uint32_t kind = (rs >> (18 + 2 * f)) & 3u;
+        if (!kind) continue;
+        const int32_t ms = (int32_t)((rs >> (6 * f)) & 63u);
+        g_u16 *reg = area + (f == 0 ? 0 : f == 1 ? 512 : 768);
+        int32_t al;
+        if (kind == 2) {
+            const int16_t *def = f == 0 ? LL_DEF : f == 1 ? OF_DEF : ML_DEF;
+            al = f == 1 ? 5 : 6;
+            build_seq_fse_g(reg, def, ms, al, mark, ksym, symat);
+        } else {
+            const uint32_t a8 = ((const JFS_GLOBAL ZDesc *)(area + TAB_CELLS))->al;
+            al = (int32_t)((a8 >> (8 * f)) & 0xFFu);
+            build_seq_fse_g(reg, (const int16_t *)(reg + zfield_cells((int)f) - 64), ms, al, mark, ksym, symat);
+        }
+    }
+}
+#endif
 
 
 // zseqb (phases B and C): wave 0 gathers ZNB blocks' descriptors at a time
@@ -3500,6 +3617,10 @@ int launch_entropy_exec(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret,
     hipLaunchKernelGGL(zseqa_kernel, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, d_info, d_tabs, d_items,
                        g_strict_reserved);
     if (hipGetLastError() != hipSuccess) return -1;
+#if JFS_ZSEQA_DEFER
+    hipLaunchKernelGGL(zbuild_kernel, dim3(nblk, ZBUILD_Q), dim3(64), 0, stream, nblk, d_info, d_tabs);
+    if (hipGetLastError() != hipSuccess) return -1;
+#endif
     hipLaunchKernelGGL(zseqb_kernel, dim3((nblk + ZSEQ_INPUTS - 1) / ZSEQ_INPUTS), dim3(128), 0, stream, d_blocks, nblk,
                        d_info, d_tabs, d_items);
 #else
