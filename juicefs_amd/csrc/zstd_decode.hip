@@ -1128,6 +1128,9 @@ struct GBlk {
 #ifndef JFS_ZSEQ_V2
 #define JFS_ZSEQ_V2 1
 #endif
+#ifndef JFS_ZSEQ_HALF
+#define JFS_ZSEQ_HALF 1  // zseqb: two workgroups per input (blocks [0, ZNB) and the rest)
+#endif
 #ifndef JFS_ZSEQ_INPUTS
 #if JFS_ZSEQ_V2
 #define JFS_ZSEQ_INPUTS 1  // zseqb: one input per workgroup packs the CUs better (123.3 vs 125.9 ms)
@@ -2399,12 +2402,26 @@ __device__ __forceinline__ void zdecode(SeqSmem &sm, int gn, uint32_t &r0, uint3
 #endif  // JFS_ZSEQ_AB
 
 // phases B (both waves) and C (wave 0) for the collected group
-__device__ __forceinline__ void seq_group2(SeqSmem &sm, int gn, uint32_t *e0, uint32_t *e1, uint32_t *e2) {
+// carry slot of a split input: 16 bytes after the ZDesc of block ZNB - 1
+// (e0, e1, e2, ready); zseqa zeroes it, the first half publishes it
+__device__ __forceinline__ uint32_t *zcarry_slot(uint16_t *tabs_in) {
+    return (uint32_t *)(tabs_in + (uint64_t)(ZNB - 1) * TAB_STRIDE + TAB_CELLS + 24);
+}
+static_assert(sizeof(ZDesc) <= 48 && TAB_STRIDE - TAB_CELLS >= 32, "carry slot after the ZDesc");
+__device__ __forceinline__ void seq_group2(SeqSmem &sm, int gn, uint32_t *e0, uint32_t *e1, uint32_t *e2,
+                                           uint32_t *wait_carry = nullptr) {
     const int l = lane_id();
     ZS_ADD(5, 1);
     uint32_t r0 = SYMB | (0u << 29), r1 = SYMB | (1u << 29), r2 = SYMB | (2u << 29);
     uint32_t brep = 0;
     zdecode(sm, gn, r0, r1, r2, brep);
+    if (wait_carry) {  // the second half of a split input: entry offsets from the first half
+        while (__hip_atomic_load(wait_carry + 3, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+            __builtin_amdgcn_s_sleep(8);
+        *e0 = __hip_atomic_load(wait_carry + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *e1 = __hip_atomic_load(wait_carry + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *e2 = __hip_atomic_load(wait_carry + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     [[maybe_unused]] uint64_t zt = ZP_NOW();
     for (int gi = 0; gi < gn; gi++) {
         const uint32_t al = sm.g[gi].al, item = sm.g[gi].item;
@@ -2518,6 +2535,9 @@ __global__ __launch_bounds__(64) void zseqa_kernel(const jfs_dev_block *__restri
                 d.al = (uint32_t)al_ll | ((uint32_t)al_of << 8) | ((uint32_t)al_ml << 16) | ((uint32_t)first << 24);
                 d.rsv = rs;
                 *(JFS_GLOBAL ZDesc *)(tabs + area + TAB_CELLS) = d;
+#if JFS_ZSEQ_HALF
+                *(JFS_GLOBAL uint4 *)(tabs + area + TAB_CELLS + 24) = make_uint4(0, 0, 0, 0);  // carry slot
+#endif
             }
             first = 0;
             cur = slot + 3 + (uint32_t)nseq;
@@ -2601,6 +2621,49 @@ __global__ __launch_bounds__(128) void zseqb_kernel(const jfs_dev_block *__restr
 #endif
     int gn = 0;
     uint32_t e0 = 1, e1 = 4, e2 = 8;  // repeat offsets carried through phase C (reset at each frame)
+#if JFS_ZSEQ_HALF
+    // two workgroups per input: blocks [0, ZNB) and [ZNB, n); the second
+    // takes its entry repeat offsets from the first at its first phase C
+    const int bi = blockIdx.x >> 1, half = blockIdx.x & 1;
+    if (bi < nblk) {
+        const ZInfo zi = info[bi];
+        if (!(zi.ovf || zi.n_items == 0xFFFFFFFFu) && (!half || zi.n_sblk > (uint32_t)ZNB)) {
+            const gc_u16 *tabs = (const gc_u16 *)tabs_all + zi.tab_off;
+            uint32_t *carry = zcarry_slot(tabs_all + zi.tab_off);
+            g_u4 *items = (g_u4 *)items_all + zi.item_off;
+            const uint32_t j1 = half ? zi.n_sblk : umin32((uint32_t)ZNB, zi.n_sblk);
+            for (uint32_t j = half ? (uint32_t)ZNB : 0u; j < j1;) {
+                const uint32_t take = umin32((uint32_t)ZNB, j1 - j);
+                if ((uint32_t)l < take) {
+                    const ZDesc d = *(const JFS_GLOBAL ZDesc *)(tabs + (uint64_t)(j + l) * TAB_STRIDE + TAB_CELLS);
+                    GBlk &g = sm.g[l];
+                    g.bs = (const gc_u8 *)(uintptr_t)d.bs;
+                    g.in = g.bs;
+                    g.ib = items;
+                    g.bsz = d.bsz;
+                    g.nseq = d.nseq;
+                    g.item = d.item;
+                    g.tll = zi.tab_off + d.tll; g.tof = zi.tab_off + d.tof; g.tml = zi.tab_off + d.tml;
+                    g.al = d.al;
+                }
+                __builtin_amdgcn_wave_barrier();
+                if (l == 0) sm.cmd = (int)take;
+                zsync();
+                seq_group2(sm, (int)take, &e0, &e1, &e2, half && j == (uint32_t)ZNB ? carry : nullptr);
+                j += take;
+            }
+            if (!half && zi.n_sblk > (uint32_t)ZNB && l == 0) {
+                __hip_atomic_store(carry + 0, e0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(carry + 1, e1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(carry + 2, e2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(carry + 3, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+    if (l == 0) sm.cmd = 0;
+    zsync();  // releases the mover
+}
+#else
     for (int f = 0; f < ZSEQ_INPUTS; ++f) {
         const int bi = blockIdx.x * ZSEQ_INPUTS + f;
         if (bi >= nblk) break;
@@ -2641,6 +2704,7 @@ __global__ __launch_bounds__(128) void zseqb_kernel(const jfs_dev_block *__restr
     if (l == 0) sm.cmd = 0;
     zsync();  // releases the mover
 }
+#endif  // JFS_ZSEQ_HALF
 #else
 __global__ __launch_bounds__(64) void zseq_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
                                                       ZInfo *__restrict__ info, uint16_t *__restrict__ tabs_all,
@@ -3621,8 +3685,13 @@ int launch_entropy_exec(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret,
     hipLaunchKernelGGL(zbuild_kernel, dim3(nblk, ZBUILD_Q), dim3(64), 0, stream, nblk, d_info, d_tabs);
     if (hipGetLastError() != hipSuccess) return -1;
 #endif
+#if JFS_ZSEQ_HALF
+    static_assert(ZSEQ_INPUTS == 1, "split inputs: one input per workgroup pair");
+    hipLaunchKernelGGL(zseqb_kernel, dim3(2 * nblk), dim3(128), 0, stream, d_blocks, nblk, d_info, d_tabs, d_items);
+#else
     hipLaunchKernelGGL(zseqb_kernel, dim3((nblk + ZSEQ_INPUTS - 1) / ZSEQ_INPUTS), dim3(128), 0, stream, d_blocks, nblk,
                        d_info, d_tabs, d_items);
+#endif
 #else
     hipLaunchKernelGGL(zseq_kernel, dim3((nblk + ZSEQ_INPUTS - 1) / ZSEQ_INPUTS), dim3(64), 0, stream, d_blocks, nblk,
                        d_info, d_tabs, d_items, g_strict_reserved);
