@@ -782,8 +782,14 @@ struct LitSmem {
     uint16_t symnext[256];
     uint32_t fse[64];    // weight FSE table (al <= 6)
     uint32_t rank[16];
-    int32_t maxbits, valid;
+    int32_t cur;     // current Huffman table: -1 none, 0 / 1 cells [0, 2048) / [2048, 4096), 2 all 4096 (12 bits)
+    int32_t smb[3];  // max bits of the table in each of those places
 };
+__device__ __forceinline__ void lit_set_cur(LitSmem &sm, int32_t place, int32_t maxbits) {
+    sm.cur = place;  // (uniform stores)
+    sm.smb[place] = maxbits;
+    __builtin_amdgcn_wave_barrier();
+}
 // stage `n` (<= 256) bytes starting at s+p into LDS (zero-padded)
 __device__ __forceinline__ void stage_bytes(uint8_t *dst, const gc_u8 *s, int32_t p, int32_t n) {
     const int l = lane_id();
@@ -791,8 +797,11 @@ __device__ __forceinline__ void stage_bytes(uint8_t *dst, const gc_u8 *s, int32_
     __builtin_amdgcn_wave_barrier();
 }
 
-// Huffman table description -> sm.huf.  Returns bytes used or -1.
-__device__ __forceinline__ int32_t read_huf(LitSmem &sm, const gc_u8 *in, const gc_u8 *s, int32_t p, int32_t n) {
+// Huffman table description -> sm.huf at cell 2048 * slot (a 12-bit table:
+// cell 0, all 4096 cells).  Returns bytes used, -1 (corrupt) or -2 (a 12-bit
+// table with narrow_only: nothing written to the table cells).
+__device__ __forceinline__ int32_t read_huf(LitSmem &sm, const gc_u8 *in, const gc_u8 *s, int32_t p, int32_t n,
+                                           int slot, bool narrow_only, int32_t *maxbits_out) {
     const int l = lane_id();
     if (n < 1) return -1;
     int32_t hb = (int32_t)rd8(s, p);
@@ -856,6 +865,8 @@ __device__ __forceinline__ int32_t read_huf(LitSmem &sm, const gc_u8 *in, const 
     r1 += lastw == 1;
     nw++;
     if (r1 < 2 || (r1 & 1)) return -1;
+    if (maxbits == 12 && narrow_only) return -2;
+    const uint32_t hbase = maxbits == 12 ? 0u : 2048u * (uint32_t)slot;
     __builtin_amdgcn_wave_barrier();
     // rank starts (weight ascending, then symbol order)
     uint32_t cnt = 0;
@@ -872,12 +883,12 @@ __device__ __forceinline__ int32_t read_huf(LitSmem &sm, const gc_u8 *in, const 
         uint32_t len = 1u << (wi - 1);
         uint32_t st = sm.rank[wi];
         uint16_t e = (uint16_t)(i | ((maxbits + 1 - wi) << 8));
-        for (uint32_t u = l; u < len; u += 64) sm.huf[st + u] = e;
+        for (uint32_t u = l; u < len; u += 64) sm.huf[hbase + st + u] = e;
         __builtin_amdgcn_wave_barrier();
         if (l == 0) sm.rank[wi] = st + len;
         __builtin_amdgcn_wave_barrier();
     }
-    sm.maxbits = maxbits;  // (uniform store)
+    *maxbits_out = maxbits;
     __builtin_amdgcn_wave_barrier();
     return used;
 }
@@ -892,48 +903,47 @@ __device__ __forceinline__ void put_word(g_u8 *lb, int64_t start, int64_t end4, 
     }
 }
 
-__device__ __forceinline__ int32_t lit_block(LitSmem &sm, const gc_u8 *in, const gc_u8 *s, const LitHdr &h, int32_t bpos,
-                             g_u8 *lb, int64_t lpos) {
+// A Huffman literal section ready to decode: the stream section (jump table
+// and streams) and the table it uses.
+struct LJob {
+    int32_t p, n;          // stream section within s
+    int32_t regen, streams;
+    int64_t lpos;          // first output byte in the literal buffer
+    int32_t hb, mb;        // table cell base, max bits
+};
+
+// Lanes 4j..4j+3 decode job j's streams (j < nj <= 2).  Returns bit j set
+// when job j is corrupt.
+__device__ __forceinline__ uint32_t lit_decode(LitSmem &sm, const gc_u8 *in, const gc_u8 *s, g_u8 *lb,
+                                               const LJob &j0, const LJob &j1, int nj) {
     const int l = lane_id();
-    if (h.type == 0) {
-        for (int32_t k = l; k < h.regen; k += 64) lb[lpos + k] = s[bpos + h.hsz + k];
-        return 0;
-    }
-    if (h.type == 1) {
-        uint8_t v = (uint8_t)rd8(s, bpos + h.hsz);
-        for (int32_t k = l; k < h.regen; k += 64) lb[lpos + k] = v;
-        return 0;
-    }
-    int32_t p = bpos + h.hsz, n = h.csize;
-    if (h.type == 2) {
-        int32_t u = read_huf(sm, in, s, p, n);
-        if (u < 0) return E_CORRUPT;
-        if (u >= n) return E_CORRUPT;  // table must leave room for the streams
-        if (l == 0) sm.valid = 1;
-        p += u;
-        n -= u;
-    } else if (!sm.valid) {
-        return E_CORRUPT;
-    }
-    const int32_t maxbits = sm.maxbits;
-    // stream geometry (lane k < streams decodes stream k)
-    int32_t mysp = p, mysn = n, mycnt = h.regen;
+    const int jj = l >> 2, sl = l & 3;
+    const bool mine = jj < nj;
+    const int32_t p = jj ? j1.p : j0.p, n = jj ? j1.n : j0.n, regen = jj ? j1.regen : j0.regen;
+    const int32_t streams = jj ? j1.streams : j0.streams, hb = jj ? j1.hb : j0.hb;
+    const int32_t maxbits = jj ? j1.mb : j0.mb;
+    const int64_t lpos = jj ? j1.lpos : j0.lpos;
+    // stream geometry (lane sl < streams decodes stream sl)
+    int32_t mysp = p, mysn = n, mycnt = regen;
     int64_t o = lpos;
-    if (h.streams == 4) {
-        if (n < 10) return E_CORRUPT;
-        int32_t s1 = (int32_t)rd16(s, p), s2 = (int32_t)rd16(s, p + 2), s3 = (int32_t)rd16(s, p + 4);
-        int32_t s4 = n - 6 - s1 - s2 - s3;
-        if (s4 < 1) return E_CORRUPT;
-        int32_t seg = (h.regen + 3) / 4;
-        mysp = p + 6 + (l >= 1 ? s1 : 0) + (l >= 2 ? s2 : 0) + (l >= 3 ? s3 : 0);
-        mysn = l == 0 ? s1 : l == 1 ? s2 : l == 2 ? s3 : s4;
-        int32_t c4 = h.regen - 3 * seg;
-        mycnt = l < 3 ? seg : (c4 > 0 ? c4 : 0);
-        o = lpos + (int64_t)(l < 3 ? l : 3) * seg;
-    }
-    // lanes 0..3 decode one stream each
     int32_t bad = 0;
-    if (l < h.streams) {
+    if (mine && streams == 4) {
+        int32_t s4 = 0, s1 = 0, s2 = 0, s3 = 0;
+        if (n < 10) {
+            bad = 1;
+        } else {
+            s1 = (int32_t)rd16(s, p); s2 = (int32_t)rd16(s, p + 2); s3 = (int32_t)rd16(s, p + 4);
+            s4 = n - 6 - s1 - s2 - s3;
+            if (s4 < 1) bad = 1;
+        }
+        const int32_t seg = (regen + 3) / 4;
+        mysp = p + 6 + (sl >= 1 ? s1 : 0) + (sl >= 2 ? s2 : 0) + (sl >= 3 ? s3 : 0);
+        mysn = sl == 0 ? s1 : sl == 1 ? s2 : sl == 2 ? s3 : s4;
+        const int32_t c4 = regen - 3 * seg;
+        mycnt = sl < 3 ? seg : (c4 > 0 ? c4 : 0);
+        o = lpos + (int64_t)(sl < 3 ? sl : 3) * seg;
+    }
+    if (mine && sl < streams && !bad) {
         BR r;
         if (!br_init(r, in, s + mysp, mysn)) {
             bad = 1;
@@ -944,7 +954,7 @@ __device__ __forceinline__ int32_t lit_block(LitSmem &sm, const gc_u8 *in, const
             // one symbol: peek, table, consume (no refill: a refill leaves >= 32
             // bits in the container, two symbols take <= 24)
             auto sym = [&]() -> uint32_t {
-                const uint32_t e = sm.huf[br_peek(r, maxbits)];
+                const uint32_t e = sm.huf[hb + br_peek(r, maxbits)];
                 r.left -= (int32_t)(e >> 8);
                 return e & 0xFFu;
             };
@@ -961,7 +971,7 @@ __device__ __forceinline__ int32_t lit_block(LitSmem &sm, const gc_u8 *in, const
             const uint32_t pmask = (1u << maxbits) - 1u;
             auto fsym = [&]() -> uint32_t {
                 const int32_t lo = r.left - maxbits;
-                const uint32_t e = sm.huf[(uint32_t)(r.c >> (uint32_t)(lo - 8 * r.cb)) & pmask];
+                const uint32_t e = sm.huf[hb + ((uint32_t)(r.c >> (uint32_t)(lo - 8 * r.cb)) & pmask)];
                 r.left -= (int32_t)(e >> 8);
                 return e & 0xFFu;
             };
@@ -990,7 +1000,7 @@ __device__ __forceinline__ int32_t lit_block(LitSmem &sm, const gc_u8 *in, const
 #else
             for (; o < end; o++) {
                 uint32_t v = br_peek(r, maxbits);
-                uint32_t e = sm.huf[v];
+                uint32_t e = sm.huf[hb + v];
                 acc |= (e & 0xFF) << (8 * (o & 3));
                 br_skip(r, (int)(e >> 8));
                 if (((o + 1) & 3) == 0) { put_word(lb, start, o + 1, acc); acc = 0; }
@@ -1002,8 +1012,83 @@ __device__ __forceinline__ int32_t lit_block(LitSmem &sm, const gc_u8 *in, const
             if (!br_done(r)) bad = 1;
         }
     }
-    bad = (int32_t)dwave_max((uint32_t)bad);
-    return bad ? E_CORRUPT : 0;
+    const uint64_t bm = __ballot(bad != 0);
+    return ((bm & 0xFull) ? 1u : 0u) | ((bm & 0xF0ull) ? 2u : 0u);
+}
+
+__device__ __forceinline__ int32_t lit_block(LitSmem &sm, const gc_u8 *in, const gc_u8 *s, const LitHdr &h, int32_t bpos,
+                             g_u8 *lb, int64_t lpos) {
+    const int l = lane_id();
+    if (h.type == 0) {
+        for (int32_t k = l; k < h.regen; k += 64) lb[lpos + k] = s[bpos + h.hsz + k];
+        return 0;
+    }
+    if (h.type == 1) {
+        uint8_t v = (uint8_t)rd8(s, bpos + h.hsz);
+        for (int32_t k = l; k < h.regen; k += 64) lb[lpos + k] = v;
+        return 0;
+    }
+    int32_t p = bpos + h.hsz, n = h.csize;
+    LJob j;
+    if (h.type == 2) {
+        int32_t m = 0;
+        int32_t u = read_huf(sm, in, s, p, n, 0, false, &m);
+        if (u < 0) return E_CORRUPT;
+        if (u >= n) return E_CORRUPT;  // table must leave room for the streams
+        lit_set_cur(sm, m == 12 ? 2 : 0, m);
+        p += u;
+        n -= u;
+        j.hb = 0;
+        j.mb = m;
+    } else {
+        const int32_t c = sm.cur;
+        if (c < 0) return E_CORRUPT;
+        j.hb = c == 1 ? 2048 : 0;
+        j.mb = sm.smb[c];
+    }
+    j.p = p; j.n = n; j.regen = h.regen; j.streams = h.streams; j.lpos = lpos;
+    return lit_decode(sm, in, s, lb, j, j, 1) ? E_CORRUPT : 0;
+}
+
+// Two Huffman literal sections decoded together (lanes 0-3 and 4-7), their
+// tables in the two halves of sm.huf.  Returns 0 (both decoded), 1 / 2 (the
+// first / second is corrupt; the first error in block order) or -2: nothing
+// decoded and the current table untouched unless the first block brings its
+// own -- the caller decodes the two one by one (12-bit tables, errors in a
+// table description, a treeless first block without a narrow table).
+struct LPend {
+    LitHdr h;
+    int32_t bpos;
+    uint32_t ord;
+    int64_t lpos;
+};
+__device__ __forceinline__ int lit_pair(LitSmem &sm, const gc_u8 *s, g_u8 *lb, const LPend &A, const LPend &B) {
+    LJob ja, jb;
+    int32_t pa = A.bpos + A.h.hsz, na = A.h.csize, pb = B.bpos + B.h.hsz, nb = B.h.csize;
+    int sa, sb;
+    if (A.h.type == 2) {
+        int32_t m = 0;
+        const int32_t u = read_huf(sm, s, s, pa, na, 0, true, &m);
+        if (u < 0 || u >= na) return -2;
+        pa += u; na -= u; sa = 0; ja.mb = m;
+    } else {
+        const int32_t c = sm.cur;
+        if (c < 0 || c == 2) return -2;
+        sa = c; ja.mb = sm.smb[c];
+    }
+    if (B.h.type == 2) {
+        int32_t m = 0;
+        const int32_t u = read_huf(sm, s, s, pb, nb, sa ^ 1, true, &m);
+        if (u < 0 || u >= nb) return -2;
+        pb += u; nb -= u; sb = sa ^ 1; jb.mb = m;
+    } else {
+        sb = sa; jb.mb = ja.mb;
+    }
+    lit_set_cur(sm, sb, jb.mb);
+    ja.p = pa; ja.n = na; ja.regen = A.h.regen; ja.streams = A.h.streams; ja.lpos = A.lpos; ja.hb = 2048 * sa;
+    jb.p = pb; jb.n = nb; jb.regen = B.h.regen; jb.streams = B.h.streams; jb.lpos = B.lpos; jb.hb = 2048 * sb;
+    const uint32_t bm = lit_decode(sm, s, s, lb, ja, jb, 2);
+    return (bm & 1u) ? 1 : (bm & 2u) ? 2 : 0;
 }
 
 // one item into the wave's 64-entry store buffer
@@ -1029,6 +1114,9 @@ __device__ __forceinline__ void item_put(ItemBuf &b, g_u4 *items, uint32_t x, ui
 }
 
 // sequence table for one field; returns bytes used or -1
+#ifndef JFS_ZLIT_PAIR
+#define JFS_ZLIT_PAIR 1  // Huffman literal sections of consecutive blocks decoded two at a time (8 lanes)
+#endif
 __device__ __forceinline__ void lit_wave(LitSmem &sm, const jfs_dev_block &b, ZInfo &zi, g_u8 *litbuf) {
     const int l = lane_id();
     const gc_u8 *s = (const gc_u8 *)b.src;
@@ -1038,15 +1126,30 @@ __device__ __forceinline__ void lit_wave(LitSmem &sm, const jfs_dev_block &b, ZI
     const int64_t lend = (int64_t)zi.lit_off + zi.lit_bytes;
     uint32_t err_blk = 0xFFFFFFFFu;
     int32_t err_code = 0;
-    if (l == 0) sm.valid = 0;
+    if (l == 0) sm.cur = -1;
     __builtin_amdgcn_wave_barrier();
+    // a Huffman section waiting for a partner (decoded before anything that
+    // could report an error after it)
+    LPend pd;
+    bool hp = false;
+    auto single = [&](const LPend &q) -> bool {
+        const int32_t e = lit_block(sm, s, s, q.h, q.bpos, litbuf, q.lpos);
+        if (e) { err_blk = q.ord; err_code = e; return false; }
+        return true;
+    };
+    auto flush = [&]() -> bool {
+        if (!hp) return true;
+        hp = false;
+        return single(pd);
+    };
     for (;;) {
         int32_t err = 0;
         uint32_t fl = 0, chk = 0;
         int ev = walk_next(w, &err, &fl, &chk);
         if (ev == EV_DONE || ev == EV_ERROR) break;
         if (ev == EV_FSTART) {
-            if (l == 0) sm.valid = 0;
+            if (!flush()) break;
+            if (l == 0) sm.cur = -1;
             __builtin_amdgcn_wave_barrier();
             continue;
         }
@@ -1058,7 +1161,10 @@ __device__ __forceinline__ void lit_wave(LitSmem &sm, const jfs_dev_block &b, ZI
         if (w.btype != 2) {
             int64_t room = (int64_t)w.cap - w.lb;
             if ((int64_t)w.bsize <= room) {
-                if (lpos + w.bsize > lend) { err_blk = ord; err_code = -104; break; }
+                if (lpos + w.bsize > lend) {
+                    if (flush()) { err_blk = ord; err_code = -104; }
+                    break;
+                }
                 if (w.btype == 0) {
                     for (int32_t k = l; k < w.bsize; k += 64) litbuf[lpos + k] = s[w.bpos + k];
                 } else {
@@ -1072,15 +1178,40 @@ __device__ __forceinline__ void lit_wave(LitSmem &sm, const jfs_dev_block &b, ZI
         }
         LitHdr h;
         int32_t e = lit_header(s, w.bpos, w.bsize, h);
-        if (e) { err_blk = ord; err_code = e; break; }
-        if (lpos + h.regen + 4 > lend) { err_blk = ord; err_code = -104; break; }
-        e = lit_block(sm, s, s, h, w.bpos, litbuf, lpos);
-        if (e) { err_blk = ord; err_code = e; break; }
+        if (e) {
+            if (flush()) { err_blk = ord; err_code = e; }
+            break;
+        }
+        if (lpos + h.regen + 4 > lend) {
+            if (flush()) { err_blk = ord; err_code = -104; }
+            break;
+        }
+        LPend q;
+        q.h = h; q.bpos = w.bpos; q.ord = ord; q.lpos = lpos;
+        if (h.type >= 2 && JFS_ZLIT_PAIR) {
+            if (hp) {
+                hp = false;
+                const int r = lit_pair(sm, s, litbuf, pd, q);
+                if (r == -2) {
+                    if (!single(pd) || !single(q)) break;
+                } else if (r) {
+                    err_blk = r == 1 ? pd.ord : ord;
+                    err_code = E_CORRUPT;
+                    break;
+                }
+            } else {
+                pd = q;
+                hp = true;
+            }
+        } else if (!single(q)) {  // raw / RLE literals: no table, no error; never waits
+            break;
+        }
         lpos += h.regen;
         int32_t nseq = 0, used = 0;
         if (nbseq_header(s, w.bpos + h.sec, w.bpos + w.bsize, &nseq, &used)) break;  // reported by the seq wave
         w.lb += (int64_t)h.regen + 3 * (int64_t)nseq;
     }
+    flush();
     if (l == 0) {
         zi.lit_err_blk = err_blk;
         zi.lit_err_code = err_code;
