@@ -205,3 +205,60 @@ print("OK")
     env = dict(os.environ, JFS_HOST_CHUNK_MB="24")
     r = subprocess.run([sys.executable, "-c", child, root], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "OK" in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])
+
+
+def _block_spans(fr):
+    """(block start, block type, literal section type, literal section end)
+    for each block of a single-segment-or-windowed frame."""
+    p = 4
+    fhd = fr[p]; p += 1
+    ss, did, fcs = (fhd >> 5) & 1, fhd & 3, fhd >> 6
+    p += (0 if ss else 1) + [0, 1, 2, 4][did] + [1 if ss else 0, 2, 4, 8][fcs]
+    out, last = [], 0
+    while not last:
+        h = int.from_bytes(fr[p:p + 3], "little"); p += 3
+        last, bt, bs = h & 1, (h >> 1) & 3, h >> 3
+        q = p
+        p += bs if bt != 1 else 1
+        if bt != 2:
+            out.append((q, bt, -1, q))
+            continue
+        b0 = fr[q]; lt, sf = b0 & 3, (b0 >> 2) & 3
+        if lt >= 2:
+            hs = 3 if sf <= 1 else 4 if sf == 2 else 5
+            v = int.from_bytes(fr[q:q + hs], "little")
+            cs = (v >> 14) & 0x3FF if hs == 3 else (v >> 18) if hs == 4 else (v >> 22)
+            out.append((q, bt, lt, q + hs + cs))
+        else:
+            out.append((q, bt, lt, q))
+    return out
+
+
+def test_zstd_literal_pairs_corrupt_vs_oracle(gpu, golden, frames_bin, oracle):
+    """Literal sections decoded two blocks at a time (JFS_ZLIT_PAIR): a damaged
+    Huffman table description or stream in either block of a pair (and in a
+    treeless block) gives the oracle's result, through the one-wave path."""
+    f = [e for e in golden["zstd"]["frames"] if e["size"] == 4 << 20 and e["level"] == 3][0]
+    fr = frames_bin[f["off"]:f["off"] + f["csize"]]
+    spans = _block_spans(fr)
+    huf = [s for s in spans if s[2] == 2]
+    tl = [s for s in spans if s[2] == 3]
+    assert len(huf) >= 4
+    variants = []
+    for q, _, lt, lend in huf[:4] + tl[:2]:
+        hs = 3 if ((fr[q] >> 2) & 3) <= 1 else 4 if ((fr[q] >> 2) & 3) == 2 else 5
+        for pos, x in ((q + hs + 1, 0x5A), ((q + lend) // 2, 0xFF), (lend - 2, 0x11)):
+            b = bytearray(fr)
+            b[pos] ^= x
+            variants.append(bytes(b))
+    k = 129 // len(variants) + 1
+    srcs = variants * k
+    caps = [f["size"]] * len(srcs)
+    r, outs = run_device(srcs, caps, gpu)
+    assert len(r) > 128
+    want = [oracle.zstd_decompress(v, f["size"]) for v in variants]
+    for i, (x, o) in enumerate(zip(r, outs)):
+        wr, wo = want[i % len(variants)]
+        assert x == wr, (i % len(variants), wr, x)
+        if x >= 0:
+            assert o == wo
