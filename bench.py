@@ -412,12 +412,52 @@ def oneshot_concurrency(comp_blocks, raw_blocks, U, n_dec=200, n_enc=20, rounds=
     del wpairs
     warm = [run(n_dec, rounds, dec, dchk)["device_batches"] for _ in range(2)]
     warm += [run(n_enc, rounds, enc, echk)["device_batches"]]
+    def native(n, k, fname, srcs, dsts, cap, check):
+        """run() with n pthreads of juicefs_amd/lib/libjfscallers.so calling
+        jfs_<fname> k times each (no interpreter lock between calls, like
+        goroutines); same sources, destinations and checks as run()."""
+        import ctypes
+        cl = ctypes.CDLL(os.path.join(ROOT, "juicefs_amd", "lib", "libjfscallers.so"))
+        cl.jfs_native_callers.restype = ctypes.c_double
+        fn = ctypes.cast(getattr(L.load(), fname), ctypes.c_void_p)
+        ns = len(srcs)
+        sp = (ctypes.c_void_p * ns)(*[ctypes.cast(ctypes.c_char_p(b), ctypes.c_void_p).value for b in srcs])
+        ln = (ctypes.c_int64 * ns)(*[len(b) for b in srcs])
+        dbuf = [(ctypes.c_char * len(dsts[(t, r)])).from_buffer(dsts[(t, r)]) for t in range(n) for r in range(k)]
+        dp = (ctypes.c_void_p * (n * k))(*[ctypes.addressof(x) for x in dbuf])
+        lat, ret = (ctypes.c_double * (n * k))(), (ctypes.c_int64 * (n * k))()
+        b0 = batches()
+        wall = cl.jfs_native_callers(fn, ctypes.c_int(c.algo), n, k, sp, ln, ns, dp, ctypes.c_int64(cap), lat, ret)
+        b1 = batches()
+        del dbuf, dp
+        assert wall > 0, "native callers failed to start"
+        errs = sum(1 for t in range(n) for r in range(k) if not check(t, r, int(ret[t * k + r])))
+        flat = list(lat)
+        return {"calls": n * k, "p50_ms": pct(flat, 0.5), "p99_ms": pct(flat, 0.99),
+                "value": n * k * U / wall / 2**30, "unit": "GiB/s", "errors": errs, "device_batches": b1 - b0}
+
+    def native_bursts(n, k, fname, srcs, dsts, cap, check, nb=5):
+        rs = [native(n, k, fname, srcs, dsts, cap, check) for _ in range(nb)]
+        med = lambda key: sorted(r[key] for r in rs)[len(rs) // 2]
+        return {"calls": n * k, "bursts": len(rs), "value": med("value"), "p50_ms": med("p50_ms"),
+                "p99_ms": med("p99_ms"), "unit": "GiB/s", "errors": sum(r["errors"] for r in rs),
+                "device_batches": [r["device_batches"] for r in rs],
+                "per_burst": [{"value": round(r["value"], 3), "p50_ms": round(r["p50_ms"], 2),
+                               "p99_ms": round(r["p99_ms"], 2)} for r in rs]}
+
     out = {"decompress_lone": run(1, 5, dec, dchk), "compress_lone": run(1, 3, enc, echk),
            f"decompress_{n_dec}_concurrent": bursts(n_dec, rounds, dec, dchk),
            f"compress_{n_enc}_concurrent": bursts(n_enc, rounds, enc, echk),
            "warmup_device_batches": warm,
            "path": "LZ4 one-call API (jfs_compress / jfs_decompress) from concurrent host threads, host buffers, "
                    "1 GPU; value = uncompressed GiB/s over the wall time of all calls"}
+    # the same calls from native threads (libjfscallers.so): the library without the interpreter lock
+    out[f"decompress_{n_dec}_concurrent_native"] = native_bursts(n_dec, rounds, "jfs_decompress", comp_blocks, ddst,
+                                                                 U, dchk)
+    out[f"compress_{n_enc}_concurrent_native"] = native_bursts(n_enc, rounds, "jfs_compress", raw_blocks, edst,
+                                                               bound, echk)
+    out["native_path"] = ("*_native: n pthreads (juicefs_amd/callers/callers.c) call jfs_decompress / jfs_compress "
+                          "k times each after one barrier, like pkg/chunk's goroutines; same buffers and checks")
     # the same calls with --compress zstd (ZStandard.Compress / Decompress)
     z = C.ZStandard()
     zb = z.CompressBound(U)
