@@ -774,7 +774,7 @@ __global__ __launch_bounds__(PLAN_T) void zplan_kernel(ZInfo *__restrict__ info,
 #define JFS_ZLIT_QUAD 1  // Huffman streams: four symbols per step (two per refill, one aligned word store)
 #endif
 struct LitSmem {
-    uint16_t huf[4096];  // sym | nb << 8
+    alignas(16) uint16_t huf[4096];  // sym | nb << 8
     uint8_t stage[256];
     uint8_t w[260];
     int16_t norm[256];
@@ -797,6 +797,9 @@ __device__ __forceinline__ void stage_bytes(uint8_t *dst, const gc_u8 *s, int32_
     __builtin_amdgcn_wave_barrier();
 }
 
+#ifndef JFS_HUF_PAR
+#define JFS_HUF_PAR 1  // Huffman table fill: lanes over symbols and cells (markers + prefix max), no per-symbol loop
+#endif
 // Huffman table description -> sm.huf at cell 2048 * slot (a 12-bit table:
 // cell 0, all 4096 cells).  Returns bytes used, -1 (corrupt) or -2 (a 12-bit
 // table with narrow_only: nothing written to the table cells).
@@ -868,6 +871,63 @@ __device__ __forceinline__ int32_t read_huf(LitSmem &sm, const gc_u8 *in, const 
     if (maxbits == 12 && narrow_only) return -2;
     const uint32_t hbase = maxbits == 12 ? 0u : 2048u * (uint32_t)slot;
     __builtin_amdgcn_wave_barrier();
+#if JFS_HUF_PAR
+    // every symbol's ordinal in (weight, symbol) order and its first cell:
+    // lanes over symbols (four rounds), one ballot per weight and round
+    uint32_t wv[4], ordv[4], posv[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int i = l + 64 * r;
+        wv[r] = i < nw ? (uint32_t)sm.w[i] : 0u;
+        ordv[r] = posv[r] = 0;
+    }
+    uint32_t run = 0, done = 0;  // first cell / first ordinal of weight k's symbols
+#pragma unroll
+    for (uint32_t k = 1; k <= 12; k++) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const uint64_t m = __builtin_amdgcn_ballot_w64(wv[r] == k);
+            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            if (wv[r] == k) {
+                ordv[r] = done + c + below;
+                posv[r] = run + ((c + below) << (k - 1));
+            }
+            c += (uint32_t)__builtin_popcountll(m);
+        }
+        run += c << (k - 1);
+        done += c;
+    }
+    // markers: a symbol's first cell holds its ordinal + 1, the others 0;
+    // symnext[ordinal] = the symbol's entry
+    const uint32_t size = 1u << maxbits;
+    uint16_t *ht = sm.huf + hbase;
+    for (uint32_t u = 8u * (uint32_t)l; u < size; u += 512u) *(uint4 *)(ht + u) = make_uint4(0, 0, 0, 0);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        if (wv[r]) {
+            ht[posv[r]] = (uint16_t)(ordv[r] + 1u);
+            sm.symnext[ordv[r]] = (uint16_t)((uint32_t)(l + 64 * r) | ((uint32_t)(maxbits + 1) - wv[r]) << 8);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    // every cell: the entry of the last marker at or below it (prefix max,
+    // lanes over consecutive pieces)
+    const uint32_t per = size >= 64u ? size >> 6 : 1u, q0 = (uint32_t)l * per;
+    uint32_t lm = 0;
+    for (uint32_t i = 0; i < per; i++)
+        if (q0 + i < size) lm = umax32(lm, ht[q0 + i]);
+    uint32_t carry = dpp_shift_up(dpp_scan_max(lm), 0u);
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t i = 0; i < per; i++) {
+        if (q0 + i < size) {
+            carry = umax32(carry, ht[q0 + i]);
+            ht[q0 + i] = sm.symnext[carry - 1u];
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+#else
     // rank starts (weight ascending, then symbol order)
     uint32_t cnt = 0;
     for (int i = 0; i < nw; i++) cnt += (sm.w[i] == (uint32_t)l) ? 1u : 0u;  // lane k counts weight k
@@ -888,6 +948,7 @@ __device__ __forceinline__ int32_t read_huf(LitSmem &sm, const gc_u8 *in, const 
         if (l == 0) sm.rank[wi] = st + len;
         __builtin_amdgcn_wave_barrier();
     }
+#endif
     *maxbits_out = maxbits;
     __builtin_amdgcn_wave_barrier();
     return used;
