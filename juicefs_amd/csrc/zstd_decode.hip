@@ -797,6 +797,9 @@ __device__ __forceinline__ void stage_bytes(uint8_t *dst, const gc_u8 *s, int32_
     __builtin_amdgcn_wave_barrier();
 }
 
+#ifndef JFS_HUF_REGW
+#define JFS_HUF_REGW 1  // Huffman weights: FSE stream and table in registers (readlane), no memory round trip per weight
+#endif
 #ifndef JFS_HUF_PAR
 #define JFS_HUF_PAR 1  // Huffman table fill: lanes over symbols and cells (markers + prefix max), no per-symbol loop
 #endif
@@ -817,6 +820,47 @@ __device__ __forceinline__ int32_t read_huf(LitSmem &sm, const gc_u8 *in, const 
         if (c < 0 || c > hb) return -1;
         if (build_fse(sm.fse, sm.norm, maxsym, al, sm.symnext, sm.symat)) return -1;
         __builtin_amdgcn_wave_barrier();
+#if JFS_HUF_REGW
+        // the weight stream (<= 127 bytes, staged) as dword q in lane q and the
+        // weight FSE table (<= 64 cells) as cell i in lane i: the serial
+        // decode reads both with readlane, no memory round trip per weight
+        const int32_t len = hb - c;
+        if (len <= 0) return -1;
+        const uint32_t last = sm.stage[hb - 1];
+        if (last == 0) return -1;
+        uint32_t dv = 0;
+        for (int k = 0; k < 4; k++) {
+            const int32_t i = c + 4 * l + k;
+            if (4 * l + k < len) dv |= (uint32_t)sm.stage[i] << (8 * k);
+        }
+        const uint32_t fv = l < (1 << al) ? sm.fse[l] : 0u;
+        int32_t left = 8 * (len - 1) + (31 - __builtin_clz(last));
+        auto bread = [&](uint32_t nb) -> uint32_t {  // bits [left - nb, left), 0 below the stream start
+            const int32_t lo = left - (int32_t)nb;
+            left = lo;
+            if (nb == 0) return 0u;
+            const int32_t q = lo >> 5;
+            const uint32_t d0 = q >= 0 ? readlane(dv, q) : 0u;
+            const uint32_t d1 = q + 1 < 32 ? readlane(dv, q + 1) : 0u;
+            const uint64_t w64 = ((uint64_t)d1 << 32) | d0;
+            return (uint32_t)(w64 >> (uint32_t)(lo - 32 * q)) & ((1u << nb) - 1u);
+        };
+        uint32_t s1 = bread((uint32_t)al), s2 = bread((uint32_t)al);
+        for (;;) {
+            if (nw > 253) return -1;
+            const uint32_t e1 = readlane(fv, (int)s1);
+            if (l == 0) sm.w[nw] = (uint8_t)(e1 & 0xFF);
+            nw++;
+            s1 = (e1 >> 16) + bread((e1 >> 8) & 0xFF);
+            if (left < 0) { if (l == 0) sm.w[nw] = (uint8_t)(readlane(fv, (int)s2) & 0xFF); nw++; break; }
+            if (nw > 253) return -1;
+            const uint32_t e2 = readlane(fv, (int)s2);
+            if (l == 0) sm.w[nw] = (uint8_t)(e2 & 0xFF);
+            nw++;
+            s2 = (e2 >> 16) + bread((e2 >> 8) & 0xFF);
+            if (left < 0) { if (l == 0) sm.w[nw] = (uint8_t)(readlane(fv, (int)s1) & 0xFF); nw++; break; }
+        }
+#else
         BR r;
         if (!br_init(r, in, s + p + 1 + c, hb - c)) return -1;
         uint32_t s1 = br_read(r, al), s2 = br_read(r, al);
@@ -834,6 +878,7 @@ __device__ __forceinline__ int32_t read_huf(LitSmem &sm, const gc_u8 *in, const 
             s2 = (e2 >> 16) + br_read(r, (e2 >> 8) & 0xFF);
             if (br_overflow(r)) { if (l == 0) sm.w[nw] = (uint8_t)(sm.fse[s1] & 0xFF); nw++; break; }
         }
+#endif
         used = 1 + hb;
     } else {
         nw = hb - 127;
