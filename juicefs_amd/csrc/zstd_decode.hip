@@ -797,6 +797,12 @@ __device__ __forceinline__ void stage_bytes(uint8_t *dst, const gc_u8 *s, int32_
     __builtin_amdgcn_wave_barrier();
 }
 
+template <class P>
+__device__ __forceinline__ void build_seq_fse_g(P t, const int16_t *norm, int32_t maxsym, int32_t al,
+                                                uint8_t *mark, uint8_t *ksym, uint8_t *symat);
+#ifndef JFS_HUF_FSEPAR
+#define JFS_HUF_FSEPAR 1  // Huffman weights' FSE table by the lane-parallel builder
+#endif
 #ifndef JFS_HUF_REGW
 #define JFS_HUF_REGW 1  // Huffman weights: FSE stream and table in registers (readlane), no memory round trip per weight
 #endif
@@ -818,8 +824,21 @@ __device__ __forceinline__ int32_t read_huf(LitSmem &sm, const gc_u8 *in, const 
         int32_t maxsym = 255, al = 0;
         int32_t c = read_ncount(sm.stage, hb, sm.norm, &maxsym, &al, 6);
         if (c < 0 || c > hb) return -1;
+#if JFS_HUF_FSEPAR
+        // the weight table by the lane-parallel sequence-table builder (u16
+        // cells sym | state << 6 into symnext; sm.w is free until the weights
+        // are decoded), then expanded to sym | nb << 8 | base << 16
+        build_seq_fse_g(sm.symnext, sm.norm, maxsym, al, sm.w, sm.w + 128, sm.symat);
+        if (l < (1 << al)) {
+            const uint32_t v = sm.symnext[l], ns = v >> 6;
+            const int nb = al - (31 - __builtin_clz(ns));
+            sm.fse[l] = (v & 63u) | ((uint32_t)nb << 8) | (((ns << nb) - (1u << al)) << 16);
+        }
+        __builtin_amdgcn_wave_barrier();
+#else
         if (build_fse(sm.fse, sm.norm, maxsym, al, sm.symnext, sm.symat)) return -1;
         __builtin_amdgcn_wave_barrier();
+#endif
 #if JFS_HUF_REGW
         // the weight stream (<= 127 bytes, staged) as dword q in lane q and the
         // weight FSE table (<= 64 cells) as cell i in lane i: the serial
