@@ -2075,69 +2075,10 @@ static bool current_device_ok() {
     return false;
 }
 
-// Chain-bitmap decode (round 6, lz4_decode.hip): the token
-// chains found by a separate grid first.  Off by default (measured slower:
-// the copier wave, not the parser, bounds the decode); JFS_LZ4_CHAIN=1 on.
-// (read per call: tests switch it within one process)
-static bool lz4_chain_on() {
-    const char *e = getenv("JFS_LZ4_CHAIN");
-    return e && atoi(e) != 0;
-}
-
-// Per-device chain-bitmap scratch of the device entry point.  The descriptors
-// are in HBM, so the host does not know the batch's spans: the scratch is
-// sized from the spans the previous call reported (mapped host memory the plan
-// kernel writes) or, first, from 512 spans (4 MiB compressed) per block;
-// blocks beyond the capacity are parsed in-kernel, never wrong.
-struct ChainScratch {
-    std::mutex mu;
-    uint8_t *p = nullptr;
-    int64_t bytes = 0;
-    int64_t cap_spans = 0;
-    int nblk_cap = 0;
-    int32_t *need_h = nullptr;  // mapped: spans the last plan needed
-    int32_t *need_d = nullptr;
-    hipEvent_t ev_done = nullptr;
-};
-ChainScratch g_chain[64];
-
 int64_t jfs_lz4_decompress_device(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *stream) {
     if (!current_device_ok()) return JFS_ERR_NO_DEVICE;
     stat_launch(JFS_ALGO_LZ4, DECOMPRESS, nblk);
-    hipStream_t st = (hipStream_t)stream;
-    int dev = 0;
-    if (!lz4_chain_on() || nblk <= 0 || hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64)
-        return jfs_launch_lz4_decode(d_blocks, nblk, d_ret, st) == 0 ? JFS_OK : JFS_ERR_HIP;
-    ChainScratch &z = g_chain[dev];
-    std::lock_guard<std::mutex> lk(z.mu);
-    if (!z.ev_done && hipEventCreateWithFlags(&z.ev_done, hipEventDisableTiming) != hipSuccess) return JFS_ERR_HIP;
-    if (!z.need_h) {
-        if (hipHostMalloc((void **)&z.need_h, 64, hipHostMallocMapped) != hipSuccess) return JFS_ERR_NO_MEMORY;
-        *(volatile int32_t *)z.need_h = 0;
-        if (hipHostGetDevicePointer((void **)&z.need_d, z.need_h, 0) != hipSuccess) return JFS_ERR_HIP;
-    }
-    const int64_t hint = *(volatile int32_t *)z.need_h;
-    int64_t want_spans = std::max<int64_t>(hint, std::min<int64_t>((int64_t)nblk * 512, 4ll << 20));
-    if (want_spans > z.cap_spans || nblk > z.nblk_cap) {
-        const int nb = std::max(nblk, z.nblk_cap);
-        const int64_t cs = std::max(want_spans, z.cap_spans);
-        const int64_t need = jfs_lz4_chain_scratch_bytes(nb, cs);
-        if (hipEventSynchronize(z.ev_done) != hipSuccess) return JFS_ERR_HIP;  // earlier launches may still use it
-        if (z.p) (void)hipFree(z.p);
-        z.p = nullptr;
-        z.bytes = z.cap_spans = 0;
-        z.nblk_cap = 0;
-        if (hipMalloc((void **)&z.p, (size_t)need) != hipSuccess) {
-            (void)hipGetLastError();
-            return jfs_launch_lz4_decode(d_blocks, nblk, d_ret, st) == 0 ? JFS_OK : JFS_ERR_HIP;
-        }
-        z.bytes = need;
-        z.cap_spans = cs;
-        z.nblk_cap = nb;
-    }
-    if (hipStreamWaitEvent(st, z.ev_done, 0) != hipSuccess) return JFS_ERR_HIP;
-    if (jfs_launch_lz4_decode_chain(d_blocks, nblk, d_ret, z.p, z.cap_spans, z.need_d, st) != 0) return JFS_ERR_HIP;
-    return hipEventRecord(z.ev_done, st) == hipSuccess ? JFS_OK : JFS_ERR_HIP;
+    return jfs_launch_lz4_decode(d_blocks, nblk, d_ret, (hipStream_t)stream) == 0 ? JFS_OK : JFS_ERR_HIP;
 }
 
 // Small-batch device decode: per-device scratch shared by every caller,

@@ -61,13 +61,6 @@ int jfs_launch_lz4_decode_lens(const jfs_dev_block *d_blocks, int nblk, int32_t 
                                hipStream_t stream);
 int jfs_launch_lz4_decode_todo(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, const int32_t *d_todo,
                                hipStream_t stream);
-// LZ4 decode with the chain bitmap (lz4_decode.hip): scratch of
-// jfs_lz4_chain_scratch_bytes(nblk, cap_spans); spans = 8 KiB of compressed
-// input (jfs_lz4_chain_spans counts them from host lengths)
-int64_t jfs_lz4_chain_scratch_bytes(int nblk, int64_t cap_spans);
-int64_t jfs_lz4_chain_spans(int nblk, const int32_t *src_len);
-int jfs_launch_lz4_decode_chain(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *scratch,
-                                int64_t cap_spans, int32_t *need_host, hipStream_t stream);
 // small-batch LZ4 decode (lz4_split.hip): compressed bytes per segment (one
 // lane each), scratch bytes for these blocks, and
 // the launch (nseg_all = sum of ceil(src_len / 256), max_cap = largest dst_cap,

@@ -897,21 +897,13 @@ __device__ __forceinline__ void batch(Smem &s, Ctx &c, bool act, int32_t o, uint
 // starting at output op0.  Returns the number of tokens copied; fewer than T
 // when an output-side fast-loop check declines a token (*bad_ip = its input
 // position).  *end_op = output position after the copied tokens.
-// The table is trusted only as far as it is one chain: token i must start
-// where token i-1 ends (the first one at ip0) and must not be a stop token
-// (both always hold for tables the parser walked itself; a chain-bitmap table
-// is checked the same way), so a broken link ends the window like an
-// output-side check and the serial path resumes at the true position
-// (*bad_ip).  *last_nxt = where the last copied token ends.
-__device__ __forceinline__ uint32_t copy_tokens(Smem &s, Ctx &c, uint32_t T, int32_t op0, int32_t ip0,
-                                                int32_t *end_op, int32_t *bad_ip, int32_t *last_nxt PROF_ARG) {
+__device__ __forceinline__ uint32_t copy_tokens(Smem &s, Ctx &c, uint32_t T, int32_t op0, int32_t *end_op,
+                                                int32_t *bad_ip PROF_ARG) {
     const int l = lane_id();
     int32_t op = op0;
-    int32_t carry = ip0;  // end of the token before the group
     const int32_t cap = c.cap;
 #ifdef JFS_LZ4_PARSEONLY  // diagnostics: the parser wave alone (the copier skips every window; wrong output)
     *end_op = op0;
-    *last_nxt = ip0;
     return T;
 #endif
     for (uint32_t g0 = 0; g0 < T; g0 += 64) {
@@ -920,8 +912,6 @@ __device__ __forceinline__ uint32_t copy_tokens(Smem &s, Ctx &c, uint32_t T, int
         const int32_t p = c.cbase + (in0 ? (int32_t)c.tab[g0 + l] : 0);
         FTok t = parse_fast(s, c, p);
         const bool sl = in0 && t.slow;
-        bool stp = t.stop;
-        int32_t nx = t.nxt;
         if (__ballot(sl)) {
             if (sl) {
                 const Tok u = parse_tok(s, c, p);
@@ -930,19 +920,15 @@ __device__ __forceinline__ uint32_t copy_tokens(Smem &s, Ctx &c, uint32_t T, int
                 t.ml = (uint32_t)u.ml;
                 t.off = (uint32_t)u.off;
                 t.llx = (uint32_t)u.llx;
-                nx = u.nxt;
-                stp = ((uint32_t)u.nxt & STOP) != 0;
             }
         }
-        const int32_t prev = (int32_t)dpp_shift_up((uint32_t)nx, (uint32_t)carry);
         const uint32_t ll = in0 ? t.ll : 0u, ml = in0 ? t.ml : 0u, off = t.off;
         const uint32_t litr = (uint32_t)(t.lit - c.cbase);
         const uint32_t len = ll + ml;
         const uint32_t incl = dpp_scan_add(len);
         const int32_t o = op + (int32_t)(incl - len);
         const int32_t om = o + (int32_t)ll;
-        const bool bad = in0 && (stp || p != prev || (t.llx && om > cap - 32) || (om + (int32_t)ml >= cap - 64) ||
-                                 ((int32_t)off > om));
+        const bool bad = in0 && ((t.llx && om > cap - 32) || (om + (int32_t)ml >= cap - 64) || ((int32_t)off > om));
         const uint64_t bm = __ballot(bad);
         const uint32_t n = bm ? (uint32_t)__builtin_ctzll(bm) : n0;
         const bool in = (uint32_t)l < n;
@@ -974,16 +960,13 @@ __device__ __forceinline__ uint32_t copy_tokens(Smem &s, Ctx &c, uint32_t T, int
             j = eb;
         }
         if (bm) {
-            *bad_ip = (int32_t)readlane((uint32_t)prev, (int)n);
+            *bad_ip = (int32_t)readlane((uint32_t)p, (int)n);
             *end_op = (int32_t)readlane((uint32_t)o, (int)n);
-            *last_nxt = *bad_ip;
             return g0 + n;
         }
         op += (int32_t)readlane(incl, 63);
-        carry = (int32_t)readlane((uint32_t)nx, (int)n0 - 1);
     }
     *end_op = op;
-    *last_nxt = carry;
     return T;
 }
 
@@ -1454,238 +1437,6 @@ struct SegWalk {
     }
 };
 
-// ---------------------------------------------------------------------------
-// Chain bitmap (round 6): the token chains of all blocks found by a separate
-// grid before the decode kernel runs, one wave per 8 KiB span of compressed
-// input, every span of every block at once.  The span's bytes are staged in
-// LDS (a walk step is two dependent LDS reads instead of two HBM/L2 round
-// trips), each lane walks its 128-byte segment speculatively from a pre-roll
-// before it, and fix-up rounds (DPP shift of the exits) make the span one
-// chain.  Lane 0 enters the span speculatively too (CPRE0 bytes before it;
-// exactly at 0 for a block's first span), so a span's bits are the true chain
-// from the first position where the true chain meets them: the decode
-// kernel's parser wave checks that the window start is a set bit and
-// otherwise walks that span itself (the segment walk above).  Output per span
-// g (global span index, spans of a block consecutive):
-//   bits[256 g + 4 l .. +4]  the 128 chain-position bits of lane l's segment,
-//   exits[g]                 the first chain position >= span end, STOP | p
-//                            when the chain stops (end-of-input rules or a
-//                            > KEXT length field), CINVALID on a guard trip.
-// ---------------------------------------------------------------------------
-constexpr int CSW = 8192;             // span bytes (64 lanes x CSEG)
-constexpr int CSEG = CSW / 64;
-constexpr int CLO = 128;              // staged bytes before the span
-constexpr int CHI = 64;               // staged bytes after it (plus the 16-byte alignment slack)
-constexpr int CST = CLO + CSW + CHI + 16;
-#ifndef JFS_LZ4_CPRE0
-#define JFS_LZ4_CPRE0 96
-#endif
-constexpr int CPRE0 = JFS_LZ4_CPRE0;  // lane 0's speculative pre-roll
-constexpr int CPRE = 32;              // the other lanes'
-static_assert(CPRE0 <= CLO && CSEG == 128, "staging covers the pre-roll; two u64 per lane");
-constexpr int CWV = 4;                // spans (waves) per workgroup
-constexpr uint32_t CINVALID = 0xFFFFFFFFu;
-constexpr int CWORDS = CSW / 32;      // bitmap dwords per span
-
-__device__ __forceinline__ int32_t chain_spans(const jfs_dev_block &d) {
-    if (d.src == nullptr || d.src_len <= 0 || d.dst_cap <= 0) return 0;
-    return (int32_t)(((int64_t)d.src_len + CSW - 1) / CSW);
-}
-
-// One workgroup: spanpre[b] = first global span of block b (-1: beyond the
-// scratch capacity, the block is decoded without a bitmap), map[g] = block of
-// span g, hdr[0] = spans to walk, hdr[1] = spans the batch needs (also to
-// *need_host, a hint for the next call's scratch size).
-__global__ __launch_bounds__(1024) void lz4_chain_plan(const jfs_dev_block *__restrict__ blocks, int nblk,
-                                                       int32_t *__restrict__ hdr, int32_t *__restrict__ spanpre,
-                                                       int32_t *__restrict__ map, int32_t cap_spans,
-                                                       int32_t *need_host) {
-    __shared__ int32_t part[1024];
-    __shared__ int32_t vend;
-    const int t = threadIdx.x;
-    const int per = (nblk + 1023) / 1024;
-    const int b0 = t * per, b1 = b0 + per < nblk ? b0 + per : nblk;
-    int64_t s = 0;
-    for (int b = b0; b < b1; ++b) s += chain_spans(((const gc_blk *)blocks)[b]);
-    const int32_t sc = s > 0x3fffffff ? 0x3fffffff : (int32_t)s;
-    part[t] = sc;
-    if (t == 0) vend = 0x7fffffff;
-    __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {
-        const int32_t v = t >= o ? part[t - o] : 0;
-        __syncthreads();
-        part[t] = part[t] + v > 0x3fffffff ? 0x3fffffff : part[t] + v;
-        __syncthreads();
-    }
-    int32_t base = part[t] - sc;
-    const int32_t total = part[1023];
-    for (int b = b0; b < b1; ++b) {
-        const int32_t ns = chain_spans(((const gc_blk *)blocks)[b]);
-        if (ns > 0 && (int64_t)base + ns <= (int64_t)cap_spans) {
-            spanpre[b] = base;
-            for (int32_t j = 0; j < ns; ++j) map[base + j] = b;
-        } else {
-            spanpre[b] = -1;
-            if (ns > 0) atomicMin(&vend, base);
-        }
-        base += ns;
-    }
-    __syncthreads();
-    if (t == 0) {
-        hdr[0] = vend < total ? vend : total;
-        hdr[1] = total;
-        if (need_host) __hip_atomic_store(need_host, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-}
-
-// Next token position after p (or STOP | p) from the staged span st (st[0] =
-// position sb): the rules of g_step; a literal-length byte of 255, a
-// match-length byte of 255 or a length byte beyond the staging take the exact
-// step from HBM.
-__device__ __forceinline__ uint32_t c_step(const uint8_t *st, int32_t sb, const Ctx &c, int32_t p, bool act) {
-    const int32_t n = c.n;
-    const uint32_t edge = (uint32_t)(p > n - 18);
-    const uint32_t r = (uint32_t)(p - sb);
-    const uint32_t tb = st[r], e1 = st[r + 1];
-    const uint32_t hi = tb >> 4;
-    const uint32_t llx = (uint32_t)(hi == 15u);
-    const uint32_t L = llx ? 15u + e1 : hi;
-    const uint32_t lstop = llx & ((uint32_t)(p + 2 >= n - 15) | (uint32_t)(p + 2 + (int32_t)L > n - 32));
-    const uint32_t qq = r + 3u + llx + L;
-    const uint32_t oob = (uint32_t)(qq >= (uint32_t)CST);
-    const uint32_t e2 = st[oob ? 0u : qq];
-    const uint32_t mlx = (uint32_t)((tb & 15u) == 15u);
-    uint32_t x = (uint32_t)p + 3u + llx + L + mlx;
-    const uint32_t slow = (uint32_t)act & (edge ^ 1u) & (lstop ^ 1u) &
-                          ((llx & (uint32_t)(e1 == 255u)) | (mlx & (oob | (uint32_t)(e2 == 255u))));
-    x = (edge | lstop | (mlx & (uint32_t)((int32_t)x >= n - 4))) ? (STOP | (uint32_t)p) : x;
-    if (__ballot(slow)) {
-        if (slow) x = g_next_exact(c, p);
-    }
-    return x;
-}
-
-__global__ __launch_bounds__(64 * CWV) __attribute__((amdgpu_waves_per_eu(4))) void lz4_chain_kernel(
-    const jfs_dev_block *__restrict__ blocks, const int32_t *__restrict__ hdr, const int32_t *__restrict__ spanpre,
-    const int32_t *__restrict__ map, uint32_t *__restrict__ exits, uint32_t *__restrict__ bits) {
-    __shared__ alignas(16) uint8_t stg[CWV][CST];
-    const int w = (int)uniform(threadIdx.x >> 6), l = lane_id();
-    uint8_t *st = stg[w];
-    const int32_t total = ((const gc_u32 *)hdr)[0];
-    for (int32_t g = (int32_t)blockIdx.x * CWV + w; g < total; g += (int32_t)gridDim.x * CWV) {
-        const int b = (int)uniform((uint32_t)((const gc_u32 *)map)[g]);
-        const jfs_dev_block d = ((const gc_blk *)blocks)[b];
-        Ctx c;
-        c.src = (const gc_u8 *)d.src;
-        c.n = d.src_len;
-        c.bug = 0;
-        const int32_t S = (g - (int32_t)((const gc_u32 *)spanpre)[b]) * CSW;
-        // stage [sb, sb + CST): 16-byte chunks aligned in HBM; bytes outside [0, n) read 0
-        const uint32_t mis = (uint32_t)(((uintptr_t)c.src + (uint32_t)(S - CLO)) & 15u);
-        const int32_t sb = S - CLO - (int32_t)mis;
-        {
-            constexpr int NCH = (CST / 16 + 63) / 64;
-            uint4 v[NCH];
-#pragma unroll
-            for (int j = 0; j < NCH; ++j) {
-                const int k = l + 64 * j;
-                const int32_t p = sb + 16 * k;
-                v[j] = make_uint4(0, 0, 0, 0);
-                if (k < CST / 16 && p < c.n && p + 16 > 0) v[j] = *(const gc_u4 *)(c.src + p);
-            }
-#pragma unroll
-            for (int j = 0; j < NCH; ++j) {
-                const int k = l + 64 * j;
-                if (k < CST / 16) *(uint4 *)(st + 16 * k) = v[j];
-            }
-            if (sb < 0 || sb + CST > c.n) {
-                for (int k = l; k < CST; k += 64) {
-                    const int32_t p = sb + k;
-                    if (p >= c.n || p < 0) st[k] = 0;
-                }
-            }
-            __builtin_amdgcn_wave_barrier();
-        }
-        // speculative walks: lane l from CPRE bytes before its segment (lane 0
-        // from CPRE0 before the span, or from the block start)
-        const int32_t plo = S + l * CSEG, phi = plo + CSEG;
-        const uint32_t cur0 = (uint32_t)(l == 0 ? (S == 0 ? 0 : S - CPRE0) : plo - CPRE);
-        uint32_t cur = cur0;
-        uint64_t vs0 = 0, vs1 = 0;
-        uint32_t sx = 0;
-        {
-            int32_t q = (int32_t)cur;
-            bool mv = true;
-            for (int steps = 0; __ballot(mv); ++steps) {
-                if (mv) {
-                    const uint32_t x = c_step(st, sb, c, q, true);
-                    const bool stop = (x & STOP) != 0;
-                    if (!stop && q >= plo) sbit2(vs0, vs1, (uint32_t)(q - plo));
-                    const bool out = stop || (int32_t)x >= phi;
-                    sx = out ? x : sx;
-                    mv = !out;
-                    q = (int32_t)x;
-                }
-                if (steps > CSEG + CPRE0) { c.bug = 6; break; }
-            }
-        }
-        // fix-up rounds: true entry of segment l = exit of segment l-1; an
-        // entry off the speculative chain walks until it joins it (or leaves)
-        uint64_t vt0 = vs0, vt1 = vs1;
-        uint32_t ex = sx;
-        for (int rounds = 0; !c.bug; ++rounds) {
-            const uint32_t In = dpp_shift_up(ex, cur0);
-            const bool ch = In != cur;
-            if (!__ballot(ch)) break;
-            if (rounds > 64) { c.bug = 3; break; }
-            bool mv = false;
-            if (ch) {
-                cur = In;
-                const uint32_t dd = In - (uint32_t)plo;
-                if ((In & STOP) || (int32_t)In >= phi) {
-                    vt0 = vt1 = 0;
-                    ex = In;
-                } else if (tbit2(vs0, vs1, dd)) {
-                    vt0 = vs0 & from_lo(dd);
-                    vt1 = vs1 & from_hi(dd);
-                    ex = sx;
-                } else {
-                    mv = true;
-                }
-            }
-            int32_t q = (int32_t)In;
-            uint64_t vp0 = 0, vp1 = 0;
-            for (int steps = 0; __ballot(mv); ++steps) {
-                if (mv) {
-                    const uint32_t dd = (uint32_t)(q - plo);
-                    const bool join = tbit2(vs0, vs1, dd);
-                    const uint32_t x = c_step(st, sb, c, q, !join);
-                    const bool stop = !join && (x & STOP) != 0;
-                    if (!join && !stop) sbit2(vp0, vp1, dd);
-                    const bool out = join || stop || (int32_t)x >= phi;
-                    if (out) {
-                        vt0 = vp0 | (join ? vs0 & from_lo(dd) : 0ull);
-                        vt1 = vp1 | (join ? vs1 & from_hi(dd) : 0ull);
-                        ex = join ? sx : x;
-                    }
-                    mv = !out;
-                    q = (int32_t)x;
-                }
-                if (steps > CSEG + 1) { c.bug = 7; break; }
-            }
-        }
-        uint4 o;
-        o.x = (uint32_t)vt0;
-        o.y = (uint32_t)(vt0 >> 32);
-        o.z = (uint32_t)vt1;
-        o.w = (uint32_t)(vt1 >> 32);
-        *(g_u4 *)(bits + (size_t)g * CWORDS + 4 * l) = o;
-        const uint32_t e63 = readlane(ex, 63);
-        if (l == 0) ((g_u32 *)exits)[g] = c.bug ? CINVALID : e63;
-        __builtin_amdgcn_wave_barrier();  // the next span's staging overwrites st
-    }
-}
-
 // Dword k (0..4*64-1) of the span's bit set; lane k/4 holds it as dword k%4 of
 // (vt0, vt1).  Out-of-span dwords read as 0.
 __device__ __forceinline__ uint32_t span_dword(uint64_t vt0, uint64_t vt1, int32_t k) {
@@ -1751,112 +1502,6 @@ __device__ __forceinline__ void parse_window(Smem &s, Ctx &c, int32_t wbase, uin
 }
 
 #if JFS_LZ4_SEG
-// Token table of the window from this lane's 32 position bits (positions plo
-// .. plo + 31, lane l = window bytes 32 l ..): positions relative to cbase in
-// stream order.  Returns the token count; *T_out = min(count, TCAP) and, when
-// the window is cut, *cut = the position of token TCAP (the next window's start).
-__device__ __forceinline__ uint32_t table_from_bits(Ctx &c, uint32_t field, int32_t plo, uint32_t *T_out,
-                                                   uint32_t *cut) {
-    const int l = lane_id();
-    const uint32_t cnt = (uint32_t)__builtin_popcount(field);
-    const uint32_t cinc = dpp_scan_add(cnt);
-    const uint32_t tall = readlane(cinc, 63);
-    *T_out = tall < (uint32_t)TCAP ? tall : (uint32_t)TCAP;
-    uint32_t ex = 0;
-    {
-        uint32_t idx = cinc - cnt;
-        uint32_t v = field;
-        while (__ballot(v != 0)) {
-            if (v) {
-                const uint32_t bb = (uint32_t)__builtin_ctz(v);
-                if (idx < (uint32_t)TCAP) c.tab[idx] = (uint16_t)((uint32_t)l * P + bb);
-                else if (idx == (uint32_t)TCAP) ex = (uint32_t)plo + bb;  // first token left to the next window
-                idx++;
-                v &= v - 1;
-            }
-        }
-    }
-    if (tall > (uint32_t)TCAP) {
-        const uint64_t hit = __ballot(cinc - cnt <= (uint32_t)TCAP && (uint32_t)TCAP < cinc);
-        *cut = readlane(ex, (int)__builtin_ctzll(hit));
-    }
-    return tall;
-}
-
-// Mode A: stage the window at wbase and table its tokens from the chain bitmap
-// (bits / ex: this block's bitmap dwords and span exits, nwords dwords).  A
-// window ends at cbase + CW or at its span's end.  Returns false, having
-// tabled nothing, when wbase is not a set bit of its span (the span's
-// speculative entry had not met the true chain yet) or the span's walk
-// failed: the parser then walks that span itself (mode B).
-__device__ __forceinline__ bool parse_window_bits(Smem &s, Ctx &c, int32_t wbase, const gc_u32 *bits,
-                                                  const gc_u32 *ex, int32_t nwords, uint32_t *T_out,
-                                                  uint32_t *efin_out PROF_ARG) {
-    static_assert(P == 32 && CW == 64 * 32, "a window lane covers one bitmap dword");
-    const int l = lane_id();
-    const int32_t k = wbase / CSW;
-    const int32_t B = (k + 1) * CSW;
-    const uint32_t exv = ex[k];
-    const uint32_t mis = (uint32_t)(((uintptr_t)c.src + (uint32_t)wbase) & 15u);
-    const int32_t cbase = wbase - (int32_t)mis;  // = stage_window's
-    // bits of positions [cbase + 32 l, +32) and [cbase + CW + 32 l, +32),
-    // loaded with the window's staging (one HBM latency)
-    const int32_t w0 = (cbase >> 5) + l;
-    const uint32_t a0 = (w0 >= 0 && w0 < nwords) ? bits[w0] : 0u;
-    const uint32_t a1 = (w0 + 1 >= 0 && w0 + 1 < nwords) ? bits[w0 + 1] : 0u;
-    const uint32_t b0 = (w0 + 64 < nwords) ? bits[w0 + 64] : 0u;
-    const uint32_t b1 = (w0 + 65 < nwords) ? bits[w0 + 65] : 0u;
-    stage_window(s, c, wbase);
-    PCOUNT(10, 1);
-    __builtin_amdgcn_wave_barrier();
-    PSTAMP(0);
-    const uint32_t sh = (uint32_t)cbase & 31u;
-    uint32_t f0 = __builtin_amdgcn_alignbit(a1, a0, sh);
-    uint32_t f1 = __builtin_amdgcn_alignbit(b1, b0, sh);
-    if (exv == CINVALID || !((readlane(f0, 0) >> mis) & 1u)) return false;
-    const int32_t wend = cbase + CW < B ? cbase + CW : B;
-    const int32_t plo = cbase + 32 * l;
-    {
-        const int32_t a = wbase - plo, b = wend - plo;  // keep bits [a, b)
-        const uint32_t ma = a <= 0 ? 0xFFFFFFFFu : a >= 32 ? 0u : (0xFFFFFFFFu << a);
-        const uint32_t mb = b >= 32 ? 0xFFFFFFFFu : b <= 0 ? 0u : ((1u << b) - 1u);
-        f0 &= ma & mb;
-    }
-    PSTAMP(1);
-    uint32_t cut = 0;
-    const uint32_t tall = table_from_bits(c, f0, plo, T_out, &cut);
-    if (tall > (uint32_t)TCAP) {
-        *efin_out = cut;
-    } else if (wend == B) {
-        *efin_out = exv;
-    } else {
-        // the first chain position >= wend (= cbase + CW) in this span
-        const int32_t b = B - (plo + CW);
-        f1 &= b >= 32 ? 0xFFFFFFFFu : b <= 0 ? 0u : ((1u << b) - 1u);
-        const uint64_t any = __ballot(f1 != 0u);
-        if (any) {
-            const int f = (int)__builtin_ctzll(any);
-            *efin_out = (uint32_t)(cbase + CW + 32 * f) + (uint32_t)__builtin_ctz(readlane(f1, f));
-        } else if (B <= cbase + 2 * CW) {
-            *efin_out = exv;
-        } else {
-            // a token reaching past the next window's bits: its successor, parsed
-            const uint64_t lm = __ballot(f0 != 0u);
-            const int f = 63 - (int)__builtin_clzll(lm);
-            const int32_t plast = cbase + 32 * f + 31 - (int32_t)__builtin_clz(readlane(f0, f));
-            const Tok u = parse_tok(s, c, plast);
-            if ((uint32_t)u.nxt & STOP) {  // (not expected: the bitmap marks no stop token) leave it to the copier
-                *T_out = *T_out - 1u;
-                *efin_out = STOP | (uint32_t)plast;
-            } else {
-                *efin_out = (uint32_t)u.nxt;
-            }
-        }
-    }
-    PSTAMP(2);
-    return true;
-}
-
 // The chain of one span (seg_chain), kept by the parser wave across windows.
 struct Span {
     uint64_t v0, v1;  // this lane's segment bits
@@ -1888,10 +1533,28 @@ __device__ __forceinline__ void parse_window_seg(Smem &s, Ctx &c, int32_t wbase,
     const uint32_t mb = b >= 32 ? 0xFFFFFFFFu : b <= 0 ? 0u : ((1u << b) - 1u);
     field &= ma & mb;
     PSTAMP(1);
-    uint32_t cut = 0;
-    const uint32_t tall = table_from_bits(c, field, plo, T_out, &cut);
+    // token table: positions (relative to cbase) in stream order
+    const uint32_t cnt = (uint32_t)__builtin_popcount(field);
+    const uint32_t cinc = dpp_scan_add(cnt);
+    const uint32_t tall = readlane(cinc, 63);
+    *T_out = tall < (uint32_t)TCAP ? tall : (uint32_t)TCAP;
+    uint32_t ex = 0;
+    {
+        uint32_t idx = cinc - cnt;
+        uint32_t v = field;
+        while (__ballot(v != 0)) {
+            if (v) {
+                const uint32_t bb = (uint32_t)__builtin_ctz(v);
+                if (idx < (uint32_t)TCAP) c.tab[idx] = (uint16_t)((uint32_t)l * P + bb);
+                else if (idx == (uint32_t)TCAP) ex = (uint32_t)plo + bb;  // first token left to the next window
+                idx++;
+                v &= v - 1;
+            }
+        }
+    }
     if (tall > (uint32_t)TCAP) {  // the window ends at token TCAP
-        *efin_out = cut;
+        const uint64_t hit = __ballot(cinc - cnt <= (uint32_t)TCAP && (uint32_t)TCAP < cinc);
+        *efin_out = readlane(ex, (int)__builtin_ctzll(hit));
     } else if (wend >= send) {
         *efin_out = sp.exit;
     } else {
@@ -1927,11 +1590,9 @@ __device__ __forceinline__ void use_buffer(Smem &s, Ctx &c, int buf) {
 // output-side check, the end of the block) it runs the serial restatement
 // and, if the fast path applies again, restarts the parser at the new input
 // position (the window the parser produced meanwhile is skipped).
-__device__ __forceinline__ void parser_wave(Smem &s, Ctx &c, const gc_u32 *cbits, const gc_u32 *cex,
-                                            int32_t cnw PROF_ARG) {
+__device__ __forceinline__ void parser_wave(Smem &s, Ctx &c PROF_ARG) {
     int32_t pip = 0;
     bool pstop = false;
-    const bool chainA = cbits != nullptr;  // mode A: tables from the chain bitmap
 #if JFS_LZ4_SEG
     Span sp;
     sp.v0 = sp.v1 = 0;
@@ -1955,11 +1616,8 @@ __device__ __forceinline__ void parser_wave(Smem &s, Ctx &c, const gc_u32 *cbits
                 use_buffer(s, c, buf);
                 uint32_t T, efin;
 #if JFS_LZ4_SEG
-                bool got = false;
-                if (chainA && !(spv && pip < sp.base + SW))
-                    got = parse_window_bits(s, c, pip, cbits, cex, cnw, &T, &efin PROF_PASS);
-                if (!got && (!spv || pip >= sp.base + SW)) {
-                    // mode B, the span at pip: the walk started ahead of time, or a fresh one
+                if (!spv || pip >= sp.base + SW) {
+                    // the span at pip: the walk started ahead of time, or a fresh one
                     if (!(spv && nxt && wk.base == pip)) wk.start(pip);
                     wk.advance(c, 1 << 20 PROF_PASS);
                     PSTAMP(1);
@@ -1968,13 +1626,11 @@ __device__ __forceinline__ void parser_wave(Smem &s, Ctx &c, const gc_u32 *cbits
                     sp.base = pip;
                     sp.exit = readlane(wk.ex, 63);
                     spv = true;
-                    // walk the next span during this one's windows (mode B only:
-                    // with the bitmap the next span is tried in mode A first)
-                    nxt = !chainA && !(sp.exit & STOP) && !c.bug;
-                    if (nxt) wk.start((int32_t)sp.exit);
+                    nxt = !(sp.exit & STOP) && !c.bug;
+                    if (nxt) wk.start((int32_t)sp.exit);  // walk the next span during this one's windows
                 }
-                if (!got) parse_window_seg(s, c, pip, sp, &T, &efin PROF_PASS);
-                if (!got && nxt) {
+                parse_window_seg(s, c, pip, sp, &T, &efin PROF_PASS);
+                if (nxt) {
                     // walk the next span while the copier is still busy with its
                     // window (at least SEG_MIN steps per window)
                     bool fin = wk.advance(c, SEG_MIN PROF_PASS);
@@ -2049,18 +1705,14 @@ __device__ __forceinline__ void copier_wave(Smem &s, Ctx &c, int32_t *retp PROF_
             } else if (m.kind == W_WIN && st.fast && st.ip < c.n - 64 && st.op < c.cap - 128) {
                 use_buffer(s, c, buf);
                 c.cbase = m.cbase;
-                int32_t end_op = st.op, bad_ip = 0, last_nxt = st.ip;
-                const uint32_t dn =
-                    m.T > 0 ? copy_tokens(s, c, m.T, st.op, st.ip, &end_op, &bad_ip, &last_nxt PROF_PASS) : 0u;
+                int32_t end_op = st.op, bad_ip = 0;
+                const uint32_t dn = m.T > 0 ? copy_tokens(s, c, m.T, st.op, &end_op, &bad_ip PROF_PASS) : 0u;
                 st.op = end_op;
                 if (dn < m.T) {
                     st.ip = bad_ip;
                     ser = true;
-                } else if (last_nxt != (int32_t)(m.efin & ~STOP)) {
-                    st.ip = last_nxt;  // the window's exit is not where its last token ends
-                    ser = true;
                 } else {
-                    st.ip = last_nxt;
+                    st.ip = (int32_t)(m.efin & ~STOP);
                     ser = (m.efin & STOP) != 0;
                 }
             } else {
@@ -2123,15 +1775,10 @@ __device__ __forceinline__ void copier_wave(Smem &s, Ctx &c, int32_t *retp PROF_
 // previous kernel of a fused chain (AES-GCM open); < 0 = that step failed.
 // todo (optional): only the blocks with todo[b] != 0 are decoded (the others
 // were decoded by lz4_split.hip and keep its results).
-// bits / spanpre / exits (optional): the chain bitmap of lz4_chain_kernel; a
-// block with spanpre[b] < 0 (beyond the bitmap's capacity) is parsed in-kernel.
 __global__ __launch_bounds__(128) JFS_LZ4_ATTR void lz4_decode_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
                                                         int32_t *__restrict__ ret,
                                                         const int32_t *__restrict__ lens,
-                                                        const int32_t *__restrict__ todo,
-                                                        const uint32_t *__restrict__ bits,
-                                                        const int32_t *__restrict__ spanpre,
-                                                        const uint32_t *__restrict__ exits) {
+                                                        const int32_t *__restrict__ todo) {
     __shared__ Smem s;
     const int b = blockIdx.x;
     if (b >= nblk) return;
@@ -2167,17 +1814,7 @@ __global__ __launch_bounds__(128) JFS_LZ4_ATTR void lz4_decode_kernel(const jfs_
         if (wave == 1 && lane_id() == 0) ret[b] = result;
         return;
     }
-    const gc_u32 *cbits = nullptr, *cex = nullptr;
-    int32_t cnw = 0;
-    if (bits && !lens) {
-        const int32_t sp0 = (int32_t)uniform((uint32_t)((const gc_u32 *)spanpre)[b]);
-        if (sp0 >= 0) {
-            cbits = (const gc_u32 *)bits + (size_t)sp0 * CWORDS;
-            cex = (const gc_u32 *)exits + sp0;
-            cnw = (int32_t)(((int64_t)c.n + CSW - 1) / CSW) * CWORDS;
-        }
-    }
-    if (wave == 0) parser_wave(s, c, cbits, cex, cnw PROF_PASS);
+    if (wave == 0) parser_wave(s, c PROF_PASS);
     else copier_wave(s, c, ret + b PROF_PASS);
 #ifdef JFS_PROF
     pr.flush_out();
@@ -2205,8 +1842,7 @@ extern "C" int jfs_launch_lz4_decode_lens(const jfs_dev_block *d_blocks, int nbl
                                           hipStream_t stream) {
     if (nblk <= 0) return 0;
     hipLaunchKernelGGL(jfs::lz4d::lz4_decode_kernel, dim3(nblk), dim3(128), 0, stream, d_blocks, nblk, d_ret, d_lens,
-                       (const int32_t *)nullptr, (const uint32_t *)nullptr, (const int32_t *)nullptr,
-                       (const uint32_t *)nullptr);
+                       (const int32_t *)nullptr);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -2214,67 +1850,6 @@ extern "C" int jfs_launch_lz4_decode_todo(const jfs_dev_block *d_blocks, int nbl
                                           hipStream_t stream) {
     if (nblk <= 0) return 0;
     hipLaunchKernelGGL(jfs::lz4d::lz4_decode_kernel, dim3(nblk), dim3(128), 0, stream, d_blocks, nblk, d_ret,
-                       (const int32_t *)nullptr, d_todo, (const uint32_t *)nullptr, (const int32_t *)nullptr,
-                       (const uint32_t *)nullptr);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
-// Chain-bitmap scratch: header | spanpre[nblk] | map[cap] | exits[cap] | bits[cap * 8 KiB / 8]
-namespace {
-struct ChainLayout {
-    int64_t hdr, spanpre, map, exits, bits, total;
-};
-ChainLayout chain_layout(int nblk, int64_t cap_spans) {
-    auto up = [](int64_t x) { return (x + 255) & ~(int64_t)255; };
-    ChainLayout L;
-    L.hdr = 0;
-    L.spanpre = 256;
-    L.map = L.spanpre + up(4 * (int64_t)nblk);
-    L.exits = L.map + up(4 * cap_spans);
-    L.bits = L.exits + up(4 * cap_spans);
-    L.total = L.bits + cap_spans * (jfs::lz4d::CSW / 8);
-    return L;
-}
-}  // namespace
-
-extern "C" int64_t jfs_lz4_chain_scratch_bytes(int nblk, int64_t cap_spans) {
-    return chain_layout(nblk, cap_spans).total;
-}
-
-extern "C" int64_t jfs_lz4_chain_spans(int nblk, const int32_t *src_len) {
-    int64_t s = 0;
-    for (int i = 0; i < nblk; ++i)
-        if (src_len[i] > 0) s += ((int64_t)src_len[i] + jfs::lz4d::CSW - 1) / jfs::lz4d::CSW;
-    return s;
-}
-
-// Plan + chain walk + decode, all on `stream`.  Blocks whose spans do not fit
-// cap_spans are decoded with the in-kernel parser; need_host (mapped host
-// memory, optional) receives the spans the batch needed.
-extern "C" int jfs_launch_lz4_decode_chain(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, void *scratch,
-                                           int64_t cap_spans, int32_t *need_host, hipStream_t stream) {
-    using namespace jfs::lz4d;
-    if (nblk <= 0) return 0;
-    if (cap_spans > 0x3fffffff) cap_spans = 0x3fffffff;
-    const ChainLayout L = chain_layout(nblk, cap_spans);
-    uint8_t *p = (uint8_t *)scratch;
-    int32_t *hdr = (int32_t *)(p + L.hdr), *spanpre = (int32_t *)(p + L.spanpre), *map = (int32_t *)(p + L.map);
-    uint32_t *exits = (uint32_t *)(p + L.exits), *bits = (uint32_t *)(p + L.bits);
-    hipLaunchKernelGGL(lz4_chain_plan, dim3(1), dim3(1024), 0, stream, d_blocks, nblk, hdr, spanpre, map,
-                       (int32_t)cap_spans, need_host);
-    // persistent grid: four 4-wave workgroups per CU (LDS), striding over the spans
-    int ncu = 256;
-    {
-        int dev = 0;
-        if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    }
-    int64_t grid = 4ll * ncu;
-    const int64_t need_wg = (cap_spans + CWV - 1) / CWV;
-    if (grid > need_wg) grid = need_wg > 0 ? need_wg : 1;
-    hipLaunchKernelGGL(lz4_chain_kernel, dim3((unsigned)grid), dim3(64 * CWV), 0, stream, d_blocks,
-                       (const int32_t *)hdr, (const int32_t *)spanpre, (const int32_t *)map, exits, bits);
-    hipLaunchKernelGGL(lz4_decode_kernel, dim3(nblk), dim3(128), 0, stream, d_blocks, nblk, d_ret,
-                       (const int32_t *)nullptr, (const int32_t *)nullptr, (const uint32_t *)bits,
-                       (const int32_t *)spanpre, (const uint32_t *)exits);
+                       (const int32_t *)nullptr, d_todo);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -18,15 +18,6 @@ from tests.test_lz4_gpu import _dense_tokens
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["inkernel", "chain"], autouse=True)
-def parser_mode(request, monkeypatch):
-    """Every case runs twice: the in-kernel segment-walk parser and the
-    chain-bitmap path (a separate grid finds the token chains first,
-    JFS_LZ4_CHAIN=1), whose tables the copier checks link by link."""
-    monkeypatch.setenv("JFS_LZ4_CHAIN", "1" if request.param == "chain" else "0")
-    return request.param
-
-
 def _run_device(gpu, comps, caps, mis_s=0, mis_d=0):
     import torch
     from juicefs_amd import device as D
