@@ -582,16 +582,30 @@ def mixed_host_path(raw_src, nblk=4096, seed=11, device_mask=0):
                     "host buffers in and out, GPU encoders and decoders, every block verified"}
 
 
-def dealer_legs(batch, U, a):
+def check_spread(device_blocks, ndev, nblk):
+    """The dealer must have put blocks on every one of the job's ndev devices
+    (as many as there were blocks): a library that saw fewer devices, or a deal
+    that skipped one, fails the leg instead of reporting a one-GPU figure."""
+    used = sorted(d for d, n in device_blocks.items() if n > 0)
+    want = min(ndev, nblk)
+    if len(used) < want:
+        raise RuntimeError(f"dealer: blocks ran on devices {used}, expected {want} of the job's {ndev} GPUs")
+    return used
+
+
+def dealer_legs(batch, U, a, world=1):
     """Rank 0 with device_mask = all GPUs: host_path (LZ4 decompress and
     compress of host buffers) and configs[4] (mixed LZ4/Zstd, 64 KiB-4 MiB),
     the batch ABI dealing blocks round-robin over every visible device; the
-    per-device block counters show the spread."""
+    per-device block counters must show all `world` GPUs used."""
     from juicefs_amd import _lib as L
     ns = min(32, batch.nblk)
     comp = [batch.comp[i * batch.slot:i * batch.slot + int(batch.csize[i])].cpu().numpy().tobytes() for i in range(ns)]
     raws = [batch.raw[i * U:(i + 1) * U].cpu().numpy().tobytes() for i in range(ns)]
     lib = L.load()
+    nvis = lib.jfs_device_count()
+    if nvis < world:
+        raise RuntimeError(f"dealer: the library sees {nvis} gfx950 devices, the job has {world}")
     lib.jfs_stats_reset()
     out = {"host_path": host_path_rate(comp, raws, U, a.host_blocks, device_mask=0)}
     if not a.no_mixed:
@@ -600,63 +614,95 @@ def dealer_legs(batch, U, a):
     ds = (L.JfsDeviceStat * 64)()
     nd = lib.jfs_device_stats(ds, 64)
     out["device_blocks"] = {int(ds[i].device): int(ds[i].blocks) for i in range(nd)}
+    out["devices_used"] = check_spread(out["device_blocks"], world, a.host_blocks)
+    out["value"] = _pick(out, "host_path", "lz4_decompress", "value")
     out["path"] = ("rank 0 alone, jfs_{de,}compress_batch with device_mask 0 (every visible GPU), blocks dealt "
                    "round-robin, one host thread per device; host buffers in and out")
     return out
 
 
-def ranked_host_path(S, world, rank, local, dev, nblk, U):
+class GpuHostOps:
+    """The batch ABI of libjfsgpu.so as ranked_host_path uses it (host
+    buffers; the tests substitute a CPU stand-in with the same methods)."""
+
+    def __init__(self, dev):
+        from juicefs_amd import compress as C
+        self.dev = dev
+        self.c = C.LZ4()
+
+    def gen(self, nblk, U, seed):
+        import torch
+        from juicefs_amd import device as D
+        dbuf = torch.empty(nblk * U, dtype=torch.uint8, device=self.dev)
+        D.gen_blocks(dbuf, nblk, U, "T", seed)
+        return dbuf.cpu().numpy()
+
+    def bound(self, U):
+        return self.c.CompressBound(U)
+
+    def compress(self, pairs, mask):
+        return self.c.CompressBatch(pairs, device_mask=mask)
+
+    def decompress(self, pairs, mask):
+        return self.c.DecompressBatch(pairs, device_mask=mask)
+
+    def reset_stats(self):
+        from juicefs_amd import _lib as L
+        L.load().jfs_stats_reset()
+
+    def device_blocks(self):
+        from juicefs_amd import _lib as L
+        ds = (L.JfsDeviceStat * 64)()
+        nd = L.load().jfs_device_stats(ds, 64)
+        return {int(ds[i].device): int(ds[i].blocks) for i in range(nd) if ds[i].blocks}
+
+
+def ranked_host_path(S, world, rank, local, dev, nblk, U, ops=None):
     """BASELINE configs[0] on every rank (N > 1): each process compresses and
     decompresses its own nblk host blocks through jfs_{de,}compress_batch
     with device_mask = its GPU only (the batch ABI's device selection,
     SURVEY.md 8e), timed between barriers, max over ranks; value = all ranks'
-    uncompressed bytes / that time.  The library's per-device counters show
-    which GPU each rank's blocks ran on."""
-    import torch
-    from juicefs_amd import _lib as L
-    from juicefs_amd import compress as C
-    from juicefs_amd import device as D
+    uncompressed bytes / that time.  The library's per-device counters must
+    show every rank's blocks on its own GPU only: anything else (a rank whose
+    blocks ran elsewhere, a mismatch on any rank) fails every rank loudly."""
+    ops = ops or GpuHostOps(dev)
     mask = 1 << local
     raw = np.empty(nblk * U, dtype=np.uint8)
-    dbuf = torch.empty(nblk * U, dtype=torch.uint8, device=dev)
-    D.gen_blocks(dbuf, nblk, U, "T", S.seed_base(rank, nblk) + 70001)
-    raw[:] = dbuf.cpu().numpy()
-    del dbuf
-    c = C.LZ4()
-    bound = c.CompressBound(U)
+    raw[:] = ops.gen(nblk, U, S.seed_base(rank, nblk) + 70001)
+    bound = ops.bound(U)
     comp = np.zeros(nblk * bound, dtype=np.uint8)
     pairs = [(comp[i * bound:(i + 1) * bound], raw[i * U:(i + 1) * U]) for i in range(nblk)]
-    res = c.CompressBatch(pairs, device_mask=mask)  # warm: staging pinned, scratch sized
-    lib = L.load()
-    lib.jfs_stats_reset()
+    ops.compress(pairs, mask)  # warm: staging pinned, scratch sized
+    ops.reset_stats()
     holder = {}
 
     def comp_step():
-        holder["c"] = c.CompressBatch(pairs, device_mask=mask)
+        holder["c"] = ops.compress(pairs, mask)
     tc = S.max_over_ranks(S.timed_steps(comp_step, 1, 0, lambda: None, world), world, dev)
     res = holder["c"]
     sizes = [n for n, e in res]
     ok = all(e is None and n > 0 for n, e in res)
     out = np.zeros(nblk * U, dtype=np.uint8)
     dpairs = [(out[i * U:(i + 1) * U], comp[i * bound:i * bound + sizes[i]]) for i in range(nblk)]
-    c.DecompressBatch(dpairs, device_mask=mask)  # warm
+    ops.decompress(dpairs, mask)  # warm
 
     def dec_step():
-        holder["d"] = c.DecompressBatch(dpairs, device_mask=mask)
+        holder["d"] = ops.decompress(dpairs, mask)
     td = S.max_over_ranks(S.timed_steps(dec_step, 1, 0, lambda: None, world), world, dev)
     ok = ok and all(e is None and n == U for n, e in holder["d"]) and np.array_equal(out, raw)
     if not S.all_ranks_ok(ok, world, dev):
         raise RuntimeError("ranked host path: round trip mismatch on some rank")
-    ds = (L.JfsDeviceStat * 64)()
-    nd = lib.jfs_device_stats(ds, 64)
-    mine = {int(ds[i].device): int(ds[i].blocks) for i in range(nd) if ds[i].blocks}
+    mine = ops.device_blocks()
     # every rank's blocks ran on its own GPU only
-    only_mine = S.all_ranks_ok(set(mine) == {local}, world, dev)
+    if not S.all_ranks_ok(set(mine) == {local}, world, dev):
+        raise RuntimeError(f"ranked host path: rank {rank} (local {local}) blocks ran on devices {sorted(mine)}; "
+                           "some rank's device_mask was not honoured")
     total = world * nblk * U
     return {"decompress": {"value": total / td / 2**30, "unit": "GiB/s", "s": td},
             "compress": {"value": total / tc / 2**30, "unit": "GiB/s", "s": tc},
+            "value": total / td / 2**30,
             "blocks_per_gpu": nblk, "n_gpus": world, "scaling": "weak",
-            "rank0_device_blocks": mine, "each_rank_used_only_its_gpu": bool(only_mine),
+            "rank0_device_blocks": mine, "each_rank_used_only_its_gpu": True,
             "path": "configs[0] per rank: jfs_compress_batch / jfs_decompress_batch with device_mask = 1 << "
                     "local_rank, host buffers, barrier-bracketed, max over ranks; every block verified"}
 
@@ -840,6 +886,8 @@ def main():
     world, rank, local = env.world, env.rank, env.local
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    if world > 1 and torch.cuda.device_count() < world:
+        raise SystemExit(f"--gpus {world}: only {torch.cuda.device_count()} GPUs visible to rank {rank}")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -938,7 +986,7 @@ def main():
         if rank == 0:
             try:
                 _mark("dealer_all_gpus")
-                out["dealer_all_gpus"] = dealer_legs(batch, U, a)
+                out["dealer_all_gpus"] = dealer_legs(batch, U, a, world)
             except Exception as e:
                 out["dealer_all_gpus"] = {"error": repr(e)}
         S._barrier(world)

@@ -109,7 +109,8 @@ int64_t jfs_decompress_batch(int algo, int nblk, const jfs_iov *iov, int64_t *ou
  * share every device's lanes instead of queueing behind one another (encode
  * calls run in turn: the encoders slow each other down).  Per-block
  * results as jfs_{de,}compress_batch (JFS_ERR_INVALID for an unknown algo[i]);
- * returns JFS_OK or the first whole-call error of a codec's call. */
+ * returns JFS_OK or the first failing codec call's whole-call error, which is
+ * then also written to out_n[i] of every block of that codec. */
 int64_t jfs_compress_batch_mixed(const int32_t *algo, int nblk, const jfs_iov *iov, int64_t *out_n,
                                  uint32_t device_mask);
 int64_t jfs_decompress_batch_mixed(const int32_t *algo, int nblk, const jfs_iov *iov, int64_t *out_n,
@@ -128,12 +129,6 @@ int64_t jfs_decompress_batch_csum(int algo, int nblk, const jfs_iov *iov, int64_
  * library uses src_len + dst_cap + 4096): longest-first greedy onto the least
  * loaded device, so no device ends more than one block above another. */
 void jfs_deal_plan(const int64_t *cost, int n, int ndev, int32_t *out_dev);
-/* Test hook (host only, no GPU): runs the coalescer's burst-spreading lane
- * acquisition (own lane blocking, other devices' lanes try-locked) on ndev fake
- * devices, NLANE concurrent workers each, iters bursts per worker.  Returns the
- * number of bursts that took at least one foreign lane, or -1 if the workers
- * did not finish within timeout_ms (a deadlock), -2 on bad arguments. */
-int64_t jfs_test_spread_locking(int ndev, int iters, int timeout_ms);
 
 /* ---- Encrypted objects (host buffers): compress + seal, open + decompress --
  * The PUT path of an encrypted volume is Compress (cached_store.go:372) and

@@ -31,6 +31,7 @@
 #include <thread>
 #include <vector>
 
+#include "../../include/jfs_gpucodec_test.h"
 #include "blockgen.h"
 #include "jfs_internal.h"
 
@@ -72,6 +73,14 @@ constexpr int64_t CSUM_SEG = 32 << 10;
 
 // Upper bound on one slot's staging (JFS_STAGING_MAX_MB; default none): a
 // request that needs more fails alone with JFS_ERR_NO_MEMORY.
+// Footprint without a cap: a slot holds one chunk's input + output, at most
+// the chunk limit (2 GiB decode, 4 GiB LZ4 / Zstd compress) plus one block;
+// a lane has NSLOT = 3 slots and a device NLANE = 2 lanes, each slot pinned
+// on the host and mirrored in HBM.  Peak per device: 2 x 3 x 4 GiB = 24 GiB
+// pinned + 24 GiB HBM when both lanes run compress batches (e.g. LZ4 and Zstd
+// at once), 12 + 12 GiB for two decode lanes; freed after JFS_STAGING_IDLE_MS
+// of inactivity or by jfs_release_staging().  Hosts with less memory to pin
+// set JFS_STAGING_MAX_MB (and JFS_HOST_CHUNK_MB[_LZ4C] to keep chunks under it).
 int64_t staging_max_bytes() {
     static int64_t v = [] {
         const char *e = getenv("JFS_STAGING_MAX_MB");
@@ -1982,13 +1991,16 @@ static int64_t batch_mixed(int dir, const int32_t *algo, int nblk, const jfs_iov
         // parse rounds ran 0.93 GiB/s against 1.47 in turn
         for (Group &g : gs) run(g);
     }
+    // the first failing codec call's code is returned, and every block of a
+    // failed call reports it in out_n (never a stale length)
     int64_t rc = JFS_OK;
     for (Group &g : gs) {
+        const std::vector<int> &ix = idx[g.algo];
         if (g.rc != JFS_OK) {
-            rc = g.rc;
+            if (rc == JFS_OK) rc = g.rc;
+            for (size_t k = 0; k < ix.size(); k++) out_n[ix[k]] = g.rc;
             continue;
         }
-        const std::vector<int> &ix = idx[g.algo];
         for (size_t k = 0; k < ix.size(); k++) out_n[ix[k]] = g.out[k];
     }
     return rc;

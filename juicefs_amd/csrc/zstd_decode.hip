@@ -825,14 +825,21 @@ __device__ __forceinline__ int32_t read_huf(LitSmem &sm, const gc_u8 *in, const 
         int32_t c = read_ncount(sm.stage, hb, sm.norm, &maxsym, &al, 6);
         if (c < 0 || c > hb) return -1;
 #if JFS_HUF_FSEPAR
-        // the weight table by the lane-parallel sequence-table builder (u16
-        // cells sym | state << 6 into symnext; sm.w is free until the weights
-        // are decoded), then expanded to sym | nb << 8 | base << 16
-        build_seq_fse_g(sm.symnext, sm.norm, maxsym, al, sm.w, sm.w + 128, sm.symat);
-        if (l < (1 << al)) {
-            const uint32_t v = sm.symnext[l], ns = v >> 6;
-            const int nb = al - (31 - __builtin_clz(ns));
-            sm.fse[l] = (v & 63u) | ((uint32_t)nb << 8) | (((ns << nb) - (1u << al)) << 16);
+        if (maxsym > 63) {
+            // (only a damaged description counts a weight symbol >= 64: the
+            // lane-parallel builder holds one symbol per lane, so take the
+            // serial spread of oracle/zstd_oracle.c and libzstd)
+            if (build_fse(sm.fse, sm.norm, maxsym, al, sm.symnext, sm.symat)) return -1;
+        } else {
+            // the weight table by the lane-parallel sequence-table builder (u16
+            // cells sym | state << 6 into symnext; sm.w is free until the weights
+            // are decoded), then expanded to sym | nb << 8 | base << 16
+            build_seq_fse_g(sm.symnext, sm.norm, maxsym, al, sm.w, sm.w + 128, sm.symat);
+            if (l < (1 << al)) {
+                const uint32_t v = sm.symnext[l], ns = v >> 6;
+                const int nb = al - (31 - __builtin_clz(ns));
+                sm.fse[l] = (v & 63u) | ((uint32_t)nb << 8) | (((ns << nb) - (1u << al)) << 16);
+            }
         }
         __builtin_amdgcn_wave_barrier();
 #else
@@ -2671,9 +2678,18 @@ __device__ __forceinline__ void seq_group2(SeqSmem &sm, int gn, uint32_t *e0, ui
     uint32_t r0 = SYMB | (0u << 29), r1 = SYMB | (1u << 29), r2 = SYMB | (2u << 29);
     uint32_t brep = 0;
     zdecode(sm, gn, r0, r1, r2, brep);
+    bool lost = false;
     if (wait_carry) {  // the second half of a split input: entry offsets from the first half
-        while (__hip_atomic_load(wait_carry + 3, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+        // Forward progress (see the zseqb launch): the first half never waits
+        // on anything, so this wait ends.  Should that ever break, the wait
+        // gives up after ~2^22 sleeps (~1 s) and the input fails with E_BUG
+        // (an IT_ERR item where its first block's entry state would go)
+        // instead of hanging the GPU.
+        for (uint32_t spins = 0;
+             __hip_atomic_load(wait_carry + 3, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0u; ++spins) {
+            if (spins > (1u << 22)) { lost = true; break; }
             __builtin_amdgcn_s_sleep(8);
+        }
         *e0 = __hip_atomic_load(wait_carry + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         *e1 = __hip_atomic_load(wait_carry + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         *e2 = __hip_atomic_load(wait_carry + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2684,7 +2700,11 @@ __device__ __forceinline__ void seq_group2(SeqSmem &sm, int gn, uint32_t *e0, ui
         g_u4 *ib = sm.g[gi].ib;
         if (al >> 24) { *e0 = 1; *e1 = 4; *e2 = 8; }
         const uint32_t x0 = readlane(r0, gi), x1 = readlane(r1, gi), x2 = readlane(r2, gi);
-        if (readlane(brep, gi) && l == 0) ib[item + 1] = make_uint4(*e0, *e1, *e2, IT_BREP);
+        if (lost && gi == 0) {
+            if (l == 0) ib[item + 1] = make_uint4(0, 0, (uint32_t)E_BUG, IT_ERR);
+        } else if (readlane(brep, gi) && l == 0) {
+            ib[item + 1] = make_uint4(*e0, *e1, *e2, IT_BREP);
+        }
         const uint32_t n0 = rep_res(x0, *e0, *e1, *e2), n1 = rep_res(x1, *e0, *e1, *e2), n2 = rep_res(x2, *e0, *e1, *e2);
         *e0 = n0; *e1 = n1; *e2 = n2;
     }
@@ -3942,6 +3962,13 @@ int launch_entropy_exec(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret,
     if (hipGetLastError() != hipSuccess) return -1;
 #endif
 #if JFS_ZSEQ_HALF
+    // Workgroup 2 bi decodes input bi's blocks [0, ZNB) and never waits on
+    // anything; 2 bi + 1 decodes the rest and, at its first phase C, waits for
+    // the repeat offsets 2 bi publishes.  Only second halves wait, and only on
+    // first halves, which always run to completion once dispatched: with the
+    // round-robin XCD dispatch the first halves even land on other XCDs than
+    // the waiting second halves, so those cannot crowd them out.  The wait is
+    // bounded anyway (seq_group2).
     static_assert(ZSEQ_INPUTS == 1, "split inputs: one input per workgroup pair");
     hipLaunchKernelGGL(zseqb_kernel, dim3(2 * nblk), dim3(128), 0, stream, d_blocks, nblk, d_info, d_tabs, d_items);
 #else

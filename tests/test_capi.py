@@ -10,10 +10,20 @@ from juicefs_amd import _lib as L
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def header_functions():
-    src = open(os.path.join(ROOT, "include", "jfs_gpucodec.h")).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(jfs_[a-z0-9_]+)\s*\(", src)))
+def header_functions(names=("jfs_gpucodec.h", "jfs_gpucodec_test.h")):
+    """Functions the public header (and the test-hook header) declare."""
+    out = set()
+    for h in names:
+        src = open(os.path.join(ROOT, "include", h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        out |= set(re.findall(r"\b(jfs_[a-z0-9_]+)\s*\(", src))
+    return sorted(out)
+
+
+def test_test_hooks_not_in_public_header():
+    # ADVICE r5: the lock-order test hook is not part of the drop-in ABI
+    assert "jfs_test_spread_locking" not in header_functions(("jfs_gpucodec.h",))
+    assert header_functions(("jfs_gpucodec_test.h",)) == ["jfs_test_spread_locking"]
 
 
 def test_exports_every_header_symbol(lib):

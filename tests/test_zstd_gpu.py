@@ -262,3 +262,61 @@ def test_zstd_literal_pairs_corrupt_vs_oracle(gpu, golden, frames_bin, oracle):
         assert x == wr, (i % len(variants), wr, x)
         if x >= 0:
             assert o == wo
+
+
+def _bits_le(fields):
+    """LSB-first bit packing of (value, nbits) fields into bytes."""
+    acc, n, out = 0, 0, bytearray()
+    for v, nb in fields:
+        acc |= (v & ((1 << nb) - 1)) << n
+        n += nb
+    while n > 0:
+        out.append(acc & 0xFF)
+        acc >>= 8
+        n -= 8
+    return bytes(out)
+
+
+def _frame_weight_symbol(sym_hi, regen=100):
+    """One-block frame whose literals are Huffman-compressed with FSE-coded
+    weights, the weights' table description (RFC 8878 4.1.1, accuracy log 5)
+    counting symbol 0 once and symbol `sym_hi` 31 times: every decoded weight
+    is sym_hi, a corrupt description (symbols >= 64 must take the
+    serial table build, like libzstd and the oracle)."""
+    zeros = sym_hi - 2  # zero-count symbols after symbol 1's zero (repeat flags)
+    f = [(0, 4), (2, 5), (1, 5)]  # AL - 5; symbol 0: count 1 (v=2); symbol 1: count 0 (v=1)
+    while zeros >= 3:
+        f.append((3, 2))
+        zeros -= 3
+    f.append((zeros, 2))
+    f.append((63, 6))  # symbol sym_hi: count 31 (v=32 >= max=31: 6 bits, x - max = 32)
+    ncount = _bits_le(f)
+    wstream = bytes([0x5A, 0xA5, 0x33, 0x81])
+    hb = len(ncount) + len(wstream)
+    huf = bytes([hb]) + ncount + wstream
+    stream = bytes([0x3C, 0x99, 0x17, 0x80])
+    csize = len(huf) + len(stream)
+    # literals header, Compressed, size format 00 (one stream, 10-bit sizes)
+    h = 2 | (0 << 2) | ((regen & 0xF) << 4) | ((regen >> 4) << 8) | (csize << 14)
+    lit = bytes([h & 0xFF, (h >> 8) & 0xFF, (h >> 16) & 0xFF]) + huf + stream
+    body = lit + bytes([0])  # no sequences
+    bh = 1 | (2 << 1) | (len(body) << 3)
+    blk = bytes([bh & 0xFF, (bh >> 8) & 0xFF, (bh >> 16) & 0xFF]) + body
+    return bytes([0x28, 0xB5, 0x2F, 0xFD, 0x20, regen]) + blk
+
+
+@pytest.mark.parametrize("nb", [3, 140])
+def test_zstd_huffman_weight_symbol_ge64_vs_oracle(gpu, oracle, nb):
+    """A Huffman weight description that counts FSE symbols 64 / 100 / 255
+    (and 40 / 63, the lane-parallel builder's range) decodes to the oracle's
+    result on the small-batch (3 inputs) and the large-batch (140) paths."""
+    frames = [_frame_weight_symbol(s) for s in (40, 63, 64, 100, 255)]
+    want = [oracle.zstd_decompress(f, 100) for f in frames]
+    assert all(w[0] < 0 for w in want[2:]), want  # the oracle rejects them
+    srcs = [frames[i % len(frames)] for i in range(nb)]
+    r, outs = run_device(srcs, [100] * nb, gpu)
+    for i, (x, o) in enumerate(zip(r, outs)):
+        wr, wo = want[i % len(frames)]
+        assert x == wr, (i % len(frames), wr, x)
+        if x >= 0:
+            assert o == wo
