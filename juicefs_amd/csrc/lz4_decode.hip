@@ -34,55 +34,34 @@
 namespace jfs {
 namespace lz4d {
 
-#ifndef JFS_LZ4_P
-#define JFS_LZ4_P 32
-#endif
-constexpr int P = JFS_LZ4_P;           // bytes per lane piece (visited set = one u64)
-static_assert(P <= 64, "visited set is one u64");
+// Tuning: every value below was measured against its alternatives (DESIGN.md
+// 3, 6b-6d); the superseded variants live in the history, not in this file.
+constexpr int P = 32;                  // window bytes per lane of the token table
 constexpr int CW = 64 * P;             // compressed window bytes handled per pass
 constexpr int CWIN = CW + 80;          // LDS staging incl. lookahead (multiple of 16)
-#ifndef JFS_LZ4_RING
-#define JFS_LZ4_RING 4096
-#endif
-constexpr int R = JFS_LZ4_RING;        // output ring bytes (power of two)
+constexpr int R = 4096;                // output ring bytes (power of two)
 constexpr int RMASK = R - 1;
-#ifndef JFS_LZ4_OV
-#define JFS_LZ4_OV 32
-#endif
-#ifndef JFS_LZ4_DP
-#define JFS_LZ4_DP 1  // exit-table parser for windows away from the input end
-#endif
-#ifndef JFS_LZ4_LITSRC
-#define JFS_LZ4_LITSRC 1  // near matches whose source lies in one literal run of the batch join the parallel round
-#endif
-#ifndef JFS_LZ4_SEG
-#define JFS_LZ4_SEG 128  // segment-walk parser (bytes per lane); 0 = per-window exit-table parser
-#endif
-constexpr int SEG = JFS_LZ4_SEG;
-#ifndef JFS_LZ4_SUBST
-#define JFS_LZ4_SUBST 1  // source-substitution hops per batch (with the whole-wave near fallback: 1 = 2 > 3)
-#endif
-#ifndef JFS_LZ4_NEARPM
-#define JFS_LZ4_NEARPM 2  // near readiness: 2 = source wholly before the batch (measured equal to 1 = exact prefix-max rule, and cheaper)
-#endif
-#ifndef JFS_LZ4_NEARSER
-#define JFS_LZ4_NEARSER 1  // near matches: one lane-parallel round, the rest by the whole wave in order
-#endif
-#ifndef JFS_LZ4_LITDIRECT
-#define JFS_LZ4_LITDIRECT 1  // literal runs >= 2R copied HBM to HBM (incompressible data)
-#endif
-#ifndef JFS_LZ4_LITSER
-#define JFS_LZ4_LITSER 0  // 1: literal runs take one 16-byte lane step, longer runs by the whole wave (measured: no gain)
-#endif
-constexpr int OV = JFS_LZ4_OV;           // speculative-walk pre-roll (bytes before the piece)
+constexpr int SEG = 128;               // segment-walk parser: bytes per lane
 constexpr int TMAX = CW / 3 + 2;       // max tokens in a window (interior token >= 3 bytes)
 // Table capacity per window.  Windows with more tokens (only runs of 3..5-byte
 // tokens) end at token TCAP and the next window starts there; the cap keeps the
 // workgroup within 10 KiB of LDS so that 16 blocks (32 waves) fit on a CU.
-#ifndef JFS_LZ4_TCAP
-#define JFS_LZ4_TCAP 448
+constexpr int TCAP = 448 < TMAX ? 448 : TMAX;
+// Diagnostic builds only (timing of phase knock-outs, WRONG output; never in
+// the product .so): -DJFS_DIAG=<mask of D_*>.
+#ifndef JFS_DIAG
+#define JFS_DIAG 0
 #endif
-constexpr int TCAP = JFS_LZ4_TCAP < TMAX ? JFS_LZ4_TCAP : TMAX;
+enum : unsigned {
+    D_SKIP_ZERO = 1,    // no ring zeroing
+    D_SKIP_LIT = 2,     // no literal copies
+    D_SKIP_FAR = 4,     // no far-match copies
+    D_SKIP_SUBST = 8,   // no source substitution
+    D_SKIP_NEAR = 16,   // no near-match copies
+    D_PARSEONLY = 32,   // the copier skips every window (the parser wave alone)
+    D_NOCOPY = 64,      // parse and batching, no batch copies
+};
+constexpr unsigned DIAG = JFS_DIAG;
 constexpr uint32_t STOP = 0x80000000u;
 constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr int KEXT = 64;               // max 255-extension bytes handled by the fast path
@@ -399,7 +378,7 @@ __device__ __forceinline__ void direct_lit(Smem &s, Ctx &c, int32_t srcpos, int3
 
 __device__ __forceinline__ void coop_lit(Smem &s, Ctx &c, int32_t srcpos, int32_t op, int32_t len) {
     const int l = lane_id();
-    if (JFS_LZ4_LITDIRECT && len >= LIT_DIRECT) {
+    if (len >= LIT_DIRECT) {
         const int32_t body = op + len - R;
         direct_lit(s, c, srcpos, op, body);
         srcpos += body - op;
@@ -454,7 +433,7 @@ __device__ __forceinline__ int32_t direct_fill(Smem &s, Ctx &c, int32_t op, int3
 
 __device__ __forceinline__ void coop_match(Smem &s, Ctx &c, int32_t op, int32_t off, int32_t len) {
     const int l = lane_id();
-    if (JFS_LZ4_LITDIRECT && len >= LIT_DIRECT && off > 0 && off <= 16 && (16 % off) == 0) {
+    if (len >= LIT_DIRECT && off > 0 && off <= 16 && (16 % off) == 0) {
         const int32_t b = direct_fill(s, c, op, off, len);
         len -= b - op;
         op = b;
@@ -704,9 +683,7 @@ __device__ __forceinline__ void batch(Smem &s, Ctx &c, bool act, int32_t o, uint
     const int32_t hz = O1 + 4 - R;
     PCOUNT(14, 1);
     if (O0 - c.F >= FLUSH_T) flush_to_line(s, c, O0);
-#ifndef JFS_SKIP_ZERO
-    zero_span(s, c, O0, O1);
-#endif
+    if constexpr (!(DIAG & D_SKIP_ZERO)) zero_span(s, c, O0, O1);
     const int32_t ms = o + (int32_t)ll, msrc = ms - (int32_t)off;
     const bool hasm = act && ml > 0;
     const bool zero = hasm && off == 0;
@@ -725,34 +702,16 @@ __device__ __forceinline__ void batch(Smem &s, Ctx &c, bool act, int32_t o, uint
         if (far) far_load(c, (uintptr_t)(c.dst + msrc) - fha, fd0, fd1, fd2, fd3, fd4, fd5);
     }
     // literal runs (source: staged window, addressed as ring + R + litr)
-#ifdef JFS_SKIP_LIT
-    if (0)
-#endif
-#if JFS_LZ4_LITSER
-    // one 16-byte step per lane; the rare longer runs finish by the whole wave
-    if (__ballot(act && ll > 0u)) {
-        PCOUNT(16, 1);
-        if (act && ll > 0u) copy16<false>(s, c.cwoff + litr, slot(c, o), ll < 16u ? (int32_t)ll : 16);
-    }
-    for (uint64_t lm = __ballot(act && ll > 16u); lm; lm &= lm - 1) {
-        const int j = (int)__builtin_ctzll(lm);
-        wave_lit(s, c, (int32_t)readlane((uint32_t)o, j), readlane(litr, j), 16, (int32_t)readlane(ll, j));
-    }
-#else
-    for (uint32_t k = 0; __ballot(act && k < ll); k += 16) {
+    for (uint32_t k = 0; !(DIAG & D_SKIP_LIT) && __ballot(act && k < ll); k += 16) {
         PCOUNT(16, 1);
         if (act && k < ll) {
             const int32_t m = ll - k < 16u ? (int32_t)(ll - k) : 16;
             copy16<false>(s, c.cwoff + litr + k, slot(c, o + (int32_t)k), m);
         }
     }
-#endif
     PSTAMP(4);
     // far matches (offset-0 matches write zeros: the span is already zero)
-#ifdef JFS_SKIP_FAR
-    if (0)
-#endif
-    if (__ballot(far)) {
+    if (!(DIAG & D_SKIP_FAR) && __ballot(far)) {
         for (uint32_t k = 0; __ballot(far && k < ml); k += 16) {
             PCOUNT(17, 1);
             if (far && k < ml) {
@@ -781,14 +740,10 @@ __device__ __forceinline__ void batch(Smem &s, Ctx &c, bool act, int32_t o, uint
     const uint32_t key = act ? (uint32_t)ms : (lane_id() < first ? 0u : 0xFFFFFFFFu);  // non-decreasing
     bool litsrc = false;  // the source lies wholly inside one literal run of this batch (written above)
     {
+        // one hop (measured: 1 > 2 > 3 hops with the whole-wave tail below)
         const uint32_t mek = pend ? (uint32_t)(ms + (int32_t)ml) : 0u;
-        bool cand = pend && off >= ml;
-#ifdef JFS_SKIP_SUBST
-        if (0)
-#endif
-        for (int it = 0; it < JFS_LZ4_SUBST; ++it) {
-            const bool want = cand && src >= O0;
-            if (!__ballot(want)) break;
+        const bool want = !(DIAG & D_SKIP_SUBST) && pend && off >= ml && src >= O0;
+        if (__ballot(want)) {
             int lo = 0;  // last lane with key <= src
 #pragma unroll
             for (int stp = 32; stp; stp >>= 1) {
@@ -800,51 +755,25 @@ __device__ __forceinline__ void batch(Smem &s, Ctx &c, bool act, int32_t o, uint
             const int32_t voff = __shfl((int)off, lo, 64);
             const bool ok = want && vms <= (uint32_t)src && (uint32_t)(src + (int32_t)ml) <= vme && voff > 0 &&
                             src - voff >= hz;
-#if JFS_LZ4_LITSRC
             // past the end of lane lo's match and before the next lane's match
             // start: inside the next token's literal run, already in the ring
-            if (it == 0) {
-                const uint32_t nms = (uint32_t)__shfl((int)key, lo + 1 < 64 ? lo + 1 : 63, 64);
-                litsrc = want && vms <= (uint32_t)src && (uint32_t)src >= vme && lo < 63 &&
-                         (uint32_t)(src + (int32_t)ml) <= nms;
-            }
-#endif
+            const uint32_t nms = (uint32_t)__shfl((int)key, lo + 1 < 64 ? lo + 1 : 63, 64);
+            litsrc = want && vms <= (uint32_t)src && (uint32_t)src >= vme && lo < 63 &&
+                     (uint32_t)(src + (int32_t)ml) <= nms;
             src = ok ? src - voff : src;
-            cand = ok;
         }
     }
-    // near matches in rounds
+    // near matches: one round in which every ready lane (source wholly before
+    // the batch, or inside one of its literal runs) copies its first (<= 16
+    // byte) step; what is left (lanes whose source waits on a match of this
+    // batch, matches longer than one step) is copied by the whole wave in lane
+    // order, which is output order, so every source is complete when its
+    // lane's turn comes
     int32_t pos = ms, rem = (int32_t)ml, D = ms - src;
     const int32_t send = src + (int32_t)ml < ms ? src + (int32_t)ml : ms;
-#if JFS_LZ4_NEARPM == 1
-    int jl = 0;  // last lane with key < send (jv: such a lane exists)
-#pragma unroll
-    for (int stp = 32; stp; stp >>= 1) {
-        const uint32_t v = (uint32_t)__shfl((int)key, jl + stp, 64);
-        jl = v < (uint32_t)send ? jl + stp : jl;
-    }
-    const bool jv = (uint32_t)__shfl((int)key, jl, 64) < (uint32_t)send;
-#endif
-#if JFS_LZ4_NEARSER
-    // one round: every ready lane copies its first (<= 16 byte) step; what is
-    // left (lanes whose source waits on a match of this batch, matches longer
-    // than one step) is copied by the whole wave in lane order, which is output
-    // order, so every source is complete when its lane's turn comes
-#ifdef JFS_SKIP_NEAR
-    if (0)
-#endif
-    {
+    if (!(DIAG & D_SKIP_NEAR)) {
         PCOUNT(18, 1);
-#if JFS_LZ4_NEARPM == 2
-        const bool go = pend && (send <= O0 || litsrc);  // source wholly before the batch, or in its literals
-#elif JFS_LZ4_NEARPM
-        const uint32_t pm = dpp_scan_max(pend ? (uint32_t)(ms + (int32_t)ml) : 0u);
-        const uint32_t pmj = (uint32_t)__shfl((int)pm, jl, 64);
-        const bool go = pend && (!jv || pmj <= (uint32_t)src);
-#else
-        const int32_t front = (int32_t)dwave_min(pend ? (uint32_t)ms : 0x7FFFFFFFu);
-        const bool go = pend && send <= front;
-#endif
+        const bool go = pend && (send <= O0 || litsrc);
         if (__ballot(go)) {
             PCOUNT(15, 1);
             if (go) {
@@ -862,34 +791,6 @@ __device__ __forceinline__ void batch(Smem &s, Ctx &c, bool act, int32_t o, uint
                       (int32_t)readlane((uint32_t)rem, j));
         }
     }
-    if (0)
-#endif
-    for (int guard = 0; __ballot(pend); ++guard) {
-        if (guard > 64) { c.bug = 5; break; }
-        PCOUNT(18, 1);
-#if JFS_LZ4_NEARPM == 1
-        // ready: no still-pending destination [ms_j, ms_j + ml_j) meets the source
-        // [src, send).  Destinations are disjoint and in lane order, so that is the
-        // prefix max of pending ends at the last lane jl with ms_jl < send.
-        const uint32_t pm = dpp_scan_max(pend ? (uint32_t)(ms + (int32_t)ml) : 0u);
-        const uint32_t pmj = (uint32_t)__shfl((int)pm, jl, 64);
-        bool go = pend && (!jv || pmj <= (uint32_t)src);
-#else
-        const int32_t front = (int32_t)dwave_min(pend ? (uint32_t)ms : 0x7FFFFFFFu);
-        bool go = pend && send <= front;
-#endif
-        while (__ballot(go)) {
-            PCOUNT(15, 1);
-            if (go) {
-                const int32_t m = rem < 16 ? (rem < D ? rem : D) : (D < 16 ? D : 16);
-                copy16<true>(s, slot(c, pos - D), slot(c, pos), m);
-                pos += m;
-                rem -= m;
-                if (m == D && D < 16) D <<= 1;
-                if (rem <= 0) { go = false; pend = false; }
-            }
-        }
-    }
     PSTAMP(6);
 }
 
@@ -902,10 +803,10 @@ __device__ __forceinline__ uint32_t copy_tokens(Smem &s, Ctx &c, uint32_t T, int
     const int l = lane_id();
     int32_t op = op0;
     const int32_t cap = c.cap;
-#ifdef JFS_LZ4_PARSEONLY  // diagnostics: the parser wave alone (the copier skips every window; wrong output)
-    *end_op = op0;
-    return T;
-#endif
+    if constexpr ((DIAG & D_PARSEONLY) != 0) {
+        *end_op = op0;
+        return T;
+    }
     for (uint32_t g0 = 0; g0 < T; g0 += 64) {
         const uint32_t n0 = T - g0 < 64u ? T - g0 : 64u;
         const bool in0 = (uint32_t)l < n0;
@@ -954,9 +855,7 @@ __device__ __forceinline__ uint32_t copy_tokens(Smem &s, Ctx &c, uint32_t T, int
             const bool act = (uint32_t)l >= j && (uint32_t)l < eb;
             const int32_t O1 = (int32_t)readlane((uint32_t)endo, (int)eb - 1);
             PSTAMP(3);
-#ifndef JFS_LZ4_NOCOPY  // diagnostics: parse-only variant (wrong output)
-            batch(s, c, act, o, ll, ml, off, litr, oj, O1 PROF_PASS);
-#endif
+            if constexpr (!(DIAG & D_NOCOPY)) batch(s, c, act, o, ll, ml, off, litr, oj, O1 PROF_PASS);
             j = eb;
         }
         if (bm) {
@@ -970,265 +869,6 @@ __device__ __forceinline__ uint32_t copy_tokens(Smem &s, Ctx &c, uint32_t T, int
     return T;
 }
 
-// next token position after p (or STOP | p), fast path with the exact parse
-// for the rare tokens the window-only parse cannot take
-__device__ __forceinline__ uint32_t step_next(const Smem &s, const Ctx &c, int32_t p, bool act) {
-    const FTok t = parse_fast(s, c, p);
-    uint32_t x = t.stop ? (STOP | (uint32_t)p) : (uint32_t)t.nxt;
-    const bool sl = act && t.slow;
-    if (__ballot(sl)) {
-        if (sl) x = (uint32_t)parse_tok(s, c, p).nxt;
-    }
-    return x;
-}
-
-// Next-token step for windows far from the input end (no end-of-input rule
-// can apply to a token that starts and whose match-length byte lies in the
-// window): two LDS byte reads and a dozen VALU ops.  Tokens with a literal-
-// length extension or a 255 match-length byte take step_next.
-template <bool LEAN>
-__device__ __forceinline__ uint32_t walk_step(const Smem &s, const Ctx &c, int32_t p, bool act) {
-    if (!LEAN) return step_next(s, c, p, act);
-    const int32_t r = p - c.cbase;  // p in [cbase, cbase + CW + OV): r + 17 < CWIN
-    const uint32_t tb = c.cw[r];
-    const uint32_t ll = tb >> 4;
-    const uint32_t e2 = c.cw[r + 3 + (int32_t)ll];
-    const bool mlx = (tb & 15u) == 15u;
-    const bool slow = act && (ll == 15u || (mlx && e2 == 255u));
-    uint32_t x = (uint32_t)(p + 3 + (int32_t)ll + (mlx ? 1 : 0));
-    if (__ballot(slow)) {
-        if (slow) x = step_next(s, c, p, true);
-    }
-    return x;
-}
-
-// Chain of one 32-byte piece: a speculative walk from OV bytes before the
-// piece records the positions it visits; fix-up rounds take the true entry
-// (exit of the previous piece) and walk only until they meet that chain.
-template <bool LEAN>
-__device__ __forceinline__ void piece_chain(Smem &s, Ctx &c, int32_t wbase, int32_t plo, int32_t phi, uint64_t &vt,
-                                            uint32_t &ex PROF_ARG) {
-    const int l = lane_id();
-    // 1. speculative walk of this lane's piece: visited positions + exit
-    // The walk starts OV bytes before the piece (a pre-roll whose positions are
-    // not recorded): by the time it reaches the piece it has usually fallen into
-    // the true chain, so few pieces need a second fix-up round.
-    uint32_t cur = l == 0 ? (uint32_t)wbase : (uint32_t)(plo - OV);
-    uint64_t vs = 0;  // positions the speculative chain visited (bit = position - plo)
-    uint32_t sx = 0;  // its exit: first position >= phi, or STOP | p
-    {
-        int32_t q = (int32_t)cur;
-        bool act = true;
-        for (int guard = 0; __ballot(act); ++guard) {
-            PCOUNT(11, 1);
-            if (act) {
-                const uint32_t x = walk_step<LEAN>(s, c, q, act);
-                if (x & STOP) {
-                    sx = x;
-                    act = false;
-                } else {
-                    if (q >= plo) vs |= 1ull << (uint32_t)(q - plo);
-                    q = (int32_t)x;
-                    if (q >= phi) {
-                        sx = (uint32_t)q;
-                        act = false;
-                    }
-                }
-            }
-            if (guard > P + OV) { c.bug = 6; break; }
-        }
-    }
-    // 2. fix-up: true entry of piece k = exit of piece k-1.  An entry on the
-    //    speculative chain keeps its suffix; otherwise walk from the entry until
-    //    the chain meets the speculative one (or leaves the piece).
-    vt = vs;  // true chain positions in this piece
-    ex = sx;  // true exit
-    for (int r = 0;; ++r) {
-        const uint32_t In = dpp_shift_up(ex, (uint32_t)wbase);
-        const bool ch = In != cur;
-        if (!__ballot(ch)) break;
-        if (r > 64) { c.bug = 3; break; }
-        PCOUNT(12, 1);
-        bool part = false;
-        if (ch) {
-            cur = In;
-            if ((In & STOP) || (int32_t)In >= phi) {
-                vt = 0;
-                ex = In;
-            } else {
-                const uint32_t d = In - (uint32_t)plo;
-                if ((vs >> d) & 1ull) {
-                    vt = vs & (~0ull << d);
-                    ex = sx;
-                } else {
-                    part = true;
-                }
-            }
-        }
-        int32_t q = (int32_t)In;
-        uint64_t vp = 0;
-        for (int guard = 0; __ballot(part); ++guard) {
-            PCOUNT(13, 1);
-            if (part) {
-                const uint32_t d = (uint32_t)(q - plo);
-                if ((vs >> d) & 1ull) {  // joined the speculative chain
-                    vt = vp | (vs & (~0ull << d));
-                    ex = sx;
-                    part = false;
-                } else {
-                    const uint32_t x = walk_step<LEAN>(s, c, q, part);
-                    if (x & STOP) {
-                        vt = vp;
-                        ex = x;
-                        part = false;
-                    } else {
-                        vp |= 1ull << d;
-                        q = (int32_t)x;
-                        if (q >= phi) {
-                            vt = vp;
-                            ex = (uint32_t)q;
-                            part = false;
-                        }
-                    }
-                }
-            }
-            if (guard > P) { c.bug = 7; break; }
-        }
-    }
-}
-
-#if JFS_LZ4_DP
-__device__ __forceinline__ uint32_t pick2(uint32_t a, uint32_t b, uint32_t m) { return a ^ ((a ^ b) & m); }
-
-// Exit table of one 32-byte piece, built backwards over its offsets i:
-//   XT byte i = offset of the first position >= 32 on the chain from i
-//   (3..49), or 255 when that chain meets a token the lean step cannot take.
-// Bytes come from the staged window (two LDS byte reads per offset); the
-// table lives in 8 VGPRs, indexed only with compile-time dword numbers
-// (mask selects, so it stays in registers).
-template <int I>
-__device__ __forceinline__ void dp_step(const uint8_t *pc, int32_t lim, uint32_t (&XT)[8]) {
-    if constexpr (I >= 0) {
-        const uint32_t tb = pc[I], e1 = pc[I + 1];
-        const uint32_t ll = tb >> 4;
-        // 0/1 integers combined with bitwise ops: short-circuit && / || here
-        // compiled to exec-mask branches (and SGPR spills) in every step
-        const uint32_t llx = (uint32_t)(ll == 15u);
-        // q: offset of the first match-length extension byte (after the offset)
-        const uint32_t q = (uint32_t)I + 3u + (llx ? 16u + e1 : ll);
-        const uint32_t oob = (uint32_t)((int32_t)q >= lim);  // not staged: exact walk
-        const uint32_t e2 = pc[oob ? 0u : q];
-        const uint32_t mlx = (uint32_t)((tb & 15u) == 15u);
-        const uint32_t nx = q + mlx;
-        // long literal runs land past the piece (else: exact walk)
-        const uint32_t slow = (llx & ((uint32_t)(e1 == 255u) | (uint32_t)(nx < 32u))) | oob |
-                              (mlx & (uint32_t)(e2 == 255u));
-        uint32_t xi = nx;
-        if constexpr (I + 3 < 32) {
-            constexpr int bq = (I + 3) >> 2;
-            const uint32_t kx = (nx >> 2) - (uint32_t)bq;  // 0..4 when nx < 32 and !llx
-            uint32_t xw = XT[bq];
-            if constexpr (bq + 1 < 8) xw = pick2(xw, XT[bq + 1], 0u - (uint32_t)(kx == 1));
-            if constexpr (bq + 2 < 8) xw = pick2(xw, XT[bq + 2], 0u - (uint32_t)(kx == 2));
-            if constexpr (bq + 3 < 8) xw = pick2(xw, XT[bq + 3], 0u - (uint32_t)(kx == 3));
-            if constexpr (bq + 4 < 8) xw = pick2(xw, XT[bq + 4], 0u - (uint32_t)(kx == 4));
-            const uint32_t xj = (xw >> (8u * (nx & 3u))) & 0xFFu;
-            xi = nx >= 32u ? nx : xj;
-        }
-        xi = slow || xi > 254u ? 255u : xi;
-        XT[I >> 2] |= xi << (8 * (I & 3));
-        dp_step<I - 1>(pc, lim, XT);
-    }
-}
-
-__device__ __forceinline__ uint32_t byte_of8(const uint32_t (&V)[8], uint32_t i) {
-    const uint32_t d = i >> 2;
-    const uint32_t m0 = 0u - (d & 1u), m1 = 0u - ((d >> 1) & 1u), m2 = 0u - ((d >> 2) & 1u);
-    const uint32_t ab = pick2(pick2(V[0], V[1], m0), pick2(V[2], V[3], m0), m1);
-    const uint32_t ce = pick2(pick2(V[4], V[5], m0), pick2(V[6], V[7], m0), m1);
-    return (pick2(ab, ce, m2) >> (8u * (i & 3u))) & 0xFFu;
-}
-
-// Chain of one 32-byte piece (lean windows) from the exit table: fix-up rounds
-// are one register lookup per lane (an exact walk for table entries 255), then
-// one walk from the true entry records the chain positions.
-__device__ __forceinline__ void table_chain(Smem &s, Ctx &c, int32_t wbase, int32_t plo, int32_t phi, uint64_t &vt,
-                                            uint32_t &ex PROF_ARG) {
-    const int l = lane_id();
-    uint32_t XT[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    dp_step<31>(c.cw + l * P, CWIN - 1 - l * P, XT);
-    uint32_t Ea = l == 0 ? (uint32_t)wbase : (uint32_t)plo;
-    uint32_t cur = 0xFFFFFFFFu;
-    ex = 0;
-    for (int r = 0;; ++r) {
-        const bool ch = Ea != cur;
-        if (!__ballot(ch)) break;
-        if (r > 70) { c.bug = 3; break; }
-        PCOUNT(12, 1);
-        cur = Ea;
-        bool walk = false;
-        if (ch) {
-            if ((Ea & STOP) || (int32_t)Ea >= phi) {
-                ex = Ea;
-            } else {
-                const uint32_t x = byte_of8(XT, Ea - (uint32_t)plo);
-                if (x == 255u) walk = true;
-                else ex = (uint32_t)plo + x;
-            }
-        }
-        if (__ballot(walk)) {
-            // exact step over the token the table cannot take, then back to the table
-            int32_t q = (int32_t)Ea;
-            for (int g = 0; __ballot(walk); ++g) {
-                PCOUNT(13, 1);
-                if (walk) {
-                    const uint32_t x = walk_step<true>(s, c, q, walk);
-                    if (x & STOP) {
-                        ex = x;
-                        walk = false;
-                    } else {
-                        q = (int32_t)x;
-                        if (q >= phi) {
-                            ex = (uint32_t)q;
-                            walk = false;
-                        } else {
-                            const uint32_t y = byte_of8(XT, (uint32_t)(q - plo));
-                            if (y != 255u) {
-                                ex = (uint32_t)plo + y;
-                                walk = false;
-                            }
-                        }
-                    }
-                }
-                if (g > P) { c.bug = 7; break; }
-            }
-        }
-        Ea = dpp_shift_up(ex, (uint32_t)wbase);
-    }
-    // true chain positions in the piece
-    vt = 0;
-    {
-        int32_t q = (int32_t)cur;
-        bool act = !(cur & STOP) && q < phi;
-        for (int g = 0; __ballot(act); ++g) {
-            PCOUNT(11, 1);
-            if (act) {
-                const uint32_t x = walk_step<true>(s, c, q, act);
-                if (x & STOP) {  // a stop token ends the chain (it is not a token)
-                    act = false;
-                } else {
-                    vt |= 1ull << (uint32_t)(q - plo);
-                    if ((int32_t)x >= phi) act = false;
-                    else q = (int32_t)x;
-                }
-            }
-            if (g > P) { c.bug = 9; break; }
-        }
-    }
-}
-#endif
-
-#if JFS_LZ4_SEG
 // ---------------------------------------------------------------------------
 // segment-walk parser (round 3): the token chain of a span of SW = 64 * SEG
 // compressed bytes at once, one SEG-byte segment per lane, read straight from
@@ -1242,18 +882,9 @@ __device__ __forceinline__ void table_chain(Smem &s, Ctx &c, int32_t wbase, int3
 // ---------------------------------------------------------------------------
 static_assert(SEG == 128, "segment bit sets are two u64 per lane");
 constexpr int SW = 64 * SEG;
-#ifndef JFS_LZ4_SPRE
-#define JFS_LZ4_SPRE 32
-#endif
-constexpr int SPRE = JFS_LZ4_SPRE;
-#ifndef JFS_LZ4_SEG_BUDGET
-#define JFS_LZ4_SEG_BUDGET 64  // at most this many walk steps of the next span per window
-#endif
-#ifndef JFS_LZ4_SEG_MIN
-#define JFS_LZ4_SEG_MIN 4  // at least this many (more while the copier is busy)
-#endif
-constexpr int SEG_MIN = JFS_LZ4_SEG_MIN;
-constexpr int SEG_BUDGET = JFS_LZ4_SEG_BUDGET;
+constexpr int SPRE = 32;         // speculative pre-roll before each segment (16 / 48 measured no better)
+constexpr int SEG_BUDGET = 64;   // at most this many walk steps of the next span per window
+constexpr int SEG_MIN = 4;       // at least this many (more while the copier is busy)
 
 // Next token position after p (or STOP | p): the exact chain rule of
 // parse_tok, bytes from HBM.
@@ -1449,59 +1080,7 @@ __device__ __forceinline__ uint32_t span_dword(uint64_t vt0, uint64_t vt1, int32
     const uint32_t v = j == 0 ? d0 : j == 1 ? d1 : j == 2 ? d2 : d3;
     return (k >= 0 && k < 4 * 64) ? v : 0u;
 }
-#endif
 
-// ---------------------------------------------------------------------------
-// parser wave: stage one window, find its true token chain, write the table
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ void parse_window(Smem &s, Ctx &c, int32_t wbase, uint32_t *T_out,
-                                             uint32_t *efin_out PROF_ARG) {
-    const int l = lane_id();
-    stage_window(s, c, wbase);
-    const int32_t cbase = c.cbase;
-    PCOUNT(10, 1);
-    __builtin_amdgcn_wave_barrier();
-    PSTAMP(0);
-
-    const int32_t plo = cbase + l * P, phi = plo + P;
-    uint64_t vt;  // true chain positions in this piece (bit = position - plo)
-    uint32_t ex;  // true exit: first position >= phi, or STOP | p
-#if JFS_LZ4_DP
-    if (cbase + CWIN + 400 < c.n) table_chain(s, c, wbase, plo, phi, vt, ex PROF_PASS);
-    else if (cbase + CWIN + 32 < c.n) piece_chain<true>(s, c, wbase, plo, phi, vt, ex PROF_PASS);
-#else
-    if (cbase + CWIN + 32 < c.n) piece_chain<true>(s, c, wbase, plo, phi, vt, ex PROF_PASS);
-#endif
-    else piece_chain<false>(s, c, wbase, plo, phi, vt, ex PROF_PASS);
-    *efin_out = readlane(ex, 63);
-    PSTAMP(1);
-
-    // 3. token table: positions (relative to cbase) in stream order
-    const uint32_t cnt = (uint32_t)__builtin_popcountll(vt);
-    const uint32_t cinc = dpp_scan_add(cnt);
-    const uint32_t tall = readlane(cinc, 63);
-    *T_out = tall < (uint32_t)TCAP ? tall : (uint32_t)TCAP;
-    {
-        uint32_t idx = cinc - cnt;
-        uint64_t v = vt;
-        while (__ballot(v != 0)) {
-            if (v) {
-                const uint32_t b = (uint32_t)__builtin_ctzll(v);
-                if (idx < (uint32_t)TCAP) c.tab[idx] = (uint16_t)((uint32_t)l * P + b);
-                else if (idx == (uint32_t)TCAP) ex = (uint32_t)plo + b;  // first token left to the next window
-                idx++;
-                v &= v - 1;
-            }
-        }
-    }
-    if (tall > (uint32_t)TCAP) {  // the window ends at token TCAP
-        const uint64_t hit = __ballot(cinc - cnt <= (uint32_t)TCAP && (uint32_t)TCAP < cinc);
-        *efin_out = readlane(ex, (int)__builtin_ctzll(hit));
-    }
-    PSTAMP(2);
-}
-
-#if JFS_LZ4_SEG
 // The chain of one span (seg_chain), kept by the parser wave across windows.
 struct Span {
     uint64_t v0, v1;  // this lane's segment bits
@@ -1573,7 +1152,6 @@ __device__ __forceinline__ void parse_window_seg(Smem &s, Ctx &c, int32_t wbase,
     }
     PSTAMP(2);
 }
-#endif
 
 // LDS-only workgroup barrier between the parser and copier waves
 __device__ __forceinline__ void wg_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
@@ -1593,7 +1171,6 @@ __device__ __forceinline__ void use_buffer(Smem &s, Ctx &c, int buf) {
 __device__ __forceinline__ void parser_wave(Smem &s, Ctx &c PROF_ARG) {
     int32_t pip = 0;
     bool pstop = false;
-#if JFS_LZ4_SEG
     Span sp;
     sp.v0 = sp.v1 = 0;
     sp.base = 0;
@@ -1602,7 +1179,6 @@ __device__ __forceinline__ void parser_wave(Smem &s, Ctx &c PROF_ARG) {
     bool nxt = false;  // wk walks the span that follows sp
     SegWalk wk;
     wk.start(0);
-#endif
     for (uint32_t k = 0;; ++k) {
         const int buf = (int)(k & 1u);
         Meta m;
@@ -1615,7 +1191,6 @@ __device__ __forceinline__ void parser_wave(Smem &s, Ctx &c PROF_ARG) {
             if (pip < c.n - 64) {
                 use_buffer(s, c, buf);
                 uint32_t T, efin;
-#if JFS_LZ4_SEG
                 if (!spv || pip >= sp.base + SW) {
                     // the span at pip: the walk started ahead of time, or a fresh one
                     if (!(spv && nxt && wk.base == pip)) wk.start(pip);
@@ -1641,9 +1216,6 @@ __device__ __forceinline__ void parser_wave(Smem &s, Ctx &c PROF_ARG) {
                     }
                 }
                 PSTAMP(1);
-#else
-                parse_window(s, c, pip, &T, &efin PROF_PASS);
-#endif
                 m.kind = c.bug ? W_BUG : W_WIN;
                 m.cbase = c.cbase;
                 m.T = T;
@@ -1665,21 +1237,14 @@ __device__ __forceinline__ void parser_wave(Smem &s, Ctx &c PROF_ARG) {
         if (restart) {
             pip = rip;
             pstop = false;
-#if JFS_LZ4_SEG
             spv = false;
             nxt = false;
-#endif
         }
     }
 }
 
-#ifndef JFS_LZ4_CPRIO
-#define JFS_LZ4_CPRIO 1  // s_setprio of the copier wave (the critical one of the pair)
-#endif
 __device__ __forceinline__ void copier_wave(Smem &s, Ctx &c, int32_t *retp PROF_ARG) {
-#if JFS_LZ4_CPRIO
-    __builtin_amdgcn_s_setprio(JFS_LZ4_CPRIO);
-#endif
+    __builtin_amdgcn_s_setprio(1);  // the copier is the critical wave of the pair (2 / 3: no better)
     Ser st;
     st.ip = 0;
     st.op = 0;
@@ -1767,10 +1332,7 @@ __device__ __forceinline__ void copier_wave(Smem &s, Ctx &c, int32_t *retp PROF_
 // resident at once only with <= 64 VGPRs, <= 10 KiB of LDS and <= 80 SGPRs
 // (above 80 the CU admits 7 waves per SIMD, above 96 six).  The SGPR cap
 // costs some SGPR spills to VGPR lanes and buys 16% (measured: 229 -> 267 GiB/s).
-#ifndef JFS_LZ4_NSGPR
-#define JFS_LZ4_NSGPR 80
-#endif
-#define JFS_LZ4_ATTR __attribute__((amdgpu_num_sgpr(JFS_LZ4_NSGPR), amdgpu_waves_per_eu(8)))
+#define JFS_LZ4_ATTR __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8)))
 // lens (optional): per-block input lengths produced on the device by the
 // previous kernel of a fused chain (AES-GCM open); < 0 = that step failed.
 // todo (optional): only the blocks with todo[b] != 0 are decoded (the others
