@@ -1,21 +1,28 @@
 // Zstd frame decoder for gfx950 (RFC 8878; behaviour of ZSTD_decompress as
 // reached from pkg/compress/compress.go:94-103 via DataDog/zstd v1.5.6).
 //
-// Three launches per batch of inputs (one jfs_dev_block = one input buffer,
-// which may hold several frames):
+// Kernels per batch of inputs (one jfs_dev_block = one input buffer, which
+// may hold several frames):
 //
-//  1. zscan     one lane per input walks frame/block/literal/sequence headers
-//               and sizes the scratch exactly (literal bytes, item count).
-//  2. zlit     one wave per input decodes literal sections (Huffman 4
-//               streams on 4 lanes, raw, RLE) into the literal buffer.
-//     zseq     one wave per input walks the headers, builds each compressed
-//               block's FSE tables, then decodes up to 64 blocks' sequence
-//               streams at once (one lane per block) into a flat item list;
-//               repeat offsets are tracked symbolically per block and the
-//               block entry states resolved in order afterwards.
-//  3. zexec     one wave per input replays the items (literal copy + match
-//               copy) through an 8 KiB LDS output ring, streams the output to
-//               HBM, checks content size / checksum, and writes the result.
+//  zscan / zplan  one lane per input walks frame/block/literal/sequence
+//                 headers and sizes the scratch exactly; device-side scans
+//                 place every input's literal, table and item ranges.
+//  zlit           one wave per input decodes the literal sections (Huffman 4
+//                 streams, two blocks at a time; raw, RLE) into the literal
+//                 buffer.
+//  zseqa          one wave per input walks the block headers and parks each
+//                 compressed block's FSE table descriptions and descriptor.
+//  zbuild         one wave per table spreads the FSE tables (position-parallel).
+//  zseqb          two workgroups per input (blocks [0, ZNB) and the rest), two
+//                 waves each: a decoder wave decodes ZNB blocks' sequence
+//                 streams at once (one lane per block) from LDS, a mover wave
+//                 keeps their bitstream rings filled; repeat offsets are
+//                 symbolic per block and resolved in block order (phase C).
+//  zexec          one wave per input replays the items (literal copy + match
+//                 copy) through an 8 KiB LDS output ring, streams the output
+//                 to HBM, checks content size / checksum, writes the result.
+// Batches of at most JFS_ZSTD_SPLIT_MAX inputs take the block-parallel path of
+// zstd_split.inc instead (same items, origin-map replay).
 //
 // Items are 16 bytes {x, y, z, kind}; errors found by the entropy waves are
 // placed in stream order so zexec reports the first error libzstd would.
@@ -369,18 +376,6 @@ __device__ __forceinline__ void br_refill(BR &r) {
     }
 }
 
-// read n (0..32) bits MSB-first
-__device__ __forceinline__ uint32_t br_read(BR &r, int n) {
-    if (n == 0) return 0u;
-    int32_t lo = r.left - n;
-    uint64_t v64 = r.c >> (uint32_t)(lo - 8 * r.cb);
-    uint32_t v = (uint32_t)v64 & (uint32_t)(0xFFFFFFFFull >> (32 - n));
-    int32_t d = 8 * r.m - lo;
-    if (d > 0) v = d >= n ? 0u : v & ~((1u << d) - 1u);
-    r.left = lo;
-    br_refill(r);
-    return v;
-}
 __device__ __forceinline__ uint32_t br_peek(const BR &r, int n) {
     int32_t lo = r.left - n;
     uint32_t v = (uint32_t)(r.c >> (uint32_t)(lo - 8 * r.cb)) & ((1u << n) - 1u);
@@ -388,84 +383,7 @@ __device__ __forceinline__ uint32_t br_peek(const BR &r, int n) {
     if (d > 0) v = d >= n ? 0u : v & ~((1u << d) - 1u);
     return v;
 }
-__device__ __forceinline__ void br_skip(BR &r, int n) {
-    r.left -= n;
-    br_refill(r);
-}
-__device__ __forceinline__ bool br_overflow(const BR &r) { return r.left < 8 * r.m; }
 __device__ __forceinline__ bool br_done(const BR &r) { return r.left == 8 * r.m; }
-
-// Wave-uniform backward reader staged through a 2 KiB LDS ring (two 1 KiB
-// chunks; chunk k = bytes [1024k, 1024k+1024) relative to b16).  The chunk
-// below the resident pair is prefetched into registers (16 B per lane) and
-// stored when the reader enters the lower resident chunk, so the only
-// vector-memory wait is once per KiB of stream.
-constexpr int SCH = 1024;
-struct SBR {
-    uint8_t *ring;  // LDS, 2 * SCH bytes
-    const gc_u4 *b16;
-    int32_t m, lowk, left, cb, lo;  // lo: lower resident chunk
-    uint64_t c;
-    uint4 pf;                       // this lane's 16 B of chunk lo - 1
-};
-__device__ __forceinline__ uint4 sbr_ld(const SBR &r, int32_t chunk) {
-    int32_t k = chunk * (SCH / 16) + lane_id();  // 16-byte block index
-    if (k < r.lowk) return make_uint4(0, 0, 0, 0);
-    return r.b16[k];
-}
-__device__ __forceinline__ void sbr_put(SBR &r, int32_t chunk, const uint4 &v) {
-    *(uint4 *)(r.ring + ((chunk * SCH + 16 * lane_id()) & (2 * SCH - 1))) = v;
-}
-__device__ __forceinline__ uint32_t sbr_dw(const SBR &r, int32_t q) {  // dword at q (q % 4 == 0), uniform
-    return uniform(*(const uint32_t *)(r.ring + (q & (2 * SCH - 1))));
-}
-__device__ __forceinline__ bool sbr_init(SBR &r, uint8_t *ring, const gc_u8 *in, const gc_u8 *p, int32_t size) {
-    uintptr_t a = (uintptr_t)p;
-    r.ring = ring;
-    r.b16 = (const gc_u4 *)(a & ~(uintptr_t)15);
-    r.m = (int32_t)(a & 15);
-    r.lowk = -(int32_t)((((uintptr_t)r.b16) - (((uintptr_t)in) & ~(uintptr_t)15)) >> 4);
-    if (size <= 0) return false;
-    int32_t top = r.m + size;
-    uint32_t last = ((const gc_u8 *)r.b16)[top - 1];
-    if (last == 0) return false;
-    int hb = 31 - __builtin_clz(last);
-    r.left = 8 * (top - 1) + hb;
-    r.cb = ((top - 1) & ~3) - 4;
-    int32_t kt = (r.cb + 4) >> 10;  // chunk holding the container's top dword
-    r.lo = kt - 1;
-    uint4 a0 = sbr_ld(r, kt), a1 = sbr_ld(r, kt - 1);
-    r.pf = sbr_ld(r, kt - 2);
-    sbr_put(r, kt, a0);
-    sbr_put(r, kt - 1, a1);
-    __builtin_amdgcn_wave_barrier();
-    r.c = ((uint64_t)sbr_dw(r, r.cb + 4) << 32) | sbr_dw(r, r.cb);
-    return true;
-}
-__device__ __forceinline__ void sbr_refill(SBR &r) {
-    if (r.left - 8 * r.cb >= 32) return;
-    int32_t nb = r.cb - 4;
-    if (nb < (r.lo + 1) * SCH) {  // entering the lower resident chunk: rotate
-        sbr_put(r, r.lo - 1, r.pf);
-        r.lo--;
-        r.pf = sbr_ld(r, r.lo - 1);
-        __builtin_amdgcn_wave_barrier();
-    }
-    r.c = (r.c << 32) | sbr_dw(r, nb);
-    r.cb = nb;
-}
-__device__ __forceinline__ uint32_t sbr_read(SBR &r, int n) {
-    if (n == 0) return 0u;
-    int32_t lo = r.left - n;
-    uint32_t v = (uint32_t)(r.c >> (uint32_t)(lo - 8 * r.cb)) & (uint32_t)(0xFFFFFFFFull >> (32 - n));
-    int32_t d = 8 * r.m - lo;
-    if (d > 0) v = d >= n ? 0u : v & ~((1u << d) - 1u);
-    r.left = lo;
-    sbr_refill(r);
-    return v;
-}
-__device__ __forceinline__ bool sbr_overflow(const SBR &r) { return r.left < 8 * r.m; }
-__device__ __forceinline__ bool sbr_done(const SBR &r) { return r.left == 8 * r.m; }
 
 // ---------------------------------------------------------------------------
 // FSE tables (LDS, one u32 per cell: sym | nb << 8 | base << 16)
@@ -568,82 +486,6 @@ __device__ __forceinline__ int32_t build_fse(uint32_t *t, const int16_t *norm, i
         __builtin_amdgcn_wave_barrier();
     }
     return 0;
-}
-
-__device__ __forceinline__ void build_rle(uint32_t *t, uint32_t sym) {
-    if (lane_id() == 0) t[0] = sym;
-}
-
-// value base / extra bits of a sequence code (which: 0 LL, 1 OF, 2 ML)
-__device__ __forceinline__ uint2 seq_code(int which, uint32_t sym) {
-    if (which == 1) return make_uint2(1u << sym, sym);
-    if (which == 0) return make_uint2(LL_BASE[sym < 36 ? sym : 0], LL_BITS[sym < 36 ? sym : 0]);
-    return make_uint2(ML_BASE[sym < 53 ? sym : 0], ML_BITS[sym < 53 ? sym : 0]);
-}
-
-// FSE decode table for sequence codes (maxsym < 64), lane-parallel:
-//  spread: the j-th step of the position walk lands on p_j = j*step mod size;
-//  the k-th cell placed (symbol order) is the k-th p_j <= high, so symbols are
-//  found with a marker max-scan over k and positions with a prefix count over j.
-//  baseline: lane = symbol walks the positions in order (rank in position order).
-__device__ __forceinline__ void build_seq_fse(uint2 *t, const int16_t *norm, int32_t maxsym, int32_t al, int which,
-                                              uint8_t *mark, uint8_t *ksym, uint8_t *symat) {
-    const int l = lane_id();
-    const int32_t size = 1 << al, mask = size - 1, step = (size >> 1) + (size >> 3) + 3;
-    const int32_t nrm = l <= maxsym ? (int32_t)norm[l] : 0;
-    const uint32_t cntp = nrm > 0 ? (uint32_t)nrm : 0u, low = nrm == -1 ? 1u : 0u;
-    const uint32_t cum_i = dpp_scan_add(cntp), low_i = dpp_scan_add(low);
-    const uint32_t cum = cum_i - cntp, lowrank = low_i - low;
-    const int32_t nlow = (int32_t)readlane(low_i, 63);
-    const int32_t high = size - 1 - nlow;
-    const int32_t per = (size + 63) >> 6;  // positions per lane (1..8)
-    for (int k = l; k < size; k += 64) mark[k] = 0;
-    __builtin_amdgcn_wave_barrier();
-    if (cntp > 0) mark[cum] = (uint8_t)(l + 1);
-    if (low) symat[size - 1 - (int32_t)lowrank] = (uint8_t)l;
-    __builtin_amdgcn_wave_barrier();
-    // ksym[k] = symbol of the k-th placed cell
-    const int32_t q0 = l * per;
-    uint32_t lm = 0;
-    for (int i = 0; i < per; i++)
-        if (q0 + i < size) lm = umax32(lm, mark[q0 + i]);
-    uint32_t carry = dpp_shift_up(dpp_scan_max(lm), 0u);
-    for (int i = 0; i < per; i++) {
-        if (q0 + i < size) {
-            carry = umax32(carry, mark[q0 + i]);
-            ksym[q0 + i] = (uint8_t)(carry - 1);
-        }
-    }
-    __builtin_amdgcn_wave_barrier();
-    // positions: k_j = number of valid p_j' for j' < j
-    uint32_t nv = 0;
-    for (int i = 0; i < per; i++) {
-        int32_t j = q0 + i;
-        if (j < size && ((j * step) & mask) <= high) nv++;
-    }
-    uint32_t k = dpp_scan_add(nv) - nv;
-    for (int i = 0; i < per; i++) {
-        int32_t j = q0 + i;
-        int32_t pj = (j * step) & mask;
-        if (j < size && pj <= high) { symat[pj] = ksym[k]; k++; }
-    }
-    __builtin_amdgcn_wave_barrier();
-    // baseline, lane = symbol
-    const bool act = l <= maxsym && nrm != 0;
-    uint32_t ns = nrm == -1 ? 1u : (uint32_t)nrm;
-    const uint2 vb = seq_code(which, act ? (uint32_t)l : 0u);
-    for (int u4 = 0; u4 < size; u4 += 4) {
-        uint32_t w4 = *(const uint32_t *)(symat + u4);
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-            if (act && ((w4 >> (8 * b)) & 0xFFu) == (uint32_t)l) {
-                int nb = al - (31 - __builtin_clz(ns));
-                t[u4 + b] = make_uint2(vb.x, (uint32_t)nb | (vb.y << 8) | (((ns << nb) - (uint32_t)size) << 16));
-                ns++;
-            }
-        }
-    }
-    __builtin_amdgcn_wave_barrier();
 }
 
 // ---------------------------------------------------------------------------
@@ -767,12 +609,6 @@ __global__ __launch_bounds__(PLAN_T) void zplan_kernel(ZInfo *__restrict__ info,
 // ---------------------------------------------------------------------------
 // kernel 2: entropy decode (wave 0 literals, wave 1 sequences)
 // ---------------------------------------------------------------------------
-#ifndef JFS_ZLIT_FASTPEEK
-#define JFS_ZLIT_FASTPEEK 1  // zlit body steps away from the stream start peek without the start check
-#endif
-#ifndef JFS_ZLIT_QUAD
-#define JFS_ZLIT_QUAD 1  // Huffman streams: four symbols per step (two per refill, one aligned word store)
-#endif
 struct LitSmem {
     alignas(16) uint16_t huf[4096];  // sym | nb << 8
     uint8_t stage[256];
@@ -800,15 +636,6 @@ __device__ __forceinline__ void stage_bytes(uint8_t *dst, const gc_u8 *s, int32_
 template <class P>
 __device__ __forceinline__ void build_seq_fse_g(P t, const int16_t *norm, int32_t maxsym, int32_t al,
                                                 uint8_t *mark, uint8_t *ksym, uint8_t *symat);
-#ifndef JFS_HUF_FSEPAR
-#define JFS_HUF_FSEPAR 1  // Huffman weights' FSE table by the lane-parallel builder
-#endif
-#ifndef JFS_HUF_REGW
-#define JFS_HUF_REGW 1  // Huffman weights: FSE stream and table in registers (readlane), no memory round trip per weight
-#endif
-#ifndef JFS_HUF_PAR
-#define JFS_HUF_PAR 1  // Huffman table fill: lanes over symbols and cells (markers + prefix max), no per-symbol loop
-#endif
 // Huffman table description -> sm.huf at cell 2048 * slot (a 12-bit table:
 // cell 0, all 4096 cells).  Returns bytes used, -1 (corrupt) or -2 (a 12-bit
 // table with narrow_only: nothing written to the table cells).
@@ -824,7 +651,6 @@ __device__ __forceinline__ int32_t read_huf(LitSmem &sm, const gc_u8 *in, const 
         int32_t maxsym = 255, al = 0;
         int32_t c = read_ncount(sm.stage, hb, sm.norm, &maxsym, &al, 6);
         if (c < 0 || c > hb) return -1;
-#if JFS_HUF_FSEPAR
         if (maxsym > 63) {
             // (only a damaged description counts a weight symbol >= 64: the
             // lane-parallel builder holds one symbol per lane, so take the
@@ -842,11 +668,6 @@ __device__ __forceinline__ int32_t read_huf(LitSmem &sm, const gc_u8 *in, const 
             }
         }
         __builtin_amdgcn_wave_barrier();
-#else
-        if (build_fse(sm.fse, sm.norm, maxsym, al, sm.symnext, sm.symat)) return -1;
-        __builtin_amdgcn_wave_barrier();
-#endif
-#if JFS_HUF_REGW
         // the weight stream (<= 127 bytes, staged) as dword q in lane q and the
         // weight FSE table (<= 64 cells) as cell i in lane i: the serial
         // decode reads both with readlane, no memory round trip per weight
@@ -886,25 +707,6 @@ __device__ __forceinline__ int32_t read_huf(LitSmem &sm, const gc_u8 *in, const 
             s2 = (e2 >> 16) + bread((e2 >> 8) & 0xFF);
             if (left < 0) { if (l == 0) sm.w[nw] = (uint8_t)(readlane(fv, (int)s1) & 0xFF); nw++; break; }
         }
-#else
-        BR r;
-        if (!br_init(r, in, s + p + 1 + c, hb - c)) return -1;
-        uint32_t s1 = br_read(r, al), s2 = br_read(r, al);
-        for (;;) {
-            if (nw > 253) return -1;
-            uint32_t e1 = sm.fse[s1];
-            if (l == 0) sm.w[nw] = (uint8_t)(e1 & 0xFF);
-            nw++;
-            s1 = (e1 >> 16) + br_read(r, (e1 >> 8) & 0xFF);
-            if (br_overflow(r)) { if (l == 0) sm.w[nw] = (uint8_t)(sm.fse[s2] & 0xFF); nw++; break; }
-            if (nw > 253) return -1;
-            uint32_t e2 = sm.fse[s2];
-            if (l == 0) sm.w[nw] = (uint8_t)(e2 & 0xFF);
-            nw++;
-            s2 = (e2 >> 16) + br_read(r, (e2 >> 8) & 0xFF);
-            if (br_overflow(r)) { if (l == 0) sm.w[nw] = (uint8_t)(sm.fse[s1] & 0xFF); nw++; break; }
-        }
-#endif
         used = 1 + hb;
     } else {
         nw = hb - 127;
@@ -942,7 +744,6 @@ __device__ __forceinline__ int32_t read_huf(LitSmem &sm, const gc_u8 *in, const 
     if (maxbits == 12 && narrow_only) return -2;
     const uint32_t hbase = maxbits == 12 ? 0u : 2048u * (uint32_t)slot;
     __builtin_amdgcn_wave_barrier();
-#if JFS_HUF_PAR
     // every symbol's ordinal in (weight, symbol) order and its first cell:
     // lanes over symbols (four rounds), one ballot per weight and round
     uint32_t wv[4], ordv[4], posv[4];
@@ -998,28 +799,6 @@ __device__ __forceinline__ int32_t read_huf(LitSmem &sm, const gc_u8 *in, const 
         }
     }
     __builtin_amdgcn_wave_barrier();
-#else
-    // rank starts (weight ascending, then symbol order)
-    uint32_t cnt = 0;
-    for (int i = 0; i < nw; i++) cnt += (sm.w[i] == (uint32_t)l) ? 1u : 0u;  // lane k counts weight k
-    uint32_t span = (l >= 1 && l <= 12) ? (cnt << (l - 1)) : 0u;
-    uint32_t incl = dpp_scan_add(span);
-    uint32_t start = incl - span;
-    if (l < 16) sm.rank[l] = start;
-    __builtin_amdgcn_wave_barrier();
-    // fill: symbol by symbol, lanes over its 2^(w-1) cells
-    for (int i = 0; i < nw; i++) {
-        uint32_t wi = sm.w[i];
-        if (!wi) continue;
-        uint32_t len = 1u << (wi - 1);
-        uint32_t st = sm.rank[wi];
-        uint16_t e = (uint16_t)(i | ((maxbits + 1 - wi) << 8));
-        for (uint32_t u = l; u < len; u += 64) sm.huf[hbase + st + u] = e;
-        __builtin_amdgcn_wave_barrier();
-        if (l == 0) sm.rank[wi] = st + len;
-        __builtin_amdgcn_wave_barrier();
-    }
-#endif
     *maxbits_out = maxbits;
     __builtin_amdgcn_wave_barrier();
     return used;
@@ -1082,7 +861,6 @@ __device__ __forceinline__ uint32_t lit_decode(LitSmem &sm, const gc_u8 *in, con
         } else {
             const int64_t start = o, end = o + mycnt;
             uint32_t acc = 0;
-#if JFS_ZLIT_QUAD
             // one symbol: peek, table, consume (no refill: a refill leaves >= 32
             // bits in the container, two symbols take <= 24)
             auto sym = [&]() -> uint32_t {
@@ -1109,7 +887,7 @@ __device__ __forceinline__ uint32_t lit_decode(LitSmem &sm, const gc_u8 *in, con
             };
             for (; o + 4 <= end; o += 4) {
                 uint32_t w;
-                if (JFS_ZLIT_FASTPEEK && r.left >= fastlim) {
+                if (r.left >= fastlim) {
                     w = fsym();
                     w |= fsym() << 8;
                     br_refill(r);
@@ -1129,15 +907,6 @@ __device__ __forceinline__ uint32_t lit_decode(LitSmem &sm, const gc_u8 *in, con
                 acc |= sym() << (8 * (o & 3));
                 br_refill(r);
             }
-#else
-            for (; o < end; o++) {
-                uint32_t v = br_peek(r, maxbits);
-                uint32_t e = sm.huf[hb + v];
-                acc |= (e & 0xFF) << (8 * (o & 3));
-                br_skip(r, (int)(e >> 8));
-                if (((o + 1) & 3) == 0) { put_word(lb, start, o + 1, acc); acc = 0; }
-            }
-#endif
             if (o & 3) {
                 for (int64_t q = (o & ~3LL) > start ? (o & ~3LL) : start; q < o; q++) lb[q] = (uint8_t)(acc >> (8 * (q & 3)));
             }
@@ -1223,32 +992,7 @@ __device__ __forceinline__ int lit_pair(LitSmem &sm, const gc_u8 *s, g_u8 *lb, c
     return (bm & 1u) ? 1 : (bm & 2u) ? 2 : 0;
 }
 
-// one item into the wave's 64-entry store buffer
-struct ItemBuf {
-    uint4 v;
-    int32_t cnt;
-    uint64_t pos;    // next item index (absolute in the item buffer)
-    uint64_t limit;  // capacity end
-    int32_t bug;
-};
-__device__ __forceinline__ void item_flush(ItemBuf &b, g_u4 *items) {
-    const int l = lane_id();
-    if (b.cnt == 0) return;
-    if (b.pos + (uint64_t)b.cnt > b.limit) { b.bug = 1; b.cnt = 0; return; }
-    if (l < b.cnt) items[b.pos + l] = b.v;
-    b.pos += b.cnt;
-    b.cnt = 0;
-}
-__device__ __forceinline__ void item_put(ItemBuf &b, g_u4 *items, uint32_t x, uint32_t y, uint32_t z, uint32_t kind) {
-    if (lane_id() == b.cnt) b.v = make_uint4(x, y, z, kind);
-    b.cnt++;
-    if (b.cnt == 64) item_flush(b, items);
-}
-
 // sequence table for one field; returns bytes used or -1
-#ifndef JFS_ZLIT_PAIR
-#define JFS_ZLIT_PAIR 1  // Huffman literal sections of consecutive blocks decoded two at a time (8 lanes)
-#endif
 __device__ __forceinline__ void lit_wave(LitSmem &sm, const jfs_dev_block &b, ZInfo &zi, g_u8 *litbuf) {
     const int l = lane_id();
     const gc_u8 *s = (const gc_u8 *)b.src;
@@ -1320,7 +1064,7 @@ __device__ __forceinline__ void lit_wave(LitSmem &sm, const jfs_dev_block &b, ZI
         }
         LPend q;
         q.h = h; q.bpos = w.bpos; q.ord = ord; q.lpos = lpos;
-        if (h.type >= 2 && JFS_ZLIT_PAIR) {
+        if (h.type >= 2) {
             if (hp) {
                 hp = false;
                 const int r = lit_pair(sm, s, litbuf, pd, q);
@@ -1350,13 +1094,8 @@ __device__ __forceinline__ void lit_wave(LitSmem &sm, const jfs_dev_block &b, ZI
     }
 }
 
-#ifndef JFS_ZLIT_WAVES
-#define JFS_ZLIT_WAVES 4  // <= 128 VGPRs: 16 one-wave workgroups per CU (LDS 10,124 B), no spills
-#endif
 __global__ __launch_bounds__(64)
-#if JFS_ZLIT_WAVES
-__attribute__((amdgpu_waves_per_eu(JFS_ZLIT_WAVES)))
-#endif
+__attribute__((amdgpu_waves_per_eu(4)))
 void zlit_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
                                                   ZInfo *__restrict__ info, uint8_t *__restrict__ litbuf) {
     __shared__ LitSmem sm;
@@ -1388,39 +1127,7 @@ struct GBlk {
 };
 // Inputs per sequence workgroup: a 4 MiB frame has 32 compressed blocks, so
 // two inputs fill the 64 lanes of phase B.
-#ifndef JFS_ZSEQ_V2
-#define JFS_ZSEQ_V2 1
-#endif
-#ifndef JFS_ZSEQ_HALF
-#define JFS_ZSEQ_HALF 1  // zseqb: two workgroups per input (blocks [0, ZNB) and the rest)
-#endif
-#ifndef JFS_ZSEQ_INPUTS
-#if JFS_ZSEQ_V2
-#define JFS_ZSEQ_INPUTS 1  // zseqb: one input per workgroup packs the CUs better (123.3 vs 125.9 ms)
-#else
-#define JFS_ZSEQ_INPUTS 2
-#endif
-#endif
-constexpr int ZSEQ_INPUTS = JFS_ZSEQ_INPUTS;
-// Phase B decodes with the tables in LDS: the blocks of a group are taken in
-// sub-groups whose tables fit this arena (u16 cells; >= 11 blocks of the
-// largest tables), one lane per block.  Gathers from a per-block table in HBM
-// (2.5 KiB x 64 lanes x every wave: hundreds of MiB live at once) missed every
-// cache and each sequence waited on one, behind the wave's item stores.
-#ifndef JFS_ZSEQ_ARENA
-#define JFS_ZSEQ_ARENA 0  // > 0: tables staged in LDS per sub-group (measured slower: few lanes per wave)
-#endif
-constexpr int ZARENA = JFS_ZSEQ_ARENA;
-#ifndef JFS_ZSEQ_RING
-#define JFS_ZSEQ_RING 1  // tables in HBM: bitstreams staged in LDS rings, items buffered in LDS
-#endif
-// lanes (blocks) per phase-B pass, sequences per period (one HBM round trip:
-// bitstream refill + item flush), ring bytes per lane (16-byte blocks)
-constexpr int ZSUB = JFS_ZSEQ_ARENA > 0 ? 16 : 64;
-constexpr int ZK = JFS_ZSEQ_ARENA > 0 ? 8 : 4;
-constexpr int ZRB = JFS_ZSEQ_ARENA > 0 ? 256 : 128;
-static_assert(ZK * 12 + 24 <= ZRB - 16 && ZRB / 16 - 1 <= 15 + 0, "a period's bits must stay resident");
-static_assert(ZARENA == 0 || ZARENA >= 1280 + 8, "one block's largest tables must fit");
+constexpr int ZSEQ_INPUTS = 1;  // zseqb: one input per workgroup packs the CUs better (123.3 vs 125.9 ms)
 // Round 3 (default): a workgroup of two waves.  Wave 0 walks the headers and
 // builds each block's FSE tables straight into the group's LDS arena (phase
 // A), then decodes the group's ZNB blocks (one lane each) with every table
@@ -1428,32 +1135,14 @@ static_assert(ZARENA == 0 || ZARENA >= 1280 + 8, "one block's largest tables mus
 // stores are fire-and-forget.  Wave 1 (the mover) keeps each lane's
 // bitstream ring filled ahead of the decoder, one barrier per period of ZK2
 // sequences.
-#ifndef JFS_ZREP_BR
-#define JFS_ZREP_BR 1  // branchy repeat-offset update: measured faster than the select chain (168.5 vs 189.5 ms)
-#endif
-#ifndef JFS_ZUNROLL
-#define JFS_ZUNROLL 0
-#endif
-#ifndef JFS_ZNB
-#define JFS_ZNB 16
-#endif
 // blocks per group = decoder lanes: 16 fit three workgroups per CU in LDS
 // (12 fit four, one decoder wave per SIMD, but measured slower: 161-171 vs
 // 152 ms on configs[3])
-constexpr int ZNB = JFS_ZNB;
+constexpr int ZNB = 16;
 constexpr int ZMQ = 64 / ZNB < 4 ? 64 / ZNB : 4;  // mover lanes per block
-#ifndef JFS_ZK2
-#define JFS_ZK2 8
-#endif
-constexpr int ZK2 = JFS_ZK2;  // sequences per period
-#ifndef JFS_ZRB2
-#define JFS_ZRB2 512
-#endif
-constexpr int ZRB2 = JFS_ZRB2;  // bitstream ring bytes per lane (blocks of 16 B)
-#ifndef JFS_ZMOVE_D
-#define JFS_ZMOVE_D 2  // periods between a mover load and its landing in the ring
-#endif
-constexpr int ZMD = JFS_ZMOVE_D;
+constexpr int ZK2 = 8;  // sequences per period
+constexpr int ZRB2 = 512;  // bitstream ring bytes per lane (blocks of 16 B)
+constexpr int ZMD = 2;
 constexpr int ZAHEAD = ZRB2 == 512 ? (ZMD == 2 ? 27 : 24) : ZRB2 / 16 - 2;  // ring blocks the mover keeps below the published position
 // <= 89 bits per sequence: a period moves the position down <= 6 blocks and
 // a refill window reaches 128 bits below it (one block more).  Loads issued
@@ -1464,30 +1153,11 @@ constexpr int ZAHEAD = ZRB2 == 512 ? (ZMD == 2 ? 27 : 24) : ZRB2 / 16 - 2;  // r
 constexpr int ZPB = (ZK2 * 89 + 127) / 128;
 constexpr int ZPRE = ZAHEAD + 3 < ZRB2 / 16 - 2 ? ZAHEAD + 3 : ZRB2 / 16 - 2;  // prefill depth below the top block
 static_assert((ZMD + 1) * ZPB + 7 <= ZAHEAD && ZAHEAD <= ZRB2 / 16 - 2 && ZPB + 2 <= 8, "ring budget");
-#if JFS_ZSEQ_V2
 struct ASmem {  // zseqa: table-build scratch
     uint8_t stage[256];
     int16_t norm[64];
     uint8_t symat[512], mark[512], ksym[512];
 };
-#ifndef JFS_ZMOVE_ROT
-#define JFS_ZMOVE_ROT 1  // mover: two alternating load sets, loads before the item stores
-#endif
-#ifndef JFS_ZSEQ_XB8
-#define JFS_ZSEQ_XB8 1  // state pass: extra-bit counts from byte tables (no shift after the lookup)
-#endif
-#ifndef JFS_ZSEQ_NEXTALL
-#define JFS_ZSEQ_NEXTALL 1  // state pass: next states computed unconditionally (no per-sequence branch)
-#endif
-#ifndef JFS_ZSEQ_XALIGN
-#define JFS_ZSEQ_XALIGN 1  // state pass: the next-state bit field by one alignbit from the window dwords
-#endif
-#ifndef JFS_ZSEQ_STATE32
-#define JFS_ZSEQ_STATE32 1  // state pass: the three next-state reads from one 32-bit field of the window
-#endif
-#ifndef JFS_ZSEQ_AB
-#define JFS_ZSEQ_AB 1  // decoder: serial state pass + lane-parallel value pass per period
-#endif
 struct SeqSmem {  // zseqb
     alignas(16) uint8_t bring[ZNB][ZRB2 + 16];   // per-lane bitstream rings (+ a mirror of block slot 0)
     alignas(16) uint16_t arena[ZNB][TAB_CELLS];  // the group's tables (LL 0, OF 512, ML 768)
@@ -1497,38 +1167,14 @@ struct SeqSmem {  // zseqb
     int32_t pos[2][ZNB];  // decoder bit positions published at each period's barrier
     int32_t more[2];      // any lane still decoding (per period parity)
     int32_t cmd;          // wave 0 -> wave 1: blocks in the group, 0 = done
-#if JFS_ZSEQ_AB
     uint2 rec[2][ZK2][ZNB];    // a period's sequences (period parity): bit position, states (sll | sof << 10 | sml << 20)
     uint32_t carry[3][ZNB];    // repeat offsets after the block's sequences so far (symbolic in its entry state)
     int32_t rcnt[2][ZNB];      // sequences recorded in the period
     uint32_t ibase[2][ZNB];    // sequence index of the period's first record
-#endif
 };
 static_assert(sizeof(SeqSmem) * (ZNB <= 12 ? 4 : 3) <= 160 * 1024, "sequence workgroups per CU (one decoder wave per SIMD)");
 static_assert(ZMQ == 4, "the mover serves each block with four lanes (stride-4 block loads)");
-#else
-struct SeqSmem {
-    uint8_t stage[256];
-    int16_t norm[64];
-    uint8_t symat[512], mark[512], ksym[512];
-    uint32_t lut_ll[36], lut_ml[53];  // value base | extra bits << 24
-    GBlk g[64];
-#if JFS_ZSEQ_ARENA > 0
-    alignas(16) uint16_t arena[ZARENA];
-    uint16_t aofs[64][4];   // arena cell offsets of a sub-group block's LL / OF / ML tables
-    uint32_t rr[3][64];     // phase B results per group block: symbolic repeat offsets
-    uint32_t brep[64];
-#endif
-#if JFS_ZSEQ_ARENA > 0 || JFS_ZSEQ_RING
-    alignas(16) uint8_t bring[ZSUB][ZRB];  // per-lane sequence bitstream ring (16-byte blocks)
-    uint4 ibuf[ZK][ZSUB];                  // items of the current period, flushed together
-#endif
-};
-#endif
 
-#ifndef JFS_FSE_POSPAR
-#define JFS_FSE_POSPAR 1  // sequence FSE tables: position-parallel state assignment
-#endif
 // u16 cell = sym | ns << 6  (nb = al - highbit(ns), next-state base = (ns << nb) - 2^al)
 template <class P>
 __device__ __forceinline__ void build_seq_fse_g(P t, const int16_t *norm, int32_t maxsym, int32_t al,
@@ -1571,7 +1217,6 @@ __device__ __forceinline__ void build_seq_fse_g(P t, const int16_t *norm, int32_
         if (j < size && pj <= high) { symat[pj] = ksym[k]; k++; }
     }
     __builtin_amdgcn_wave_barrier();
-#if JFS_FSE_POSPAR
     // position-parallel: 64 cells per step; a cell's state is its symbol's
     // counter plus its rank among the step's cells of that symbol (one ballot
     // per distinct symbol in the step); one coalesced store per step
@@ -1591,20 +1236,6 @@ __device__ __forceinline__ void build_seq_fse_g(P t, const int16_t *norm, int32_
         }
         if (u < size) t[u] = (uint16_t)cell;
     }
-#else
-    const bool act = l <= maxsym && nrm != 0;
-    uint32_t ns = nrm == -1 ? 1u : (uint32_t)nrm;
-    for (int u4 = 0; u4 < size; u4 += 4) {
-        uint32_t w4 = *(const uint32_t *)(symat + u4);
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-            if (act && ((w4 >> (8 * b)) & 0xFFu) == (uint32_t)l) {
-                t[u4 + b] = (uint16_t)((uint32_t)l | (ns << 6));
-                ns++;
-            }
-        }
-    }
-#endif
     __builtin_amdgcn_wave_barrier();
 }
 
@@ -1647,10 +1278,6 @@ __device__ __forceinline__ int32_t seq_table_g(SM &sm, P tabs, uint32_t area, ui
     return *have ? 0 : -1;
 }
 
-#ifndef JFS_ZSEQA_DEFER
-#define JFS_ZSEQA_DEFER 1  // zseqa parses table descriptions only; zbuild spreads all blocks' tables in parallel
-#endif
-#if JFS_ZSEQA_DEFER
 // A deferred table's normalized counts wait in the last 64 cells of its own
 // region (zbuild reads them into registers before spreading over the region);
 // ZDesc.rsv carries per field maxsym (6 bits at 6f) and the build kind
@@ -1691,12 +1318,7 @@ __device__ __forceinline__ int32_t seq_table_defer(SM &sm, g_u16 *tabs, uint32_t
     }
     return *have ? 0 : -1;
 }
-#endif
 
-__device__ __forceinline__ uint32_t rep_dec(uint32_t v) {  // libzstd: rep0 - 1, 0 becomes 1
-    if (v & SYMB) return v + 1;
-    return v - 1 == 0 ? 1u : v - 1;
-}
 __device__ __forceinline__ uint32_t rep_res(uint32_t v, uint32_t e0, uint32_t e1, uint32_t e2) {
     if (!(v & SYMB)) return v;
     uint32_t j = (v >> 29) & 3, d = v & 0x1FFFFFFFu;
@@ -1704,358 +1326,7 @@ __device__ __forceinline__ uint32_t rep_res(uint32_t v, uint32_t e0, uint32_t e1
     return e > d + 1 ? e - d : 1u;
 }
 
-#if JFS_ZSEQ_ARENA > 0 || JFS_ZSEQ_RING
-// Backward bit reader over a per-lane LDS ring of ZRB / 16 stream blocks (16 B
-// each; block k at ring offset (k & 15) * 16, blocks below the input read as
-// zero).  Same bit semantics as BR; the ring is refilled once per period of ZK
-// sequences (<= 89 bits per sequence: <= 6 blocks per period), so the
-// sequence loop itself waits on LDS only.
-struct LR {
-    const gc_u4 *b16;
-    uint8_t *ring;
-    int32_t m, lowk, left, cb, lr;  // lr: lowest block resident in the ring
-    uint64_t c;
-};
 
-__device__ __forceinline__ uint32_t lr_dw(const LR &r, int32_t q) { return *(const uint32_t *)(r.ring + (q & (ZRB - 1))); }
-
-// blocks [lo, r.lr) into the ring (at most 8); r.lr = lo
-__device__ __forceinline__ void lr_load(LR &r, int32_t lo, bool on) {
-    uint4 v[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const int32_t k = r.lr - 1 - j;
-        v[j] = make_uint4(0, 0, 0, 0);
-        if (on && k >= lo && k >= r.lowk) v[j] = r.b16[k];
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const int32_t k = r.lr - 1 - j;
-        if (on && k >= lo) *(uint4 *)(r.ring + ((k & (ZRB / 16 - 1)) << 4)) = v[j];
-    }
-    if (on && lo < r.lr) r.lr = lo;
-}
-
-__device__ __forceinline__ bool lr_init(LR &r, uint8_t *ring, const gc_u8 *in, const gc_u8 *p, int32_t size) {
-    const uintptr_t a = (uintptr_t)p;
-    r.ring = ring;
-    r.b16 = (const gc_u4 *)(a & ~(uintptr_t)15);
-    r.m = (int32_t)(a & 15);
-    r.lowk = -(int32_t)((((uintptr_t)r.b16) - (((uintptr_t)in) & ~(uintptr_t)15)) >> 4);
-    if (size <= 0) return false;
-    const int32_t top = r.m + size;
-    const uint32_t last = ((const gc_u8 *)r.b16)[top - 1];
-    if (last == 0) return false;
-    r.left = 8 * (top - 1) + (31 - __builtin_clz(last));
-    r.cb = ((top - 1) & ~3) - 4;
-    r.lr = ((top - 1) >> 4) + 1;  // nothing resident yet
-    return true;
-}
-
-// first fill (after lr_init; wave-uniform call, `on` = this lane reads a stream)
-__device__ __forceinline__ void lr_start(LR &r, bool on) {
-    const int32_t kt = r.lr - 1;
-    lr_load(r, kt - 7, on);
-    if (ZRB / 16 > 8) lr_load(r, kt - (ZRB / 16 - 1), on);
-    __builtin_amdgcn_wave_barrier();
-    if (on) r.c = ((uint64_t)lr_dw(r, r.cb + 4) << 32) | lr_dw(r, r.cb);
-}
-
-// start of a period: blocks [ck - 15, ck] resident, ck = block of the next dword
-__device__ __forceinline__ void lr_period(LR &r, bool on) {
-    lr_load(r, ((r.cb - 4) >> 4) - (ZRB / 16 - 1), on);
-    __builtin_amdgcn_wave_barrier();
-}
-
-__device__ __forceinline__ uint32_t lr_read(LR &r, int n) {
-    if (n == 0) return 0u;
-    const int32_t lo = r.left - n;
-    uint32_t v = (uint32_t)(r.c >> (uint32_t)(lo - 8 * r.cb)) & (uint32_t)(0xFFFFFFFFull >> (32 - n));
-    const int32_t d = 8 * r.m - lo;
-    if (d > 0) v = d >= n ? 0u : v & ~((1u << d) - 1u);
-    r.left = lo;
-    if (r.left - 8 * r.cb < 32) {
-        r.cb -= 4;
-        r.c = (r.c << 32) | lr_dw(r, r.cb);
-    }
-    return v;
-}
-#endif
-
-#if !JFS_ZSEQ_V2 && (JFS_ZSEQ_ARENA > 0 || JFS_ZSEQ_RING)
-// Phase B with the sequence bitstreams staged in per-lane LDS rings and the
-// items buffered in LDS: one HBM round trip per period of ZK sequences (ring
-// refill + item flush) instead of several per sequence.  TP: table cells in
-// LDS (arena) or in HBM.
-template <class TP>
-__device__ __forceinline__ void seq_periods(SeqSmem &sm, const GBlk &d, bool mine, TP tl, TP to, TP tm, uint32_t &r0,
-                                            uint32_t &r1, uint32_t &r2, uint32_t &brep) {
-    // lanes [0, g1 - g0): one block each; periods of ZK sequences, each
-    // starting with a ring refill and ending with the item flush
-    const int l = lane_id();
-    const int32_t all = d.al & 0xFF, alof = (d.al >> 8) & 0xFF, alml = (d.al >> 16) & 0xFF;
-    g_u4 *it = d.ib + d.item;
-    bool run = false;
-    LR r = {};
-    if (mine) {
-        if (d.nseq == 0) {
-            it[1] = make_uint4(0, 0, 0, IT_BREP);
-            it[2] = make_uint4(0, 0, 0, IT_BEND);
-            brep = 1;
-        } else if (!lr_init(r, sm.bring[mine ? l : 0], d.in, d.bs, d.bsz)) {
-            it[1] = make_uint4(0, 0, (uint32_t)E_CORRUPT, IT_ERR);
-        } else {
-            brep = 1;
-            run = true;
-        }
-    }
-    lr_start(r, run);
-    uint32_t sll = 0, sof = 0, sml = 0;
-    if (run) {
-        sll = lr_read(r, all);
-        sof = lr_read(r, alof);
-        sml = lr_read(r, alml);
-    }
-    const uint32_t szl = 1u << all, szo = 1u << alof, szm = 1u << alml;
-    for (int32_t i0 = 0; __ballot(run); i0 += ZK) {
-        lr_period(r, run);
-        int32_t nbuf = 0;
-        bool fin = false;
-        uint4 term = make_uint4(0, 0, 0, 0);
-        int32_t tidx = 0;
-        for (int k = 0; k < ZK; ++k) {
-            if (run) {
-                const int32_t i = i0 + k;
-                if (r.left < 8 * r.m) {  // overflow
-                    term = make_uint4(0, 0, (uint32_t)E_CORRUPT, IT_ERR);
-                    tidx = 2 + i;
-                    fin = true;
-                    run = false;
-                } else {
-                    const uint32_t cl = tl[sll], co = to[sof], cm = tm[sml];
-                    const uint32_t lv = sm.lut_ll[cl & 63], mv = sm.lut_ml[cm & 63], ofc = co & 63;
-                    const uint32_t ofv = (1u << ofc) + lr_read(r, (int)ofc);
-                    const uint32_t ml = (mv & 0xFFFFFFu) + lr_read(r, (int)(mv >> 24));
-                    const uint32_t ll = (lv & 0xFFFFFFu) + lr_read(r, (int)(lv >> 24));
-                    uint32_t off;
-                    if (ofv > 3) {
-                        off = ofv - 3;
-                        r2 = r1; r1 = r0; r0 = off;
-                    } else {
-                        const uint32_t kk = ofv - 1 + (ll == 0 ? 1u : 0u);
-                        if (kk == 0) {
-                            off = r0;
-                        } else {
-                            const uint32_t t = kk == 1 ? r1 : kk == 2 ? r2 : rep_dec(r0);
-                            if (kk != 1) r2 = r1;
-                            r1 = r0;
-                            r0 = t;
-                            off = t;
-                        }
-                    }
-                    if (i + 1 < d.nseq) {
-                        const uint32_t nsl = cl >> 6, nso = co >> 6, nsm = cm >> 6;
-                        const int nbl = all - (31 - __builtin_clz(nsl));
-                        const int nbm = alml - (31 - __builtin_clz(nsm));
-                        const int nbo = alof - (31 - __builtin_clz(nso));
-                        sll = ((nsl << nbl) - szl) + lr_read(r, nbl);
-                        sml = ((nsm << nbm) - szm) + lr_read(r, nbm);
-                        sof = ((nso << nbo) - szo) + lr_read(r, nbo);
-                    }
-                    sm.ibuf[k][l] = make_uint4(ll, ml, off, IT_SEQ);
-                    nbuf = k + 1;
-                    if (i + 1 == d.nseq) {
-                        term = r.left == 8 * r.m ? make_uint4(0, 0, 0, IT_BEND)
-                                                 : make_uint4(0, 0, (uint32_t)E_CORRUPT, IT_ERR);
-                        tidx = 2 + d.nseq;
-                        fin = true;
-                        run = false;
-                    }
-                }
-            }
-        }
-        // flush the period's items (then the block's terminal item)
-        if (mine) {
-#pragma unroll
-            for (int k = 0; k < ZK; ++k)
-                if (k < nbuf) it[2 + i0 + k] = sm.ibuf[k][l];
-            if (fin) it[tidx] = term;
-        }
-    }
-}
-
-#endif
-
-#if !JFS_ZSEQ_V2
-// phases B and C for the collected group
-__device__ __forceinline__ void seq_group(SeqSmem &sm, int gn, const gc_u16 *tabs, uint32_t *e0, uint32_t *e1,
-                                          uint32_t *e2) {
-    const int l = lane_id();
-    [[maybe_unused]] uint64_t zt = ZP_NOW();
-    ZS_ADD(5, 1);
-    __builtin_amdgcn_wave_barrier();
-    wait_vm();  // table cells written in phase A are complete before they are gathered
-#if JFS_ZSEQ_ARENA > 0
-    for (int g0 = 0; g0 < gn;) {
-    // sub-group [g0, g1): as many blocks as the arena holds; their tables are
-    // staged field by field (all loads of a block before its LDS writes)
-    int g1 = g0;
-    {
-        uint32_t used = 0;
-        while (g1 < gn) {
-            const uint32_t a = sm.g[g1].al;
-            const uint32_t nl = 1u << (a & 0xFF), no = 1u << ((a >> 8) & 0xFF), nm = 1u << ((a >> 16) & 0xFF);
-            const uint32_t sz = ((nl + 1) & ~1u) + ((no + 1) & ~1u) + ((nm + 1) & ~1u);
-            if (used + sz > (uint32_t)ZARENA || g1 - g0 >= ZSUB) break;
-            const uint32_t ol = used, oo = ol + ((nl + 1) & ~1u), om = oo + ((no + 1) & ~1u);
-            const GBlk &d = sm.g[g1];
-            const gc_u32 *ql = (const gc_u32 *)(tabs + d.tll), *qo = (const gc_u32 *)(tabs + d.tof),
-                         *qm = (const gc_u32 *)(tabs + d.tml);
-            const uint32_t dl = (nl + 1) >> 1, dof = (no + 1) >> 1, dm = (nm + 1) >> 1;  // dwords
-            uint32_t vl[4], vo[2], vm[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) vl[j] = (uint32_t)l + 64u * j < dl ? ql[l + 64 * j] : 0u;
-#pragma unroll
-            for (int j = 0; j < 2; ++j) vo[j] = (uint32_t)l + 64u * j < dof ? qo[l + 64 * j] : 0u;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) vm[j] = (uint32_t)l + 64u * j < dm ? qm[l + 64 * j] : 0u;
-            uint32_t *ar = (uint32_t *)sm.arena;
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                if ((uint32_t)l + 64u * j < dl) ar[(ol >> 1) + l + 64 * j] = vl[j];
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-                if ((uint32_t)l + 64u * j < dof) ar[(oo >> 1) + l + 64 * j] = vo[j];
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                if ((uint32_t)l + 64u * j < dm) ar[(om >> 1) + l + 64 * j] = vm[j];
-            if (l == 0) {
-                sm.aofs[g1 - g0][0] = (uint16_t)ol;
-                sm.aofs[g1 - g0][1] = (uint16_t)oo;
-                sm.aofs[g1 - g0][2] = (uint16_t)om;
-            }
-            used += sz;
-            g1++;
-        }
-    }
-    __builtin_amdgcn_wave_barrier();
-    ZS_ADD(4, 1);
-    { const uint64_t t = ZP_NOW(); ZS_ADD(1, t - zt); zt = t; }
-    uint32_t r0 = SYMB | (0u << 29), r1 = SYMB | (1u << 29), r2 = SYMB | (2u << 29);
-    uint32_t brep = 0;
-    const bool mine = l < g1 - g0;
-    const GBlk d = sm.g[mine ? g0 + l : g0];
-    seq_periods(sm, d, mine, (const uint16_t *)sm.arena + sm.aofs[mine ? l : 0][0],
-                (const uint16_t *)sm.arena + sm.aofs[mine ? l : 0][1], (const uint16_t *)sm.arena + sm.aofs[mine ? l : 0][2],
-                r0, r1, r2, brep);
-#elif JFS_ZSEQ_RING
-    uint32_t r0 = SYMB | (0u << 29), r1 = SYMB | (1u << 29), r2 = SYMB | (2u << 29);
-    uint32_t brep = 0;
-    {
-        const bool mine = l < gn;
-        const GBlk d = sm.g[mine ? l : 0];
-        seq_periods(sm, d, mine, tabs + d.tll, tabs + d.tof, tabs + d.tml, r0, r1, r2, brep);
-    }
-#else
-    uint32_t r0 = SYMB | (0u << 29), r1 = SYMB | (1u << 29), r2 = SYMB | (2u << 29);
-    uint32_t brep = 0;
-    if (l < gn) {
-        const GBlk d = sm.g[l];
-        const int32_t all = d.al & 0xFF, alof = (d.al >> 8) & 0xFF, alml = (d.al >> 16) & 0xFF;
-        const gc_u16 *tl = tabs + d.tll, *to = tabs + d.tof, *tm = tabs + d.tml;
-        g_u4 *it = d.ib + d.item;
-        if (d.nseq == 0) {
-            it[1] = make_uint4(0, 0, 0, IT_BREP);
-            it[2] = make_uint4(0, 0, 0, IT_BEND);
-            brep = 1;
-        } else {
-            BR r;
-            if (!br_init(r, d.in, d.bs, d.bsz)) {
-                it[1] = make_uint4(0, 0, (uint32_t)E_CORRUPT, IT_ERR);
-            } else {
-                brep = 1;
-                uint32_t sll = br_read(r, all), sof = br_read(r, alof), sml = br_read(r, alml);
-                const uint32_t szl = 1u << all, szo = 1u << alof, szm = 1u << alml;
-                for (int32_t i = 0; i < d.nseq; i++) {
-                    if (br_overflow(r)) { it[2 + i] = make_uint4(0, 0, (uint32_t)E_CORRUPT, IT_ERR); break; }
-#ifdef JFS_ZSEQ_NOTAB  // diagnostics only: wrong output
-                    const uint32_t cl = (sll & 63) | (64u << 6), co = (sof & 31) | (32u << 6), cm = (sml & 63) | (64u << 6);
-#else
-                    const uint32_t cl = tl[sll], co = to[sof], cm = tm[sml];
-#endif
-                    const uint32_t lv = sm.lut_ll[cl & 63], mv = sm.lut_ml[cm & 63], ofc = co & 63;
-                    uint32_t ofv = (1u << ofc) + br_read(r, (int)ofc);
-                    uint32_t ml = (mv & 0xFFFFFFu) + br_read(r, (int)(mv >> 24));
-                    uint32_t ll = (lv & 0xFFFFFFu) + br_read(r, (int)(lv >> 24));
-                    uint32_t off;
-                    if (ofv > 3) {
-                        off = ofv - 3;
-                        r2 = r1; r1 = r0; r0 = off;
-                    } else {
-                        uint32_t k = ofv - 1 + (ll == 0 ? 1u : 0u);
-                        if (k == 0) {
-                            off = r0;
-                        } else {
-                            uint32_t t = k == 1 ? r1 : k == 2 ? r2 : rep_dec(r0);
-                            if (k != 1) r2 = r1;
-                            r1 = r0;
-                            r0 = t;
-                            off = t;
-                        }
-                    }
-                    if (i + 1 < d.nseq) {
-                        const uint32_t nsl = cl >> 6, nso = co >> 6, nsm = cm >> 6;
-                        const int nbl = all - (31 - __builtin_clz(nsl));
-                        const int nbm = alml - (31 - __builtin_clz(nsm));
-                        const int nbo = alof - (31 - __builtin_clz(nso));
-                        sll = ((nsl << nbl) - szl) + br_read(r, nbl);
-                        sml = ((nsm << nbm) - szm) + br_read(r, nbm);
-                        sof = ((nso << nbo) - szo) + br_read(r, nbo);
-                    }
-#ifndef JFS_ZSEQ_NOSTORE  // diagnostics only: wrong output
-                    it[2 + i] = make_uint4(ll, ml, off, IT_SEQ);
-#endif
-                    if (i + 1 == d.nseq)
-                        it[2 + d.nseq] = br_done(r) ? make_uint4(0, 0, 0, IT_BEND)
-                                                    : make_uint4(0, 0, (uint32_t)E_CORRUPT, IT_ERR);
-                }
-            }
-        }
-    }
-#endif
-#if JFS_ZSEQ_ARENA > 0
-    if (l < g1 - g0) {
-        sm.rr[0][g0 + l] = r0;
-        sm.rr[1][g0 + l] = r1;
-        sm.rr[2][g0 + l] = r2;
-        sm.brep[g0 + l] = brep;
-    }
-    __builtin_amdgcn_wave_barrier();
-    { const uint64_t t = ZP_NOW(); ZS_ADD(2, t - zt); zt = t; }
-    g0 = g1;
-    }  // sub-groups
-#endif
-    // phase C: entry states in stream order
-    for (int g = 0; g < gn; g++) {
-        const uint32_t al = sm.g[g].al, item = sm.g[g].item;
-        g_u4 *ib = sm.g[g].ib;
-        if (al >> 24) { *e0 = 1; *e1 = 4; *e2 = 8; }
-#if JFS_ZSEQ_ARENA > 0
-        const uint32_t x0 = sm.rr[0][g], x1 = sm.rr[1][g], x2 = sm.rr[2][g];
-        if (sm.brep[g] && l == 0) ib[item + 1] = make_uint4(*e0, *e1, *e2, IT_BREP);
-#else
-        const uint32_t x0 = readlane(r0, g), x1 = readlane(r1, g), x2 = readlane(r2, g);
-        if (readlane(brep, g) && l == 0) ib[item + 1] = make_uint4(*e0, *e1, *e2, IT_BREP);
-#endif
-        const uint32_t n0 = rep_res(x0, *e0, *e1, *e2), n1 = rep_res(x1, *e0, *e1, *e2), n2 = rep_res(x2, *e0, *e1, *e2);
-        *e0 = n0; *e1 = n1; *e2 = n2;
-    }
-    __builtin_amdgcn_wave_barrier();
-    { const uint64_t t = ZP_NOW(); ZS_ADD(3, t - zt); }
-}
-#endif  // !JFS_ZSEQ_V2
-
-#if JFS_ZSEQ_V2
 // LDS-only barrier between the decoder and mover waves (the decoder's item
 // stores stay in flight)
 __device__ __forceinline__ void zsync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
@@ -2085,7 +1356,7 @@ __device__ __forceinline__ void zr_put(uint8_t *ring, int32_t k, const uint4 &v)
 }
 // Refill: bits [left - 96, left) from the ring (one round of four LDS dword
 // reads; the mover wrote zeros below the stream start, so bits there read as
-// zero, like lr_read).  hi = bits [left - 64, left), lo = bits [left - 96, left - 64).
+// zero, like the bit readers above).  hi = bits [left - 64, left), lo = bits [left - 96, left - 64).
 __device__ __forceinline__ void zw_fill(const uint8_t *ring, int32_t left, uint64_t &hi, uint32_t &lo) {
     const int32_t cb = ((left - 96) >> 5) << 2;  // 8 * cb in (left - 128, left - 96]
     const uint32_t *w = (const uint32_t *)(ring + (cb & (ZRB2 - 1)));  // + 16 bytes: the mirror
@@ -2114,14 +1385,8 @@ __device__ __forceinline__ uint32_t zw_get(uint64_t hi, int32_t &c, uint32_t n) 
     c += (int32_t)n;
     return __builtin_amdgcn_ubfe(x, 32u - n, n);
 }
-// the 64-bit window after c (<= 63) bits were consumed; its top 32 bits are exact
-__device__ __forceinline__ uint64_t zw_shift(uint64_t hi, uint32_t lo, int32_t c) {
-    return c ? (hi << c) | (((uint64_t)lo << 32) >> (64 - c)) : hi;
-}
 
-#if JFS_ZSEQ_AB
 __device__ __forceinline__ void zvalues(SeqSmem &sm, int gn, int b);
-#endif
 // Wave 1: stage the group's tables (built in HBM by zseqa) into the arena,
 // prefill the rings, then one refill round per period until the decoder
 // reports no lane running.
@@ -2183,7 +1448,6 @@ __device__ __forceinline__ void zmover(SeqSmem &sm, int gn, const gc_u16 *tabs) 
     }
     { const uint64_t t = ZP_NOW(); ZS_ADD(1, t - zt); }
     zsync();  // tables and rings ready
-#if JFS_ZMOVE_ROT
     // Two sets of pending loads, used alternately: the loads a period issues
     // land (into the ring) two periods later from the same registers.  With
     // one shifting queue the copies between queue slots read registers whose
@@ -2222,9 +1486,7 @@ __device__ __forceinline__ void zmover(SeqSmem &sm, int gn, const gc_u16 *tabs) 
             vv[i] = *(oo[i] && k >= 0 ? g.b16 + k : (const gc_u4 *)tabs);
         }
         if (on && lo < lr) lr = lo;
-#if JFS_ZSEQ_AB
         if (p > 0) zvalues(sm, gn, (p - 1) & 1);  // the decoder's previous period
-#endif
         zsync();
         return sm.more[p & 1] != 0;
     };
@@ -2234,65 +1496,10 @@ __device__ __forceinline__ void zmover(SeqSmem &sm, int gn, const gc_u16 *tabs) 
         if (!period(kb, vb, ob)) break;
         ++p;
     }
-#else
-    // pend[0]: loads issued ZMD iterations ago (landed now), pend[ZMD - 1]: newest
-    int32_t pend_k[ZMD][2];
-    uint4 pend_v[ZMD][2];
-    bool pend_on[ZMD][2];
-#pragma unroll
-    for (int d = 0; d < ZMD; ++d)
-#pragma unroll
-        for (int i = 0; i < 2; ++i) { pend_k[d][i] = 0; pend_v[d][i] = make_uint4(0, 0, 0, 0); pend_on[d][i] = false; }
-    int p = 0;
-    [[maybe_unused]] uint64_t zm0 = ZP_NOW(), zacc[5] = {0, 0, 0, 0, 0};
-    for (;; ++p) {
-        // land the blocks loaded ZMD periods ago
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-            if (pend_on[0][i]) zr_put(ring, pend_k[0][i], zclip(pend_v[0][i], pend_k[0][i], g.m));
-        [[maybe_unused]] uint64_t zm1 = ZP_NOW();
-        zacc[0] += zm1 - zm0;
-#if JFS_ZSEQ_AB
-        if (p > 0) zvalues(sm, gn, (p - 1) & 1);  // the decoder's previous period
-#endif
-        [[maybe_unused]] uint64_t zm2 = ZP_NOW();
-        zacc[1] += zm2 - zm1;
-#pragma unroll
-        for (int d = 0; d + 1 < ZMD; ++d)
-#pragma unroll
-            for (int i = 0; i < 2; ++i) { pend_k[d][i] = pend_k[d + 1][i]; pend_v[d][i] = pend_v[d + 1][i]; pend_on[d][i] = pend_on[d + 1][i]; }
-        // next loads: ZAHEAD blocks below the position published at the last barrier
-        const int32_t left = p == 0 ? 0 : sm.pos[(p - 1) & 1][j];
-        const int32_t tgt = p == 0 ? lr : ((left - 1) >> 7) - ZAHEAD;
-        int32_t lo = lr - 8;
-        if (tgt > lo) lo = tgt;
-        if (KFLOOR > lo) lo = KFLOOR;
-        if (lo > lr) lo = lr;
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int32_t k = lr - 1 - q - 4 * i;
-            pend_k[ZMD - 1][i] = k;
-            pend_on[ZMD - 1][i] = on && k >= lo;
-            pend_v[ZMD - 1][i] = make_uint4(0, 0, 0, 0);
-            if (pend_on[ZMD - 1][i] && k >= 0) pend_v[ZMD - 1][i] = g.b16[k];
-        }
-        if (on && lo < lr) lr = lo;
-        [[maybe_unused]] uint64_t zm3 = ZP_NOW();
-        zacc[2] += zm3 - zm2;
-        zsync();
-        zm0 = ZP_NOW();
-        zacc[3] += zm0 - zm3;
-        zacc[4] += 1;
-        if (!sm.more[p & 1]) break;
-    }
-#endif
-#if JFS_ZSEQ_AB
     zvalues(sm, gn, p & 1);  // the last period
     zsync();
-#endif
 }
 
-#if JFS_ZSEQ_AB
 // Phase B for the group (lane = block), tables and bitstreams in LDS, in two
 // passes per period.  The STATE pass (wave 0, the decoder) is the serial part:
 // per lane and sequence three cells, two extra-bit lookups and one bitstream
@@ -2316,9 +1523,6 @@ __device__ __forceinline__ uint32_t zsub(uint32_t x, uint32_t a0, uint32_t a1, u
     return y > dd ? y - dd : 1u;
 }
 __device__ __forceinline__ void zvalues(SeqSmem &sm, int gn, int b) {
-#ifdef JFS_SKIP_ZVALUES  // diagnostics: the state pass alone (wrong output)
-    return;
-#endif
     const int l = lane_id();
     const int j = l & (ZNB - 1);
     static_assert(ZNB == 16 && ZK2 == 8, "value pass layout: 16 blocks x 4 records per round, two rounds");
@@ -2441,40 +1645,25 @@ __device__ __forceinline__ void zdecode(SeqSmem &sm, int gn, uint32_t &r0, uint3
                     run = false;
                 } else {
                     const uint32_t cl = tl[sll], co = to[sof], cm = tm[sml];
-#if JFS_ZSEQ_XALIGN
                     const int32_t cbw = ((left - 96) >> 5) << 2;  // as zw_fill
                     const uint32_t *w4 = (const uint32_t *)(ring + (cbw & (ZRB2 - 1)));
                     const uint32_t d0 = w4[0], d1 = w4[1], d2 = w4[2], d3 = w4[3];
                     const int32_t tw = left - 8 * cbw - 64;  // [32, 64)
-#else
-                    uint64_t hi;
-                    uint32_t lo;
-                    zw_fill(ring, left, hi, lo);
-#endif
                     sm.rec[p & 1][k][l] = make_uint2((uint32_t)left, sll | (sof << 10) | (sml << 20));
-#if JFS_ZSEQ_XB8
                     const int32_t c = (int32_t)((uint32_t)sm.xb_ll[cl & 63] + (uint32_t)sm.xb_ml[cm & 63] + (co & 63));
-#else
-                    const int32_t c = (int32_t)((sm.lut_ll[cl & 63] >> 24) + (sm.lut_ml[cm & 63] >> 24) + (co & 63));
-#endif
                     int32_t c2 = 0;
                     // (the next states are computed for the last sequence too --
                     // the lane stops right after -- so no branch per sequence)
-                    if (JFS_ZSEQ_NEXTALL || i + 1 < d.nseq) {
-#if JFS_ZSEQ_XALIGN
+                    {
                         // the 32 bits below position left - c: bits [u, u + 32) of d0..d3
                         const uint32_t u = (uint32_t)(tw + 32 - c), wsel = u >> 5;
                         const uint32_t lo_d = wsel == 0 ? d0 : wsel == 1 ? d1 : d2;
                         const uint32_t hi_d = wsel == 0 ? d1 : wsel == 1 ? d2 : d3;
                         const uint64_t h2 = (uint64_t)__builtin_amdgcn_alignbit(hi_d, lo_d, u & 31u) << 32;
-#else
-                        const uint64_t h2 = zw_shift(hi, lo, c);
-#endif
                         const uint32_t nsl = cl >> 6, nso = co >> 6, nsm = cm >> 6;
                         const uint32_t nbl = kl31 + (uint32_t)__builtin_clz(nsl);
                         const uint32_t nbm = km31 + (uint32_t)__builtin_clz(nsm);
                         const uint32_t nbo = ko31 + (uint32_t)__builtin_clz(nso);
-#if JFS_ZSEQ_STATE32
                         // the three state reads (<= 9 + 9 + 8 bits) all lie in the
                         // window's top 32 bits: one extraction, three field reads
                         const uint32_t x = (uint32_t)(h2 >> 32);
@@ -2482,12 +1671,7 @@ __device__ __forceinline__ void zdecode(SeqSmem &sm, int gn, uint32_t &r0, uint3
                         sll = ((nsl << nbl) - szl) + __builtin_amdgcn_ubfe(x, ol, nbl);
                         sml = ((nsm << nbm) - szm) + __builtin_amdgcn_ubfe(x, om, nbm);
                         sof = ((nso << nbo) - szo) + __builtin_amdgcn_ubfe(x, oo, nbo);
-                        c2 = JFS_ZSEQ_NEXTALL && i + 1 >= d.nseq ? 0 : (int32_t)(32u - oo);
-#else
-                        sll = ((nsl << nbl) - szl) + zw_get(h2, c2, nbl);
-                        sml = ((nsm << nbm) - szm) + zw_get(h2, c2, nbm);
-                        sof = ((nso << nbo) - szo) + zw_get(h2, c2, nbo);
-#endif
+                        c2 = i + 1 >= d.nseq ? 0 : (int32_t)(32u - oo);
                     }
                     left -= c + c2;
                     ++i;
@@ -2522,147 +1706,6 @@ __device__ __forceinline__ void zdecode(SeqSmem &sm, int gn, uint32_t &r0, uint3
     }
     { const uint64_t t = ZP_NOW(); ZS_ADD(2, t - zt); }
 }
-#else
-// Wave 0: phase B for the group (lane = block), tables and bitstreams in LDS.
-__device__ __forceinline__ void zdecode(SeqSmem &sm, int gn, uint32_t &r0, uint32_t &r1, uint32_t &r2,
-                                        uint32_t &brep) {
-    const int l = lane_id();
-    const bool mine = l < gn;
-    const GBlk d = sm.g[mine ? l : 0];
-    const ZGeo g = zgeo(d);
-    const uint8_t *ring = sm.bring[l < ZNB ? l : 0];
-    const uint16_t *tl = sm.arena[l < ZNB ? l : 0], *to = tl + 512, *tm = tl + 768;
-    const int32_t all = d.al & 0xFF, alof = (d.al >> 8) & 0xFF, alml = (d.al >> 16) & 0xFF;
-    const int32_t m8 = 8 * g.m;
-    g_u4 *it = d.ib + d.item;
-    zsync();  // the mover has staged the tables and prefilled the rings
-    [[maybe_unused]] uint64_t zt = ZP_NOW();
-    bool run = false;
-    int32_t left = 0, i = 0;
-    uint32_t sll = 0, sof = 0, sml = 0;
-    if (mine) {
-        if (d.nseq == 0) {
-            it[1] = make_uint4(0, 0, 0, IT_BREP);
-            it[2] = make_uint4(0, 0, 0, IT_BEND);
-            brep = 1;
-        } else {
-            const uint32_t last = d.bsz > 0 ? ring[(g.top - 1) & (ZRB2 - 1)] : 0u;
-            if (last == 0) {
-                it[1] = make_uint4(0, 0, (uint32_t)E_CORRUPT, IT_ERR);
-            } else {
-                brep = 1;
-                run = true;
-                left = 8 * (g.top - 1) + (31 - __builtin_clz(last));
-            }
-        }
-    }
-    if (run) {
-        uint64_t hi;
-        uint32_t lo;
-        zw_fill(ring, left, hi, lo);
-        int32_t c = 0;
-        sll = zw_get(hi, c, all);
-        sof = zw_get(hi, c, alof);
-        sml = zw_get(hi, c, alml);
-        left -= c;
-    }
-    const uint32_t szl = 1u << all, szo = 1u << alof, szm = 1u << alml;
-    const uint32_t kl31 = (uint32_t)all - 31u, ko31 = (uint32_t)alof - 31u, km31 = (uint32_t)alml - 31u;
-    g_u4 *itp = it + 2;  // the next sequence's item
-    for (int p = 0;; ++p) {
-#if JFS_ZUNROLL
-#pragma unroll
-#endif
-        for (int k = 0; k < ZK2; ++k) {
-            if (run) {
-                if (left < m8) {  // overflow
-                    *itp = make_uint4(0, 0, (uint32_t)E_CORRUPT, IT_ERR);
-                    run = false;
-                } else {
-                    const uint32_t cl = tl[sll], co = to[sof], cm = tm[sml];
-                    uint64_t hi;
-                    uint32_t lo;
-                    zw_fill(ring, left, hi, lo);
-                    const uint32_t lv = sm.lut_ll[cl & 63], mv = sm.lut_ml[cm & 63], ofc = co & 63;
-                    int32_t c = 0;
-                    const uint32_t ofv = (1u << ofc) + zw_get(hi, c, ofc);
-                    const uint32_t ml = (mv & 0xFFFFFFu) + zw_get(hi, c, mv >> 24);
-                    const uint32_t ll = (lv & 0xFFFFFFu) + zw_get(hi, c, lv >> 24);
-                    // repeat offsets (RFC 8878 3.1.2.5), branch-free: kk 0..2 = rep
-                    // 1..3 (shifted when ll == 0), 3 = rep1 - 1, 4 = a new offset
-#if JFS_ZREP_BR
-                    uint32_t off;
-                    if (ofv > 3) {
-                        off = ofv - 3;
-                        r2 = r1; r1 = r0; r0 = off;
-                    } else {
-                        const uint32_t kk = ofv - 1 + (ll == 0 ? 1u : 0u);
-                        if (kk == 0) {
-                            off = r0;
-                        } else {
-                            const uint32_t t = kk == 1 ? r1 : kk == 2 ? r2 : rep_dec(r0);
-                            if (kk != 1) r2 = r1;
-                            r1 = r0;
-                            r0 = t;
-                            off = t;
-                        }
-                    }
-#elif JFS_ZREP_BR == 2
-                    // select by masks (no exec-mask branches)
-                    const uint32_t kk = ofv > 3 ? 4u : ofv - 1 + (ll == 0 ? 1u : 0u);
-                    const uint32_t rd0 = (r0 & SYMB) ? r0 + 1 : umax32(r0 - 1, 1u);
-                    const uint32_t m0 = 0u - (uint32_t)(kk == 0), m1 = 0u - (uint32_t)(kk == 1),
-                                   m2 = 0u - (uint32_t)(kk == 2), m3 = 0u - (uint32_t)(kk == 3),
-                                   m4 = 0u - (uint32_t)(kk == 4);
-                    const uint32_t off = (r0 & m0) | (r1 & m1) | (r2 & m2) | (rd0 & m3) | ((ofv - 3) & m4);
-                    const uint32_t ge2 = m2 | m3 | m4, ge1 = ge2 | m1;
-                    r2 = (r1 & ge2) | (r2 & ~ge2);
-                    r1 = (r0 & ge1) | (r1 & ~ge1);
-                    r0 = off;
-#else
-                    const uint32_t kk = ofv > 3 ? 4u : ofv - 1 + (ll == 0 ? 1u : 0u);
-                    const uint32_t rd0 = (r0 & SYMB) ? r0 + 1 : (r0 - 1 == 0 ? 1u : r0 - 1);
-                    const uint32_t off = kk == 0 ? r0 : kk == 1 ? r1 : kk == 2 ? r2 : kk == 3 ? rd0 : ofv - 3;
-                    r2 = kk >= 2 ? r1 : r2;
-                    r1 = kk >= 1 ? r0 : r1;
-                    r0 = off;
-#endif
-                    if (i + 1 < d.nseq) {
-                        const uint64_t h2 = zw_shift(hi, lo, c);
-                        int32_t c2 = 0;
-                        const uint32_t nsl = cl >> 6, nso = co >> 6, nsm = cm >> 6;
-                        // nb = al - highbit(ns) = (al - 31) + clz(ns)
-                        const uint32_t nbl = kl31 + (uint32_t)__builtin_clz(nsl);
-                        const uint32_t nbm = km31 + (uint32_t)__builtin_clz(nsm);
-                        const uint32_t nbo = ko31 + (uint32_t)__builtin_clz(nso);
-                        sll = ((nsl << nbl) - szl) + zw_get(h2, c2, nbl);
-                        sml = ((nsm << nbm) - szm) + zw_get(h2, c2, nbm);
-                        sof = ((nso << nbo) - szo) + zw_get(h2, c2, nbo);
-                        c += c2;
-                    }
-                    left -= c;
-                    itp[0] = make_uint4(ll, ml, off, IT_SEQ);
-                    if (i + 1 == d.nseq) {
-                        itp[1] = left == m8 ? make_uint4(0, 0, 0, IT_BEND) : make_uint4(0, 0, (uint32_t)E_CORRUPT, IT_ERR);
-                        run = false;
-                    }
-                    ++i;
-                    ++itp;
-                }
-            }
-        }
-        if (l < ZNB) sm.pos[p & 1][l] = left;
-        const bool any = __ballot(run) != 0;
-        if (l == 0) sm.more[p & 1] = any ? 1 : 0;
-        [[maybe_unused]] const uint64_t tw = ZP_NOW();
-        zsync();
-        ZS_ADD(4, ZP_NOW() - tw);
-        if (!any) break;
-    }
-    { const uint64_t t = ZP_NOW(); ZS_ADD(2, t - zt); }
-}
-
-#endif  // JFS_ZSEQ_AB
 
 // phases B (both waves) and C (wave 0) for the collected group
 // carry slot of a split input: 16 bytes after the ZDesc of block ZNB - 1
@@ -2711,9 +1754,7 @@ __device__ __forceinline__ void seq_group2(SeqSmem &sm, int gn, uint32_t *e0, ui
     __builtin_amdgcn_wave_barrier();
     { const uint64_t t = ZP_NOW(); ZS_ADD(3, t - zt); }
 }
-#endif  // JFS_ZSEQ_V2
 
-#if JFS_ZSEQ_V2
 // zseqa (phase A): one wave per input walks the headers, builds each
 // compressed block's FSE tables into its HBM table area and writes the
 // block's ZDesc after them; zseqb decodes the sequences.
@@ -2784,20 +1825,14 @@ __global__ __launch_bounds__(64) void zseqa_kernel(const jfs_dev_block *__restri
             if (cblk >= cap_cblk || slot + 3 + (uint32_t)nseq > cap_items) { bug = 1; break; }
             const uint32_t area = cblk * TAB_STRIDE;
             cblk++;
-            uint32_t rs = 0;  // deferred builds (JFS_ZSEQA_DEFER)
+            uint32_t rs = 0;  // deferred table builds (zbuild)
             if (nseq > 0) {
                 if (ip + 1 > end) { put(0, 0, (uint32_t)E_SRCSIZE, IT_ERR); break; }
                 uint32_t modes = rd8(s, ip++);
                 if ((modes & 3) && strict_reserved) { put(0, 0, (uint32_t)E_CORRUPT, IT_ERR); break; }
-#if JFS_ZSEQA_DEFER
                 int32_t c = seq_table_defer(sm, tabs, area, &t_ll, &al_ll, &hv_ll, modes >> 6, s, ip, end - ip, 0, &rs);
                 if (c >= 0) { ip += c; c = seq_table_defer(sm, tabs, area + 512, &t_of, &al_of, &hv_of, (modes >> 4) & 3, s, ip, end - ip, 1, &rs); }
                 if (c >= 0) { ip += c; c = seq_table_defer(sm, tabs, area + 768, &t_ml, &al_ml, &hv_ml, (modes >> 2) & 3, s, ip, end - ip, 2, &rs); }
-#else
-                int32_t c = seq_table_g(sm, tabs, area, &t_ll, &al_ll, &hv_ll, modes >> 6, s, ip, end - ip, 0);
-                if (c >= 0) { ip += c; c = seq_table_g(sm, tabs, area + 512, &t_of, &al_of, &hv_of, (modes >> 4) & 3, s, ip, end - ip, 1); }
-                if (c >= 0) { ip += c; c = seq_table_g(sm, tabs, area + 768, &t_ml, &al_ml, &hv_ml, (modes >> 2) & 3, s, ip, end - ip, 2); }
-#endif
                 if (c < 0) { put(0, 0, (uint32_t)E_CORRUPT, IT_ERR); break; }
                 ip += c;
             }
@@ -2811,9 +1846,7 @@ __global__ __launch_bounds__(64) void zseqa_kernel(const jfs_dev_block *__restri
                 d.al = (uint32_t)al_ll | ((uint32_t)al_of << 8) | ((uint32_t)al_ml << 16) | ((uint32_t)first << 24);
                 d.rsv = rs;
                 *(JFS_GLOBAL ZDesc *)(tabs + area + TAB_CELLS) = d;
-#if JFS_ZSEQ_HALF
                 *(JFS_GLOBAL uint4 *)(tabs + area + TAB_CELLS + 24) = make_uint4(0, 0, 0, 0);  // carry slot
-#endif
             }
             first = 0;
             cur = slot + 3 + (uint32_t)nseq;
@@ -2827,13 +1860,9 @@ __global__ __launch_bounds__(64) void zseqa_kernel(const jfs_dev_block *__restri
     ZS_ADD(0, ZP_NOW() - za);
 }
 
-#if JFS_ZSEQA_DEFER
 // zbuild: spreads the FSE tables zseqa left described.  Grid (inputs, ZBUILD_Q):
 // workgroup (i, q) takes tables q, q + Q, ... of input i (three per block).
-#ifndef JFS_ZBUILD_Q
-#define JFS_ZBUILD_Q 16
-#endif
-constexpr int ZBUILD_Q = JFS_ZBUILD_Q;
+constexpr int ZBUILD_Q = 16;
 __global__ __launch_bounds__(64) void zbuild_kernel(int nblk, const ZInfo *__restrict__ info,
                                                     uint16_t *__restrict__ tabs_all) {
     __shared__ uint8_t symat[512], mark[512], ksym[512];
@@ -2864,16 +1893,11 @@ __global__ __launch_bounds__(64) void zbuild_kernel(int nblk, const ZInfo *__res
         }
     }
 }
-#endif
-
 
 // zseqb (phases B and C): wave 0 gathers ZNB blocks' descriptors at a time
 // (in stream order over the workgroup's inputs), decodes their sequences
 // with wave 1 keeping the tables and bitstreams in LDS, then resolves the
 // symbolic repeat offsets in block order.
-#ifndef JFS_ZSEQ_DPRIO
-#define JFS_ZSEQ_DPRIO 0
-#endif
 __global__ __launch_bounds__(128) void zseqb_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
                                                     ZInfo *__restrict__ info, uint16_t *__restrict__ tabs_all,
                                                     uint4 *__restrict__ items_all) {
@@ -2892,12 +1916,8 @@ __global__ __launch_bounds__(128) void zseqb_kernel(const jfs_dev_block *__restr
         }
         return;
     }
-#if JFS_ZSEQ_DPRIO
-    __builtin_amdgcn_s_setprio(JFS_ZSEQ_DPRIO);  // the decoder wave is the critical one of the pair
-#endif
     int gn = 0;
     uint32_t e0 = 1, e1 = 4, e2 = 8;  // repeat offsets carried through phase C (reset at each frame)
-#if JFS_ZSEQ_HALF
     // two workgroups per input: blocks [0, ZNB) and [ZNB, n); the second
     // takes its entry repeat offsets from the first at its first phase C
     const int bi = blockIdx.x >> 1, half = blockIdx.x & 1;
@@ -2939,206 +1959,25 @@ __global__ __launch_bounds__(128) void zseqb_kernel(const jfs_dev_block *__restr
     if (l == 0) sm.cmd = 0;
     zsync();  // releases the mover
 }
-#else
-    for (int f = 0; f < ZSEQ_INPUTS; ++f) {
-        const int bi = blockIdx.x * ZSEQ_INPUTS + f;
-        if (bi >= nblk) break;
-        const ZInfo zi = info[bi];
-        if (zi.ovf || zi.n_items == 0xFFFFFFFFu) continue;
-        const gc_u16 *tabs = (const gc_u16 *)tabs_all + zi.tab_off;
-        g_u4 *items = (g_u4 *)items_all + zi.item_off;
-        for (uint32_t j = 0; j < zi.n_sblk;) {
-            const uint32_t take = umin32((uint32_t)(ZNB - gn), zi.n_sblk - j);
-            if ((uint32_t)l < take) {
-                const ZDesc d = *(const JFS_GLOBAL ZDesc *)(tabs + (uint64_t)(j + l) * TAB_STRIDE + TAB_CELLS);
-                GBlk &g = sm.g[gn + l];
-                g.bs = (const gc_u8 *)(uintptr_t)d.bs;
-                g.in = g.bs;
-                g.ib = items;
-                g.bsz = d.bsz;
-                g.nseq = d.nseq;
-                g.item = d.item;
-                g.tll = zi.tab_off + d.tll; g.tof = zi.tab_off + d.tof; g.tml = zi.tab_off + d.tml;
-                g.al = d.al;
-            }
-            __builtin_amdgcn_wave_barrier();
-            gn += (int)take;
-            j += take;
-            if (gn == ZNB) {
-                if (l == 0) sm.cmd = gn;
-                zsync();
-                seq_group2(sm, gn, &e0, &e1, &e2);
-                gn = 0;
-            }
-        }
-    }
-    if (gn) {
-        if (l == 0) sm.cmd = gn;
-        zsync();
-        seq_group2(sm, gn, &e0, &e1, &e2);
-    }
-    if (l == 0) sm.cmd = 0;
-    zsync();  // releases the mover
-}
-#endif  // JFS_ZSEQ_HALF
-#else
-__global__ __launch_bounds__(64) void zseq_kernel(const jfs_dev_block *__restrict__ blocks, int nblk,
-                                                      ZInfo *__restrict__ info, uint16_t *__restrict__ tabs_all,
-                                                      uint4 *__restrict__ items_all, int strict_reserved) {
-    __shared__ SeqSmem sm;
-    const int l = lane_id();
-    for (int i = l; i < 36; i += 64) sm.lut_ll[i] = LL_BASE[i] | ((uint32_t)LL_BITS[i] << 24);
-    for (int i = l; i < 53; i += 64) sm.lut_ml[i] = ML_BASE[i] | ((uint32_t)ML_BITS[i] << 24);
-    auto flush = [&](int gn, uint32_t *e0, uint32_t *e1, uint32_t *e2) {
-        seq_group(sm, gn, (const gc_u16 *)tabs_all, e0, e1, e2);
-    };
-    int gn = 0;
-    uint32_t e0 = 1, e1 = 4, e2 = 8;  // repeat offsets carried through phase C (reset at each frame)
-    [[maybe_unused]] uint64_t za = ZP_NOW();
-    for (int f = 0; f < ZSEQ_INPUTS; ++f) {
-        const int bi = blockIdx.x * ZSEQ_INPUTS + f;
-        if (bi >= nblk) break;
-        const jfs_dev_block b = blocks[bi];
-        ZInfo &zi = info[bi];
-        if (zi.ovf) continue;
-        const gc_u8 *s = (const gc_u8 *)b.src;
-        g_u16 *tabs = (g_u16 *)tabs_all + zi.tab_off;
-        g_u4 *items = (g_u4 *)items_all + zi.item_off;
-        Walk w;
-        walk_init(w, s, b.src_len, b.dst_cap);
-        const uint32_t cap_items = zi.n_items, cap_cblk = zi.n_cblk;
-        uint32_t cur = 0, cblk = 0;  // next item slot, next table area
-        int first = 0, bug = 0;
-        uint32_t t_ll = 0, t_of = 0, t_ml = 0;
-        int32_t al_ll = 0, al_of = 0, al_ml = 0, hv_ll = 0, hv_of = 0, hv_ml = 0;
-        auto put = [&](uint32_t x, uint32_t y, uint32_t z, uint32_t kind) {
-            if (cur >= cap_items) { bug = 1; return; }
-            if (l == 0) items[cur] = make_uint4(x, y, z, kind);
-            cur++;
-        };
-        for (;;) {
-            int32_t err = 0;
-            uint32_t fl = 0, chk = 0;
-            int ev = walk_next(w, &err, &fl, &chk);
-            if (ev == EV_DONE) break;
-            if (ev == EV_ERROR) { put(0, 0, (uint32_t)err, IT_ERR); break; }
-            if (ev == EV_FSTART) {
-                hv_ll = hv_of = hv_ml = 0;
-                first = 1;
-                put(0, 0, 0, IT_FSTART);
-                continue;
-            }
-            if (ev == EV_FEND) {
-                put((uint32_t)w.fcs, (uint32_t)(w.fcs >> 32), chk, IT_FEND | (fl << 8));
-                if (fl & FE_MISSING) break;
-                continue;
-            }
-            const uint32_t ord = w.ordinal - 1;
-            if (w.btype != 2) {
-                put(ord, (uint32_t)w.bsize, 0, IT_BSTART);
-                put((uint32_t)w.bsize, 0, 0, IT_SEQ);
-                put(0, 0, 0, IT_BEND);
-                w.lb += w.bsize;
-                continue;
-            }
-            LitHdr h;
-            int32_t e = lit_header(s, w.bpos, w.bsize, h);
-            const uint32_t slot = cur;
-            put(ord, e ? 0u : (uint32_t)h.regen, 0, IT_BSTART);
-            if (e) { put(0, 0, (uint32_t)e, IT_ERR); break; }
-            const int32_t end = w.bpos + w.bsize;
-            int32_t ip = w.bpos + h.sec;
-            int32_t nseq = 0, used = 0;
-            e = nbseq_header(s, ip, end, &nseq, &used);
-            if (e) { put(0, 0, (uint32_t)e, IT_ERR); break; }
-            ip += used;
-            w.lb += (int64_t)h.regen + 3 * (int64_t)nseq;
-            if (cblk >= cap_cblk || slot + 3 + (uint32_t)nseq > cap_items) { bug = 1; break; }
-            const uint32_t area = cblk * TAB_STRIDE;
-            cblk++;
-            if (nseq > 0) {
-                if (ip + 1 > end) { put(0, 0, (uint32_t)E_SRCSIZE, IT_ERR); break; }
-                uint32_t modes = rd8(s, ip++);
-                if ((modes & 3) && strict_reserved) { put(0, 0, (uint32_t)E_CORRUPT, IT_ERR); break; }
-                int32_t c = seq_table_g(sm, tabs, area, &t_ll, &al_ll, &hv_ll, modes >> 6, s, ip, end - ip, 0);
-                if (c >= 0) { ip += c; c = seq_table_g(sm, tabs, area + 512, &t_of, &al_of, &hv_of, (modes >> 4) & 3, s, ip, end - ip, 1); }
-                if (c >= 0) { ip += c; c = seq_table_g(sm, tabs, area + 768, &t_ml, &al_ml, &hv_ml, (modes >> 2) & 3, s, ip, end - ip, 2); }
-                if (c < 0) { put(0, 0, (uint32_t)E_CORRUPT, IT_ERR); break; }
-                ip += c;
-            }
-            if (l == 0) {
-                GBlk &d = sm.g[gn];
-                d.bs = s + ip;
-                d.in = s;
-                d.ib = items;
-                d.bsz = end - ip;
-                d.nseq = nseq;
-                d.item = slot;
-                d.tll = zi.tab_off + t_ll; d.tof = zi.tab_off + t_of; d.tml = zi.tab_off + t_ml;
-                d.al = (uint32_t)al_ll | ((uint32_t)al_of << 8) | ((uint32_t)al_ml << 16) | ((uint32_t)first << 24);
-            }
-            first = 0;
-            cur = slot + 3 + (uint32_t)nseq;
-            gn++;
-            if (gn == 64) {
-                ZS_ADD(0, ZP_NOW() - za);
-                flush(gn, &e0, &e1, &e2);
-                za = ZP_NOW();
-                gn = 0;
-            }
-        }
-        if (l == 0) zi.n_items = bug ? 0xFFFFFFFFu : cur;
-    }
-    ZS_ADD(0, ZP_NOW() - za);
-    if (gn) flush(gn, &e0, &e1, &e2);
-    wait_vm();
-}
-
-#endif  // JFS_ZSEQ_V2
 
 // ---------------------------------------------------------------------------
 // kernel 3: execute items
 // ---------------------------------------------------------------------------
-#ifndef JFS_ZEXEC_V2
-#define JFS_ZEXEC_V2 1  // batches as in the LZ4 copier (lz4_decode.hip batch()): zeroed span + OR'd 16-byte steps
-#endif
-#if JFS_ZEXEC_V2
 // V2 needs no far-source buffer: the ring takes its 4 KiB (sources up to 8 KiB
 // back stay in LDS; fewer far matches, rarer waits for flushed output)
 constexpr int R = 8192;
-#else
-constexpr int R = 4096;
-#endif
 constexpr int RMASK = R - 1;
 constexpr int LW = 2048;          // literal staging window
 constexpr int FLUSH_T = 1024;
 
-constexpr int CH = 256;           // output chunk of the parallel gather (4 bytes per lane)
-
-constexpr int FB = 64;           // far-source prefetch bytes per lane (16 B alignment slack)
-constexpr int FBUSE = FB - 16;
 constexpr int BSPAN = 2048;      // max output span of one lane-parallel batch
 static_assert(BSPAN <= R / 2, "a batch span and the unflushed tail fit the ring");
-#if JFS_ZEXEC_V2
-#ifndef JFS_ZLONGI
-#define JFS_ZLONGI 64
-#endif
-constexpr int LONGI = JFS_ZLONGI;  // items with a literal run or match longer than this go whole-wave
-#else
-constexpr int LONGI = 1024;      // items longer than this are copied by the whole wave
-#endif
-#ifndef JFS_ZEXEC_LEVELS
-#define JFS_ZEXEC_LEVELS 0  // 1: near matches in dependency rounds (binary search over lanes); measured slower (119 vs 114 ms)
-#endif
-#ifndef JFS_ZEXEC_NEARSER
-#define JFS_ZEXEC_NEARSER 1  // near matches: one lane-parallel round, the rest by the whole wave in order
-#endif
+constexpr int LONGI = 64;  // items with a literal run or match longer than this go whole-wave
 
 // 10,240 bytes: 16 workgroups (one per frame of a 4,096-frame launch) fit a
 // CU's 160 KiB, so a launch is one round (at 10,304 bytes it was 15 per CU and
 // the 256 leftover frames ran as a second round).  Over-reads past lw and
 // farbuf (dword/alignbyte tails) only fetch bytes that are never used.
-#if JFS_ZEXEC_V2
 struct XSmem {
     alignas(16) uint8_t ring[R];
     union {
@@ -3146,16 +1985,6 @@ struct XSmem {
         uint64_t xxh[4];             // frame checksum (between batches)
     };
 };
-#else
-struct XSmem {
-    alignas(16) uint8_t ring[R];
-    alignas(16) uint8_t lw[LW];
-    union {
-        alignas(16) uint8_t farbuf[64 * FB];  // within a batch
-        uint64_t xxh[4];                      // frame checksum (between batches)
-    };
-};
-#endif
 static_assert(sizeof(XSmem) * 16 <= 160 * 1024, "16 zexec workgroups per CU");
 
 struct X {
@@ -3273,92 +2102,6 @@ __device__ __forceinline__ uint64_t xxh64_dev(XSmem &s, const gc_u8 *p, int64_t 
     return h;
 }
 
-// ---------------------------------------------------------------------------
-// lane-per-item copy engine.  A batch is <= 64 consecutive sequence items,
-// one per lane, producing output [O0, O1) with O1 - O0 <= BSPAN.  Literal
-// runs copy first (their source is the staged literal window); matches then
-// copy in rounds: a match is ready once every output byte below its source
-// end is final, i.e. its source ends at or below the earliest still-pending
-// match start.  Copies move 4 bytes per step (LDS dword pair + alignbyte,
-// byte-granular ring writes).  Sources that the batch's own ring writes could
-// overwrite (below O1 - R) are read from HBM; for those the first FBUSE bytes
-// are prefetched into LDS before the literal copies.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t ld4(const uint8_t *base, uint32_t a) {
-    const uint32_t a0 = a & ~3u;
-    const uint32_t d0 = *(const uint32_t *)(base + a0), d1 = *(const uint32_t *)(base + a0 + 4);
-    return __builtin_amdgcn_alignbyte(d1, d0, a & 3u);
-}
-// 4 bytes at source byte address a (any alignment): linear LDS buffer or ring slot space
-template <bool RING>
-__device__ __forceinline__ uint32_t ld4r(const XSmem &s, const uint8_t *base, uint32_t a) {
-    const uint32_t a0 = a & ~3u;
-    uint32_t d0, d1;
-    if (RING) {
-        d0 = *(const uint32_t *)(s.ring + (a0 & RMASK));
-        d1 = *(const uint32_t *)(s.ring + ((a0 + 4) & RMASK));
-    } else {
-        d0 = *(const uint32_t *)(base + a0);
-        d1 = *(const uint32_t *)(base + a0 + 4);
-    }
-    return __builtin_amdgcn_alignbyte(d1, d0, a & 3u);
-}
-__device__ __forceinline__ uint32_t hbm4(const X &x, int32_t pos) {
-    const uintptr_t a = (uintptr_t)(x.dst + pos);
-    const gc_u32 *q = (const gc_u32 *)(a & ~(uintptr_t)3);
-    return __builtin_amdgcn_alignbyte(q[1], q[0], (uint32_t)(a & 3));
-}
-__device__ __forceinline__ void put4(XSmem &s, const X &x, int32_t o, uint32_t w, int32_t n) {
-    s.ring[slot(x, o)] = (uint8_t)w;
-    if (n > 1) s.ring[slot(x, o + 1)] = (uint8_t)(w >> 8);
-    if (n > 2) s.ring[slot(x, o + 2)] = (uint8_t)(w >> 16);
-    if (n > 3) s.ring[slot(x, o + 3)] = (uint8_t)(w >> 24);
-}
-// source dword at byte address a (4-aligned) of a linear LDS buffer or of the ring
-template <bool RING>
-__device__ __forceinline__ uint32_t sdw(const XSmem &s, const uint8_t *base, uint32_t a) {
-    if (RING) return *(const uint32_t *)(s.ring + (a & RMASK));
-    return *(const uint32_t *)(base + a);
-}
-// Copy n bytes from source byte address sa (linear LDS buffer, or ring slot
-// space when RING) to output [o, o+n).  Source bytes must be final before the
-// copy, or lie >= 16 bytes (STEP16) / >= 4 bytes before each destination byte.
-// Destination: head bytes, then aligned dwords (16 bytes per step), then tail.
-template <bool RING>
-__device__ __forceinline__ void cp_run(XSmem &s, const X &x, const uint8_t *base, uint32_t sa, int32_t o, int32_t n,
-                                       bool step16) {
-    const uint32_t da = slot(x, o) & 3u;
-    int32_t head = (int32_t)((4u - da) & 3u);
-    head = head < n ? head : n;
-    if (head) put4(s, x, o, ld4r<RING>(s, base, sa), head);
-    int32_t k = head;
-    if (step16) {
-        for (; k + 16 <= n; k += 16) {
-            const uint32_t b = sa + (uint32_t)k, b0 = b & ~3u, sh = b & 3u;
-            const uint32_t r0 = sdw<RING>(s, base, b0), r1 = sdw<RING>(s, base, b0 + 4), r2 = sdw<RING>(s, base, b0 + 8),
-                           r3 = sdw<RING>(s, base, b0 + 12), r4 = sdw<RING>(s, base, b0 + 16);
-            const uint32_t d = slot(x, o + k);
-            *(uint32_t *)(s.ring + d) = __builtin_amdgcn_alignbyte(r1, r0, sh);
-            *(uint32_t *)(s.ring + ((d + 4) & RMASK)) = __builtin_amdgcn_alignbyte(r2, r1, sh);
-            *(uint32_t *)(s.ring + ((d + 8) & RMASK)) = __builtin_amdgcn_alignbyte(r3, r2, sh);
-            *(uint32_t *)(s.ring + ((d + 12) & RMASK)) = __builtin_amdgcn_alignbyte(r4, r3, sh);
-        }
-    }
-    for (; k + 4 <= n; k += 4) *(uint32_t *)(s.ring + slot(x, o + k)) = ld4r<RING>(s, base, sa + (uint32_t)k);
-    if (k < n) put4(s, x, o + k, ld4r<RING>(s, base, sa + (uint32_t)k), n - k);
-}
-__device__ __forceinline__ void cp_lds(XSmem &s, const X &x, const uint8_t *base, uint32_t a, int32_t o, int32_t n) {
-    cp_run<false>(s, x, base, a, o, n, true);
-}
-__device__ __forceinline__ void cp_ring(XSmem &s, const X &x, int32_t src, int32_t o, int32_t n, uint32_t off) {
-    if (off >= 4) {
-        cp_run<true>(s, x, nullptr, slot(x, src), o, n, off >= 16);
-    } else {
-        for (int32_t k = 0; k < n; k++) s.ring[slot(x, o + k)] = s.ring[slot(x, src + k)];
-    }
-}
-
-#if JFS_ZEXEC_V2
 // ---------------------------------------------------------------------------
 // V2 batch: the LZ4 copier's scheme (lz4_decode.hip batch()).
 // The batch's ring span is zeroed, then every write is an LDS atomic OR of
@@ -3557,138 +2300,6 @@ __device__ __forceinline__ void x_batch2(XSmem &s, X &x, bool act, int32_t o, ui
     }
     XP_ADD(4, ZP_NOW() - tq3);
 }
-#endif
-
-#if !JFS_ZEXEC_V2
-__device__ __forceinline__ void x_batch(XSmem &s, X &x, bool act, int32_t o, uint32_t ll, uint32_t ml, uint32_t off,
-                                        int32_t lit, int32_t O0, int32_t O1) {
-    const int l = lane_id();
-    const int32_t hz = O1 - R;  // sources below hz come from HBM
-    uint64_t tq0 = ZP_NOW();
-    if (O0 - x.F >= FLUSH_T) xflush_line(s, x, O0, false);
-    if (hz > x.Fw) { wait_vm(); x.Fw = x.F; }
-    const int32_t ms = o + (int32_t)ll, msrc = ms - (int32_t)off;
-    const bool hasm = act && ml > 0;
-    // bytes [msrc, msrc + nfar) come from HBM (far part), the rest from the ring
-    int32_t nfar = hasm && msrc < hz ? (msrc + (int32_t)ml <= hz ? (int32_t)ml : hz - msrc) : 0;
-    const bool far = nfar > 0;
-    const int32_t fsnap = x.F;
-    // far prefetch, first pass (4 x 16 B, aligned) into this lane's farbuf slot
-    uint4 f0 = make_uint4(0, 0, 0, 0), f1 = f0, f2 = f0, f3 = f0;
-    const uintptr_t fa = (uintptr_t)(x.dst + msrc);
-    if (far) {
-        const gc_u4 *q = (const gc_u4 *)(fa & ~(uintptr_t)15);
-        f0 = q[0]; f1 = q[1]; f2 = q[2]; f3 = q[3];
-    }
-    uint64_t tq1 = ZP_NOW();
-    // round 0: literal runs
-    if (act) cp_lds(s, x, s.lw, (uint32_t)(lit - (int32_t)x.lw0), o, (int32_t)ll);
-    uint64_t tq2 = ZP_NOW();
-    if (__ballot(far)) {
-        uint4 *fb = (uint4 *)(s.farbuf + FB * l);
-        if (far) { fb[0] = f0; fb[1] = f1; fb[2] = f2; fb[3] = f3; }
-        if (fsnap > x.Fw) x.Fw = fsnap;  // the prefetch was waited for: earlier flushes are complete
-    }
-    __builtin_amdgcn_wave_barrier();
-    uint64_t tq3 = ZP_NOW();
-    XP_ADD(1, tq1 - tq0);
-    XP_ADD(2, tq2 - tq1);
-    XP_ADD(3, tq3 - tq2);
-    XP_ADD(5, 1);
-    // far parts: FBUSE bytes per pass through the farbuf, all far lanes together
-    if (__ballot(far)) {
-        int32_t done = 0;
-        for (;;) {
-            const int32_t n1 = nfar - done < FBUSE ? nfar - done : FBUSE;
-            if (far && n1 > 0)
-                cp_lds(s, x, s.farbuf, (uint32_t)(FB * l) + (uint32_t)((fa + (uintptr_t)done) & 15), ms + done, n1);
-            done += FBUSE;
-            const bool more = far && done < nfar;
-            if (!__ballot(more)) break;
-            if (more) {
-                const gc_u4 *q = (const gc_u4 *)((fa + (uintptr_t)done) & ~(uintptr_t)15);
-                uint4 *fb = (uint4 *)(s.farbuf + FB * l);
-                uint4 g0 = q[0], g1 = q[1], g2 = q[2], g3 = q[3];
-                fb[0] = g0; fb[1] = g1; fb[2] = g2; fb[3] = g3;
-            }
-            __builtin_amdgcn_wave_barrier();
-        }
-    }
-    // matches (ring parts)
-    bool pend = hasm && nfar < (int32_t)ml;
-    const int32_t ms2 = ms + nfar, msrc2 = msrc + nfar, ml2 = (int32_t)ml - nfar;
-#if JFS_ZEXEC_NEARSER
-    // one lane-parallel round for every match whose source is final (far, or
-    // wholly before the batch), then the rest by the whole wave in lane order
-    // (output order: every source is final when its match's turn comes)
-    {
-        const int32_t send = msrc + (int32_t)ml < ms ? msrc + (int32_t)ml : ms;
-        const bool ready = pend && (far || send <= O0);
-        if (ready) {
-            cp_ring(s, x, msrc2, ms2, ml2, off);
-            pend = false;
-        }
-        __builtin_amdgcn_wave_barrier();
-        XP_ADD(6, 1);
-#if JFS_ZEXEC_LEVELS
-        // dependency rounds: a pending match goes when no still-pending match
-        // of an earlier lane writes into its source.  Pending match regions are
-        // disjoint and in lane order, so with M = prefix max of their ends the
-        // first lane whose M passes this lane's source start is the only
-        // candidate (binary search over lanes with ds_bpermute).  The lowest
-        // pending lane always goes, so rounds <= pending lanes.
-        for (int guard2 = 0; __ballot(pend); ++guard2) {
-            const uint32_t pe = pend ? (uint32_t)(ms2 + ml2) : 0u;
-            const uint32_t M = dpp_scan_max(pe);
-            const int32_t sendp = msrc2 + ml2 < ms2 ? msrc2 + ml2 : ms2;
-            int32_t pos = 0;
-#pragma unroll
-            for (int st = 32; st; st >>= 1) {
-                const int32_t q = pos + st - 1;
-                const uint32_t mq = (uint32_t)__builtin_amdgcn_ds_bpermute((q & 63) << 2, (int)M);
-                if (q < l && mq <= (uint32_t)msrc2) pos += st;
-            }
-            const int32_t ps = __builtin_amdgcn_ds_bpermute((pos & 63) << 2, pend ? ms2 : 0x7FFFFFFF);
-            const bool go = pend && !(pos < l && ps < sendp);
-            if (go) cp_ring(s, x, msrc2, ms2, ml2, off);
-            __builtin_amdgcn_wave_barrier();
-            pend = pend && !go;
-            if (guard2 > 64) { x.bug = 104; break; }
-        }
-#endif
-        for (uint64_t pm = __ballot(pend); pm; pm &= pm - 1) {
-            const int j = (int)__builtin_ctzll(pm);
-            const int32_t jd = (int32_t)readlane((uint32_t)ms2, j), jsrc = (int32_t)readlane((uint32_t)msrc2, j);
-            const int32_t jn = (int32_t)readlane((uint32_t)ml2, j), D = jd - jsrc;
-            const int32_t stp = D < 64 ? D : 64;
-            for (int32_t k = 0; k < jn; k += stp) {
-                const int32_t i = k + l;
-                if (l < stp && i < jn) s.ring[slot(x, jd + i)] = s.ring[slot(x, jsrc + i)];
-                __builtin_amdgcn_wave_barrier();
-            }
-        }
-        pend = false;
-    }
-    int guard = 0;
-#else
-    int guard = 0;
-#endif
-    while (__ballot(pend)) {
-        const int32_t front = (int32_t)dwave_min(pend ? (uint32_t)ms : 0x7FFFFFFFu);
-        const int32_t send = msrc + (int32_t)ml < ms ? msrc + (int32_t)ml : ms;
-        const bool ready = pend && (far || send <= front);
-        if (ready) {
-            cp_ring(s, x, msrc2, ms2, ml2, off);
-            pend = false;
-        }
-        __builtin_amdgcn_wave_barrier();
-        XP_ADD(6, 1);
-        if (++guard > 64) { x.bug = 101; break; }
-    }
-    XP_ADD(4, ZP_NOW() - tq3);
-}
-
-#endif  // !JFS_ZEXEC_V2
 
 // whole-wave copy of one long match (ring or HBM sources)
 __device__ __forceinline__ void x_match(XSmem &s, X &x, uint32_t off, int32_t len) {
@@ -3727,11 +2338,7 @@ __device__ __forceinline__ void x_run(XSmem &s, X &x, uint32_t n, uint32_t ll, u
     const int32_t O0run = x.op;
     const int32_t o = O0run + (int32_t)(incl - len);
     const int32_t lit = (int32_t)*lp + (int32_t)(lincl - lln);
-#if JFS_ZEXEC_V2
     const bool lng = in && (ll > (uint32_t)LONGI || ml > (uint32_t)LONGI);
-#else
-    const bool lng = in && len > (uint32_t)LONGI;
-#endif
     uint32_t j = 0;
     while (j < n) {
         const int32_t oj = (int32_t)readlane((uint32_t)o, (int)j), lj = (int32_t)readlane((uint32_t)lit, (int)j);
@@ -3757,11 +2364,7 @@ __device__ __forceinline__ void x_run(XSmem &s, X &x, uint32_t n, uint32_t ll, u
         const uint64_t tw0 = ZP_NOW();
         if (L1 > lj) lit_window(s, x, lj, L1 - lj);
         XP_ADD(0, ZP_NOW() - tw0);
-#if JFS_ZEXEC_V2
         x_batch2(s, x, act, o, ll, ml, off, lit, oj, O1);
-#else
-        x_batch(s, x, act, o, ll, ml, off, lit, oj, O1);
-#endif
         x.op = O1;
         j = eb;
     }
@@ -3801,22 +2404,14 @@ __global__ __launch_bounds__(64) void zexec_kernel(const jfs_dev_block *__restri
     int32_t regen = 0, lused = 0;
     uint32_t rin0 = 1, rin1 = 4, rin2 = 8;  // repeat offsets at the start of the current block
     bool done = false;
-#if JFS_ZEXEC_V2
     // items one chunk ahead: the next 64 are loaded while this chunk runs
     uint4 ahead = make_uint4(0, 0, 0, 0);
     if ((uint32_t)l < nit) ahead = it[l];
-#endif
     for (uint32_t base = 0; base < nit && !done; base += 64) {
         uint64_t tb0 = ZP_NOW();
-#if JFS_ZEXEC_V2
         const uint4 mine = ahead;
         ahead = make_uint4(0, 0, 0, 0);
         if (base + 64 + l < nit) ahead = it[base + 64 + l];
-#else
-        uint4 mine = make_uint4(0, 0, 0, 0);
-        if (base + l < nit) mine = it[base + l];
-        wait_vm();
-#endif
         XP_ADD(0, ZP_NOW() - tb0);
         uint32_t cnt = nit - base < 64 ? nit - base : 64;
         const uint64_t nonseq = __ballot((uint32_t)l >= cnt || (mine.w & 0xFF) != IT_SEQ);
@@ -3953,15 +2548,11 @@ int launch_entropy_exec(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret,
     using namespace jfs::zstdd;
     hipLaunchKernelGGL(zlit_kernel, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, d_info, d_lit);
     if (hipGetLastError() != hipSuccess) return -1;
-#if JFS_ZSEQ_V2
     hipLaunchKernelGGL(zseqa_kernel, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, d_info, d_tabs, d_items,
                        g_strict_reserved);
     if (hipGetLastError() != hipSuccess) return -1;
-#if JFS_ZSEQA_DEFER
     hipLaunchKernelGGL(zbuild_kernel, dim3(nblk, ZBUILD_Q), dim3(64), 0, stream, nblk, d_info, d_tabs);
     if (hipGetLastError() != hipSuccess) return -1;
-#endif
-#if JFS_ZSEQ_HALF
     // Workgroup 2 bi decodes input bi's blocks [0, ZNB) and never waits on
     // anything; 2 bi + 1 decodes the rest and, at its first phase C, waits for
     // the repeat offsets 2 bi publishes.  Only second halves wait, and only on
@@ -3971,14 +2562,6 @@ int launch_entropy_exec(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret,
     // bounded anyway (seq_group2).
     static_assert(ZSEQ_INPUTS == 1, "split inputs: one input per workgroup pair");
     hipLaunchKernelGGL(zseqb_kernel, dim3(2 * nblk), dim3(128), 0, stream, d_blocks, nblk, d_info, d_tabs, d_items);
-#else
-    hipLaunchKernelGGL(zseqb_kernel, dim3((nblk + ZSEQ_INPUTS - 1) / ZSEQ_INPUTS), dim3(128), 0, stream, d_blocks, nblk,
-                       d_info, d_tabs, d_items);
-#endif
-#else
-    hipLaunchKernelGGL(zseq_kernel, dim3((nblk + ZSEQ_INPUTS - 1) / ZSEQ_INPUTS), dim3(64), 0, stream, d_blocks, nblk,
-                       d_info, d_tabs, d_items, g_strict_reserved);
-#endif
     if (hipGetLastError() != hipSuccess) return -1;
     hipLaunchKernelGGL(zexec_kernel, dim3(nblk), dim3(64), 0, stream, d_blocks, nblk, d_info, d_lit, d_items, d_ret,
                        (const int32_t *)nullptr);
