@@ -66,6 +66,7 @@ struct SBlock {
 
 struct BStat {
     int32_t bad, last_ok, total, todo;
+    int32_t unsettled;  // the gather met an entry that is not a literal yet
     int32_t fix[FIX_ROUNDS];
     int32_t jmp[JUMP_ROUNDS];
 };
@@ -91,7 +92,8 @@ struct Tok {
     bool last, cut;  // cut: the stream ends inside the token's header fields
 };
 
-__device__ __forceinline__ Tok parse(const gc_u8 *s, int64_t n, int64_t x, bool want_off) {
+template <class RD>
+__device__ __forceinline__ Tok parse_rd(RD s, int64_t n, int64_t x, bool want_off) {
     Tok t;
     t.cut = false;
     t.off = 0;
@@ -144,6 +146,9 @@ __device__ __forceinline__ Tok parse(const gc_u8 *s, int64_t n, int64_t x, bool 
     t.ml = ml + 4;
     t.next = q;
     return t;
+}
+__device__ __forceinline__ Tok parse(const gc_u8 *s, int64_t n, int64_t x, bool want_off) {
+    return parse_rd(s, n, x, want_off);
 }
 
 // block of global segment g (blocks are few: linear search over the seg0's)
@@ -334,21 +339,54 @@ __global__ __launch_bounds__(T) void scan_kernel(Scratch sc) {
     }
 }
 
+// One WAVE per segment: the segment's true tokens are parsed wave-uniformly
+// and each token's origin run is written by the whole wave (consecutive
+// entries per lane: coalesced stores).  (One thread per segment wrote ~2 KB
+// of scattered 16-byte stores each: 147 us of a lone 4 MiB block's 426.)
+constexpr int EWV = T / 64;  // segments per workgroup
+constexpr int ESTG = 1024;   // compressed bytes staged per segment (its tokens' fields, mostly)
 __global__ __launch_bounds__(T) void emit_kernel(int nb, int nseg_all, Scratch sc) {
-    const int g = blockIdx.x * T + threadIdx.x;
+    __shared__ alignas(16) uint8_t stg[EWV][ESTG];
+    const int l = lane_id();
+    const int g = (int)uniform((uint32_t)(blockIdx.x * EWV + (threadIdx.x >> 6)));
     if (g >= nseg_all) return;
-    const int b = block_of(sc.blk, nb, g);
+    const int b = (int)uniform((uint32_t)block_of(sc.blk, nb, g));
     BStat &st = sc.st[b];
     if (st.fix[FIX_ROUNDS - 1] || st.bad) return;
     const SBlock B = sc.blk[b];
-    const gc_u8 *s = (const gc_u8 *)B.src;
+    const gc_u8 *s = (const gc_u8 *)(((uint64_t)uniform((uint32_t)((uint64_t)(uintptr_t)B.src >> 32)) << 32) |
+                                     uniform((uint32_t)(uintptr_t)B.src));
     g_u32 *org = (g_u32 *)(sc.org + B.org_off);
-    const int64_t n = B.n, cap = B.cap, k = g - B.seg0;
+    const int64_t n = (int32_t)uniform((uint32_t)B.n), cap = (int32_t)uniform((uint32_t)B.cap),
+                  k = g - (int32_t)uniform((uint32_t)B.seg0);
     const int64_t s0 = k * SEG, s1 = s0 + SEG < n ? s0 + SEG : n;
-    int64_t x = sc.entry[g], op = sc.cnt[g];
+    int64_t x = (int32_t)uniform((uint32_t)sc.entry[g]), op = (int32_t)uniform((uint32_t)sc.cnt[g]);
+    // the parse reads the segment's bytes from LDS (one wave-uniform LDS round
+    // trip per field instead of an L2 one); bytes past the staging from HBM
+    uint8_t *buf = stg[threadIdx.x >> 6];
+    const uintptr_t a0 = ((uintptr_t)(s + s0)) & ~(uintptr_t)15, aend = (uintptr_t)(s + n);
+    {
+        const uintptr_t a = a0 + 16u * (uint32_t)l;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (a < aend) v = *(const gc_u4 *)a;  // (an aligned chunk holding a valid byte: same page)
+        *(uint4 *)(buf + 16 * l) = v;
+        __builtin_amdgcn_wave_barrier();
+    }
+    struct Rd {
+        const gc_u8 *s;
+        const uint8_t *buf;
+        uintptr_t a0;
+        __device__ uint32_t operator[](int64_t p) const {  // (p wave-uniform: scalar branch)
+            const uint32_t r = (uint32_t)uniform((uint32_t)((uintptr_t)(s + p) - a0));
+            uint32_t v;
+            if ((uintptr_t)(s + p) - a0 < (uintptr_t)ESTG) v = buf[r];
+            else v = s[p];
+            return uniform(v);
+        }
+    } rd{s, buf, a0};
     while (x < s1) {
-        const uint32_t tok = s[x];
-        const Tok t = parse(s, n, x, true);
+        const uint32_t tok = rd[x];
+        const Tok t = parse_rd(rd, n, x, true);
         // literal-length bytes: liblz4 stops reading them (a "loop error" it
         // ignores) once its input position reaches iend-15 after a 255 byte;
         // lenip < iend-14 means the terminator was read before that point
@@ -360,48 +398,23 @@ __global__ __launch_bounds__(T) void emit_kernel(int nb, int nseg_all, Scratch s
                  ((tok & 15) != 15 || t.mlip < n - 4) && op + t.ll + t.ml <= cap - 5;
         }
         if (!ok) {
-            st.bad = 1;
+            if (l == 0) st.bad = 1;
             return;
         }
-        // origin entries, 16-byte stores where the run is 4-aligned (the
-        // area starts 16-byte aligned: org_off is a multiple of 4 entries)
-        {
-            const uint32_t v0 = (uint32_t)(-(t.lenip) - 1);  // entry i = v0 - i
-            int64_t i = 0;
-            for (; i < t.ll && ((op + i) & 3); i++) org[op + i] = v0 - (uint32_t)i;
-            for (; i + 4 <= t.ll; i += 4) {
-                const uint32_t v = v0 - (uint32_t)i;
-                *(g_u4 *)(org + op + i) = make_uint4(v, v - 1u, v - 2u, v - 3u);
-            }
-            for (; i < t.ll; i++) org[op + i] = v0 - (uint32_t)i;
-        }
+        const uint32_t v0 = (uint32_t)(-(t.lenip) - 1);  // literal entry i = v0 - i
+        const int32_t ll = (int32_t)t.ll, ml = (int32_t)t.ml;
+        for (int32_t i = l; i < ll; i += 64) org[op + i] = v0 - (uint32_t)i;
         op += t.ll;
         if (t.last) {
-            st.last_ok = 1;
+            if (l == 0) st.last_ok = 1;
             return;
         }
-        {
-            const int64_t base = op - t.off;
-            const uint32_t off = (uint32_t)t.off;
-            uint32_t j = 0;  // entry i = base + (i mod off)
-            int64_t i = 0;
-            for (; i < t.ml && ((op + i) & 3); i++) {
-                org[op + i] = (uint32_t)(base + j);
-                j = j + 1 == off ? 0u : j + 1;
-            }
-            for (; i + 4 <= t.ml; i += 4) {
-                uint32_t e[4];
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    e[q] = (uint32_t)(base + j);
-                    j = j + 1 == off ? 0u : j + 1;
-                }
-                *(g_u4 *)(org + op + i) = make_uint4(e[0], e[1], e[2], e[3]);
-            }
-            for (; i < t.ml; i++) {
-                org[op + i] = (uint32_t)(base + j);
-                j = j + 1 == off ? 0u : j + 1;
-            }
+        // match entry i = op - off + (i mod off): overlapped matches point before the match
+        const int64_t base = op - t.off;
+        const uint32_t off = (uint32_t)t.off;
+        for (int32_t i = l; i < ml; i += 64) {
+            const uint32_t ui = (uint32_t)i;
+            org[op + i] = (uint32_t)(base + (ui < off ? ui : ui % off));
         }
         op += t.ml;
         x = t.next;
@@ -460,7 +473,7 @@ __global__ void verdict_kernel(int nb, Scratch sc, int32_t *__restrict__ ret, in
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= nb) return;
     BStat &st = sc.st[b];
-    const bool bad = st.bad || !st.last_ok || st.fix[FIX_ROUNDS - 1] || st.jmp[JUMP_ROUNDS - 1];
+    const bool bad = st.bad || !st.last_ok || st.fix[FIX_ROUNDS - 1] || st.unsettled;
     st.todo = bad;
     todo[b] = bad;
     if (!bad) ret[b] = st.total;
@@ -470,13 +483,15 @@ __global__ void verdict_kernel(int nb, Scratch sc, int32_t *__restrict__ ret, in
     if (st.fix[FIX_ROUNDS - 1]) atomicAdd(&g_split_counts[2], 1ull);
     else if (st.bad) atomicAdd(&g_split_counts[4], 1ull);
     else if (!st.last_ok) atomicAdd(&g_split_counts[5], 1ull);
-    else if (st.jmp[JUMP_ROUNDS - 1]) atomicAdd(&g_split_counts[3], 1ull);
+    else if (st.unsettled) atomicAdd(&g_split_counts[3], 1ull);
 }
 
+// (runs before the verdict: an entry that is still not a literal flags its
+// block, whose output the exact kernel then rewrites whole)
 __global__ __launch_bounds__(T) void gather_kernel(Scratch sc) {
     const int b = blockIdx.y;
-    const BStat &st = sc.st[b];
-    if (st.todo) return;
+    BStat &st = sc.st[b];
+    if (st.bad || !st.last_ok || st.fix[FIX_ROUNDS - 1]) return;  // (entries not all written: never read)
     const int64_t p = ((int64_t)blockIdx.x * T + threadIdx.x) * 4;
     const int64_t total = st.total;
     if (p >= total) return;
@@ -486,6 +501,13 @@ __global__ __launch_bounds__(T) void gather_kernel(Scratch sc) {
     g_u8 *d = (g_u8 *)B.dst;
     const uint4 v = *(const gc_u4 *)(org + p);
     const uint32_t e[4] = {v.x, v.y, v.z, v.w};
+    bool lit = true;
+#pragma unroll
+    for (int i = 0; i < 4; i++) lit &= p + i >= total || (int32_t)e[i] < 0;
+    if (!lit) {
+        st.unsettled = 1;
+        return;
+    }
     if (p + 4 <= total && (((uintptr_t)(d + p)) & 3u) == 0) {
         uint32_t w = 0;
 #pragma unroll
@@ -547,13 +569,22 @@ extern "C" int jfs_launch_lz4_split(const jfs_dev_block *d_desc, int nb, int32_t
         hipLaunchKernelGGL(count_kernel, dim3(gs), dim3(T), 0, st, nb, (int)nseg_all, sc);
     }
     hipLaunchKernelGGL(scan_kernel, dim3(nb), dim3(T), 0, st, sc);
-    if (nseg_all > 0) hipLaunchKernelGGL(emit_kernel, dim3(gs), dim3(T), 0, st, nb, (int)nseg_all, sc);
+    if (nseg_all > 0)
+        hipLaunchKernelGGL(emit_kernel, dim3((unsigned)((nseg_all + EWV - 1) / EWV)), dim3(T), 0, st, nb, (int)nseg_all, sc);
     // jump grid: about 2,048 workgroups in all (every entry of a 4 MiB block
     // is covered after a few strides), at most one per 1,024 entries
     const unsigned jx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((max_cap / 4 + T) / T, (2048 + nb - 1) / nb));
-    for (int r = 0; r < JUMP_ROUNDS; r++) hipLaunchKernelGGL(jump_kernel, dim3(jx, (unsigned)nb), dim3(T), 0, st, sc, r);
-    hipLaunchKernelGGL(verdict_kernel, dim3((nb + 63) / 64), dim3(64), 0, st, nb, sc, d_ret, todo);
+    // Rounds: after round r every entry points >= HOPS^r steps up its chain (or
+    // to a literal), and a chain is at most one step per token (a step from a
+    // token's match lands in an earlier token's output or in its own
+    // literals), i.e. <= max_cap / 4 + 1 steps: HOPS^jr above that settles
+    // every well-formed block (8 rounds for 4 MiB; each idle launch cost ~6 us
+    // of a lone decode).  The gather checks every entry regardless.
+    int jr = 1;
+    for (double reach = HOPS; reach <= (double)max_cap / 4 + 1 && jr < JUMP_ROUNDS; reach *= HOPS) jr++;
+    for (int r = 0; r < jr; r++) hipLaunchKernelGGL(jump_kernel, dim3(jx, (unsigned)nb), dim3(T), 0, st, sc, r);
     hipLaunchKernelGGL(gather_kernel, gp, dim3(T), 0, st, sc);
+    hipLaunchKernelGGL(verdict_kernel, dim3((nb + 63) / 64), dim3(64), 0, st, nb, sc, d_ret, todo);
     if (hipGetLastError() != hipSuccess) return -1;
     // the exact one-workgroup kernel for the flagged blocks (the others exit at once)
     return jfs_launch_lz4_decode_todo(d_desc, nb, d_ret, todo, st);

@@ -215,3 +215,36 @@ def test_split_device_sizes_beyond_host_budget_go_exact(gpu, oracle):
         assert dh[o:o + len(s)].tobytes() == s
     done, handed = D.lz4_split_counts()[:2]
     assert handed == len(srcs), (done, handed)
+
+
+def _chain_stream(units, seed=7):
+    """An LZ4 stream of `units` 11-byte output units, each one literal byte and
+    a 10-byte match at offset 11: every match byte copies the same byte of the
+    unit before, so its origin chain runs back through every earlier unit."""
+    rng = random.Random(seed)
+    first = bytes(rng.randrange(256) for _ in range(11))
+    out = bytearray([0xB6]) + first + (11).to_bytes(2, "little")  # ll 11, ml 10
+    for _ in range(units - 1):
+        out += bytes([0x16, rng.randrange(256)]) + (11).to_bytes(2, "little")  # ll 1, ml 10
+    out += bytes([0xF0, 1]) + bytes(rng.randrange(256) for _ in range(16))  # last: 16 literals
+    return bytes(out)
+
+
+def test_split_deep_origin_chains(gpu, oracle):
+    """Origin chains ~380,000 steps deep (4 MiB of 11-byte units): the pointer
+    jumping's round count, sized from the proven bound (a chain takes at most
+    one step per token), settles them on the split path itself."""
+    comps = [_chain_stream(381300), _chain_stream(20000, seed=8), _chain_stream(3, seed=9)]
+    caps = []
+    for c in comps:
+        n, _ = oracle.lz4_decompress(c, 8 << 20)
+        assert n > 0
+        caps.append(n)
+    assert caps[0] > 4_190_000
+    D.lz4_split_counts(reset=True)
+    r, outs = run_small(comps, caps, gpu)
+    for c, cap, x, o in zip(comps, caps, r, outs):
+        want_n, want = oracle.lz4_decompress(c, cap)
+        assert x == want_n and o == want
+    cnt = D.lz4_split_counts()
+    assert cnt[0] == len(comps) and cnt[1] == 0, cnt
