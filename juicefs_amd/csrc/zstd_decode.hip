@@ -2622,10 +2622,18 @@ int launch_split(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, jfs::z
         hipLaunchKernelGGL(zsemit_kernel, dim3((unsigned)nbk), dim3(ST), 0, st, nblk, (const ZInfo *)d_info,
                            (const uint4 *)d_items, sc);
     const unsigned jx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((max_cap / 4 + ST) / ST, (2048 + nblk - 1) / nblk));
-    for (int r = 0; r < SJ_ROUNDS; r++) hipLaunchKernelGGL(zsjump_kernel, dim3(jx, (unsigned)nblk), dim3(ST), 0, st, sc, r);
-    hipLaunchKernelGGL(zsverd_kernel, dim3((nblk + 63) / 64), dim3(64), 0, st, nblk, sc, d_ret);
+    // Rounds: after round r every entry points >= SJ_HOPS^r steps up its chain
+    // (or to a literal), and a step from a match byte lands in an earlier
+    // sequence's output (overlaps point before their match), so a chain has
+    // at most one step per sequence, <= max_cap / 3 + 1 (matches are >= 3
+    // bytes): SJ_HOPS^jr above that settles every well-formed input (8 rounds
+    // for 4 MiB).  The gather checks every entry regardless.
+    int jr = 1;
+    for (double reach = SJ_HOPS; reach <= (double)max_cap / 3 + 1 && jr < SJ_ROUNDS; reach *= SJ_HOPS) jr++;
+    for (int r = 0; r < jr; r++) hipLaunchKernelGGL(zsjump_kernel, dim3(jx, (unsigned)nblk), dim3(ST), 0, st, sc, r);
     hipLaunchKernelGGL(zsgather_kernel, dim3((unsigned)((max_cap / 4 + ST) / ST), (unsigned)nblk), dim3(ST), 0, st,
                        d_blocks, (const ZInfo *)d_info, (const uint8_t *)d_lit, sc);
+    hipLaunchKernelGGL(zsverd_kernel, dim3((nblk + 63) / 64), dim3(64), 0, st, nblk, sc, d_ret);
     hipLaunchKernelGGL(zexec_kernel, dim3(nblk), dim3(64), 0, st, d_blocks, nblk, (const ZInfo *)d_info,
                        (const uint8_t *)d_lit, (const uint4 *)d_items, d_ret, (const int32_t *)sc.todo);
     return hipGetLastError() == hipSuccess ? 0 : -1;
