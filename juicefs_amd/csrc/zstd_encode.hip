@@ -12,7 +12,7 @@
 // confirmation), ZSTD_compressLiterals + HUF_compress (table reuse), and
 // ZSTD_entropyCompressSequences (FSE table choice, normalisation, bitstream).
 //
-// Three kernels per launch, the serial parts kept serial only where the format
+// The kernels of a launch, the serial parts kept serial only where the format
 // makes them so:
 //   zl1_parse_kernel  one wave per FRAME: the greedy parse of every 128 KiB
 //                     block in order (the hash table and repeat offsets carry
@@ -24,10 +24,12 @@
 //   zl1_seq_kernel    one wave per BLOCK: gathers the block's literals (and
 //                     their histograms per Huffman stream) and writes the
 //                     complete sequences section (FSE tables + bitstream).
-//   zl1_lit_kernel    one wave per FRAME, block after block: the literal
-//                     section (Huffman table build / reuse decision, exact
-//                     sizes), the raw / RLE / compressed choice, and the
-//                     block bytes written in place.
+//   zl1_lithuf        one wave per BLOCK: the block's new Huffman table and
+//                     its description;
+//   zl1_litdec        one wave per FRAME, block after block: the literal
+//                     section choice (table reuse decision, exact sizes), the
+//                     raw / RLE / compressed choice and the block offsets;
+//   zl1_litwrite      one wave per BLOCK: the block bytes written in place.
 // Small batches (<= JFS_ZL1_SPEC_MAX blocks of multi-block frames) replace the
 // frame-serial parse by zl1_spec_merge / zl1_spec_parse: every block parses at
 // once from the prefix maxima of the other blocks' write sets, again until no
@@ -402,18 +404,35 @@ __device__ bool all_equal(const Src &S, int32_t a, int32_t b) {
 // ---------------------------------------------------------------------------
 // kernel 1: the parse (one wave per frame)
 // ---------------------------------------------------------------------------
+// the serial loop's state between two segments of a block
+struct SegSt {
+    int32_t ip0, anchor;
+    uint32_t o1, o2, saved;
+};
+
 // One block of ZSTD_compressBlock_fast_generic (+ the block decisions the
 // parse must predict), on the wave's LDS table T; off1 / off2 = the repeat
 // offsets handed in (updated as the serial loop passes them on).
+// Segments (the speculative parse): the loop's iterations whose search step
+// starts at ip0 < se, entered from the state *sin (nullptr: the block start)
+// and left in sout at the first search step at or past se (a match and its
+// inserts / repeat loop belong to the iteration that found it).  A segment's
+// sequences go to index (anchor in - bs) / 4 of the block's area: every
+// sequence covers >= 4 bytes, so the segments' ranges never overlap; ns / nl
+// count the segment's own.  The block fields are written by the first
+// segment (rin) and the last (se >= be: rout, flags, ns / nl of the segment).
 template <bool WIDE>
 __device__ __forceinline__ void parse_block(const FInfo &F, BInfo &B, int32_t k, Tab<WIDE> &T, const Src &S,
-                            uint64_t *__restrict__ seqs, uint32_t &off1, uint32_t &off2) {
+                            uint64_t *__restrict__ seqs, uint32_t &off1, uint32_t &off2, const SegSt *sin,
+                            int32_t se, SegSt &sout, int32_t &ons, int32_t &onl) {
     const int l = lane_id();
     const uint32_t hlog = F.hlog, mls = F.mls, tsize = 1u << hlog;
     const int32_t maxDist = 1 << F.wlog;
     ZP_DECL
     const int32_t bs = B.bs, be = B.be;
     const uint32_t rin0 = off1, rin1 = off2;
+    ons = 0;
+    onl = 0;
     if (be - bs < 7) {  // ZSTD_buildSeqStore: too small to compress, match state untouched
         if (l == 0) {
             B.ns = 0;
@@ -421,9 +440,9 @@ __device__ __forceinline__ void parse_block(const FInfo &F, BInfo &B, int32_t k,
             B.rin0 = rin0; B.rin1 = rin1; B.rout0 = rin0; B.rout1 = rin1;
             B.flags = F_NOCOMP;
         }
+        onl = be - bs;
         return;
     }
-    const bool rle = k > 0 && all_equal(S, bs, be);
     const int32_t prefixPos = be > maxDist ? be - maxDist : 0;
     const uint32_t prefixIdx = (uint32_t)prefixPos + 1, R = (uint32_t)be;
     if (WIDE && prefixPos > 0) {  // entries that left the window: the window's lowest index
@@ -435,16 +454,23 @@ __device__ __forceinline__ void parse_block(const FInfo &F, BInfo &B, int32_t k,
     ZP(6);
     ZPC(11);
     // ---- ZSTD_compressBlock_fast_generic
-    uint64_t *sq = seqs + B.seq_off;
     const int32_t ilimit = be - 8;
     int32_t ip0 = bs, anchor = bs, ns = 0, nl = 0;
     uint32_t o1 = off1, o2 = off2, saved = 0;
-    if (ip0 == prefixPos) ip0++;
-    {
+    if (!sin) {
+        if (ip0 == prefixPos) ip0++;
         const uint32_t maxRep = (uint32_t)(ip0 > maxDist ? maxDist : ip0);
         if (o2 > maxRep) { saved = o2; o2 = 0; }
         if (o1 > maxRep) { saved = o1; o1 = 0; }
+        if (l == 0) { B.rin0 = rin0; B.rin1 = rin1; }
+    } else {
+        ip0 = sin->ip0;
+        anchor = sin->anchor;
+        o1 = sin->o1;
+        o2 = sin->o2;
+        saved = sin->saved;
     }
+    uint64_t *sq = seqs + B.seq_off + (anchor - bs) / 4;
     // sequence records collect in a VGPR (lane i: record 64 g + i) and are
     // stored 64 at a time: no store per sequence for later vmcnt waits to drain
     uint64_t sbuf = 0;
@@ -579,6 +605,14 @@ __device__ __forceinline__ void parse_block(const FInfo &F, BInfo &B, int32_t k,
             }
         }
         ZP(1);
+        if (ip0 >= se) {  // the next segment's first search step: its tags come off
+            if (on) {
+                T.lo[h0] = (uint16_t)olo0;
+                T.lo[h1] = (uint16_t)olo1;
+            }
+            lds_order();
+            break;
+        }
         if (!onm) break;
         const bool rep = dec && o1 > 0 && AR.y == A.y;  // MEM_read32(ip2 - offset_1) == MEM_read32(ip2)
         const bool k0 = c0 && __builtin_amdgcn_alignbyte(X0.y, X0.x, 2) == val0;
@@ -682,13 +716,26 @@ __device__ __forceinline__ void parse_block(const FInfo &F, BInfo &B, int32_t k,
         const int32_t g0 = ns & ~63;
         if (g0 + l < ns) sq[g0 + l] = sbuf;
     }
+    ons = ns;
+    if (se < be) {  // a segment before the block's last: hand the loop's state on
+        onl = nl;
+        sout.ip0 = ip0;
+        sout.anchor = anchor;
+        sout.o1 = o1;
+        sout.o2 = o2;
+        sout.saved = saved;
+        ZP_FLUSH();
+        return;
+    }
     nl += be - anchor;
+    onl = nl;
+    const bool rle = k > 0 && all_equal(S, bs, be);
     const uint32_t ro0 = o1 ? o1 : saved, ro1 = o2 ? o2 : saved;
     const bool assumed = B.conf ? B.conf == 1 : !rle;
     if (l == 0) {
         B.ns = ns;
         B.nl = nl;
-        B.rin0 = rin0; B.rin1 = rin1; B.rout0 = ro0; B.rout1 = ro1;
+        B.rout0 = ro0; B.rout1 = ro1;
         B.flags = (rle ? F_RLE : 0) | (assumed ? F_ASSUMED : 0);
     }
     if (assumed) {
@@ -715,7 +762,10 @@ __global__ __launch_bounds__(64) void zl1_parse_kernel(const FInfo *__restrict__
     __syncthreads();
     const Src S = make_src(F.src, F.n);
     uint32_t off1 = 1, off2 = 4;  // repStartValue
-    for (int32_t k = 0; k < F.nb; k++) parse_block<WIDE>(F, bi[F.b0 + k], k, T, S, seqs, off1, off2);
+    SegSt so;
+    int32_t a, b;
+    for (int32_t k = 0; k < F.nb; k++)
+        parse_block<WIDE>(F, bi[F.b0 + k], k, T, S, seqs, off1, off2, nullptr, 0x7FFFFFFF, so, a, b);
 }
 
 // ---------------------------------------------------------------------------
@@ -734,72 +784,103 @@ __global__ __launch_bounds__(64) void zl1_parse_kernel(const FInfo *__restrict__
 // (whose inputs are the empty table and repStartValue) every block's parse is
 // the serial one.  Text settles in 7-8 rounds, random and zero data in 3 (CPU
 // simulation on the fixture inputs); at most nb + 1 rounds in any case.
+// Segments: a block splits into segsz-byte segments (the loop's iterations
+// whose search step starts inside, parse_block) when the batch has few blocks,
+// so a round is a fraction of a block parse; the same fixed point holds with
+// the loop's state (position, anchor, repeat offsets) handed from segment to
+// segment like the table.  A CPU simulation of the bench frame
+// (scripts/sim/spec_sim.cc) settles in 7 rounds of 128 KiB, 11 of 32 KiB,
+// 15 of 16 KiB: 7, 2.75 and 1.9 block parses of wall time.
 struct SpecB {
     int32_t chg;          // run this round
-    uint32_t rin0, rin1;  // repeat offsets handed in
-    uint32_t pad;
+    uint32_t rin0, rin1;  // first segment of a block: repeat offsets handed in
+    int32_t blk, q;       // block (index into bi) and segment of the block
+    SegSt in, out;        // later segments: the loop's state handed in / out
+    int32_t ns, nl;       // sequences and literals of the segment
 };
-constexpr uint32_t SPEC_TSZ = 1u << 14;  // table slots per block (wide frames: hashLog <= 14)
+constexpr uint32_t SPEC_TSZ = 1u << 14;  // table slots per segment (wide frames: hashLog <= 14)
+constexpr int SPEC_MAXSEG = 4096;        // segments per frame (the merge's flags)
 
-// one workgroup per frame
+// grid (frame, 256-bucket chunk): chunk 0's thread 0 passes the repeat
+// offsets in block order and the loop's state from segment to segment; every
+// thread takes one bucket through the frame's segments (prefix maxima of the
+// write sets).  Flags only ever rise (zl1_spec_parse clears its own).
 __global__ __launch_bounds__(256) void zl1_spec_merge(const FInfo *__restrict__ fi, const int32_t *__restrict__ sflist,
-                                                      const int32_t *__restrict__ sslot, const BInfo *__restrict__ bi,
-                                                      const uint32_t *__restrict__ W, uint32_t *__restrict__ I,
-                                                      SpecB *__restrict__ sp, int32_t *__restrict__ any, int first) {
+                                                      const int32_t *__restrict__ sslot, const int32_t *__restrict__ snseg,
+                                                      const BInfo *__restrict__ bi, const uint32_t *__restrict__ W,
+                                                      uint32_t *__restrict__ I, SpecB *__restrict__ sp,
+                                                      int32_t *__restrict__ any, int first) {
+    __shared__ uint32_t mark[SPEC_MAXSEG / 32];
+    __shared__ int32_t anyc;
     const FInfo F = fi[sflist[blockIdx.x]];
-    const int32_t s0 = sslot[blockIdx.x];
+    const int32_t s0 = sslot[blockIdx.x], nseg = snseg[blockIdx.x];
     const uint32_t tsize = 1u << F.hlog;
     const int t = threadIdx.x;
-    if (t == 0) {  // repeat offsets in block order (the serial kernel's off1 / off2)
-        uint32_t r0 = 1, r1 = 4;
-        for (int32_t k = 0; k < F.nb; k++) {
-            SpecB &x = sp[s0 + k];
-            const BInfo &B = bi[F.b0 + k];
-            x.chg = first || x.rin0 != r0 || x.rin1 != r1;
-            x.rin0 = r0;
-            x.rin1 = r1;
-            if (B.be - B.bs >= 7 && (B.flags & F_ASSUMED)) {
+    for (int i = t; i < SPEC_MAXSEG / 32; i += 256) mark[i] = 0;
+    if (t == 0) anyc = 0;
+    __syncthreads();
+    if (blockIdx.y == 0 && t == 0) {
+        uint32_t r0 = 1, r1 = 4;  // repStartValue
+        for (int32_t s = 0; s < nseg; s++) {
+            SpecB &x = sp[s0 + s];
+            bool c = first != 0;
+            if (x.q == 0) {
+                c |= x.rin0 != r0 || x.rin1 != r1;
+                x.rin0 = r0;
+                x.rin1 = r1;
+            } else if (!first) {  // (round 0 keeps the host's guess)
+                const SegSt p = sp[s0 + s - 1].out;
+                c |= x.in.ip0 != p.ip0 || x.in.anchor != p.anchor || x.in.o1 != p.o1 || x.in.o2 != p.o2 ||
+                     x.in.saved != p.saved;
+                x.in = p;
+            }
+            if (c) {
+                atomicOr(&mark[s >> 5], 1u << (s & 31));
+                anyc = 1;
+            }
+            const bool lastq = s + 1 == nseg || sp[s0 + s + 1].q == 0;
+            const BInfo &B = bi[x.blk];
+            if (lastq && B.be - B.bs >= 7 && (B.flags & F_ASSUMED)) {
                 r0 = B.rout0;
                 r1 = B.rout1;
             }
         }
     }
-    __syncthreads();
-    for (uint32_t h = t; h < tsize; h += 256) {
+    const uint32_t h = blockIdx.y * 256 + t;
+    if (h < tsize) {
         uint32_t run = 0;
-        for (int32_t k = 0; k < F.nb; k++) {
-            const size_t o = (size_t)(s0 + k) * SPEC_TSZ + h;
+        for (int32_t s = 0; s < nseg; s++) {
+            const size_t o = (size_t)(s0 + s) * SPEC_TSZ + h;
             if (I[o] != run) {
                 I[o] = run;
-                if (!first) atomicOr(&sp[s0 + k].chg, 1);
+                atomicOr(&mark[s >> 5], 1u << (s & 31));
+                anyc = 1;
             }
             run = umax32(run, W[o]);
         }
     }
     __syncthreads();
-    if (t < 64) {
-        int32_t c = 0;
-        for (int32_t k = t; k < F.nb; k += 64) c |= sp[s0 + k].chg;
-        if (__ballot(c != 0) && t == 0) atomicOr(any, 1);
-    }
+    for (int32_t s = t; s < nseg; s += 256)
+        if ((mark[s >> 5] >> (s & 31)) & 1u) sp[s0 + s].chg = 1;
+    if (t == 0 && anyc) atomicOr(any, 1);
 }
 
-// one wave per block whose inputs changed
+// one wave per segment whose inputs changed
 template <bool WIDE>
-__global__ __launch_bounds__(64) void zl1_spec_parse(const FInfo *__restrict__ fi, const int32_t *__restrict__ sblist,
-                                                     BInfo *__restrict__ bi, uint64_t *__restrict__ seqs,
-                                                     const uint32_t *__restrict__ I, uint32_t *__restrict__ W,
-                                                     const SpecB *__restrict__ sp) {
+__global__ __launch_bounds__(64) void zl1_spec_parse(const FInfo *__restrict__ fi, BInfo *__restrict__ bi,
+                                                     uint64_t *__restrict__ seqs, const uint32_t *__restrict__ I,
+                                                     uint32_t *__restrict__ W, SpecB *__restrict__ sp, int32_t segsz) {
     extern __shared__ uint32_t smem[];
     const int g = blockIdx.x;
     const SpecB x = sp[g];
     if (!x.chg) return;
     const int l = lane_id();
-    BInfo &B = bi[sblist[g]];
+    BInfo &B = bi[x.blk];
     const FInfo F = fi[B.frame];
-    const int32_t k = sblist[g] - F.b0;
+    const int32_t k = x.blk - F.b0;
     const uint32_t tsize = 1u << F.hlog;
     const int32_t maxDist = 1 << F.wlog;
+    const int32_t ss = B.bs + x.q * segsz, se = B.be - ss > segsz ? ss + segsz : 0x7FFFFFFF;
     Tab<WIDE> T;
     T.lo = (uint16_t *)smem;
     T.hi = smem + (tsize >> 1);
@@ -820,14 +901,54 @@ __global__ __launch_bounds__(64) void zl1_spec_parse(const FInfo *__restrict__ f
     __syncthreads();
     const Src S = make_src(F.src, F.n);
     uint32_t off1 = x.rin0, off2 = x.rin1;
-    parse_block<WIDE>(F, B, k, T, S, seqs, off1, off2);
+    SegSt out = x.in;
+    int32_t ns = 0, nl = 0;
+    parse_block<WIDE>(F, B, k, T, S, seqs, off1, off2, x.q ? &x.in : nullptr, se, out, ns, nl);
     __syncthreads();
-    // the block's write set: the entries now at indices of this block
+    // the segment's write set: the entries now at indices of this segment
+    // (entries of earlier segments past ss are in its input already: the
+    // merge's maxima do not change)
     uint32_t *Wk = W + (size_t)g * SPEC_TSZ;
     const uint32_t R = (uint32_t)B.be;
     for (uint32_t h = l; h < tsize; h += 64) {
         const uint32_t e = T.get(h, R);
-        Wk[h] = e > (uint32_t)B.bs ? e : 0u;
+        Wk[h] = e > (uint32_t)ss ? e : 0u;
+    }
+    if (l == 0) {
+        SpecB &y = sp[g];
+        y.chg = 0;
+        y.out = out;
+        y.ns = ns;
+        y.nl = nl;
+    }
+}
+
+// one wave per block of the speculative frames, after the last round: the
+// segments' sequences moved together (forward: a record never moves up),
+// the block's counts
+__global__ __launch_bounds__(64) void zl1_spec_compact(const int32_t *__restrict__ bfirst, BInfo *__restrict__ bi,
+                                                       uint64_t *__restrict__ seqs, const SpecB *__restrict__ sp) {
+    const int l = lane_id();
+    const int32_t g0 = bfirst[blockIdx.x], g1 = bfirst[blockIdx.x + 1];
+    BInfo &B = bi[sp[g0].blk];
+    if (B.flags & F_NOCOMP) return;  // (set whole by the parse)
+    uint64_t *sq = seqs + B.seq_off;
+    int32_t ns = 0, nl = 0;
+    for (int32_t g = g0; g < g1; g++) {
+        const SpecB x = sp[g];
+        const int32_t base = x.q ? (x.in.anchor - B.bs) / 4 : 0;
+        if (base != ns)
+            for (int32_t i = 0; i < x.ns; i += 64) {
+                const uint64_t v = i + l < x.ns ? sq[base + i + l] : 0;
+                __builtin_amdgcn_wave_barrier();
+                if (i + l < x.ns) sq[ns + i + l] = v;
+            }
+        ns += x.ns;
+        nl += x.nl;
+    }
+    if (l == 0) {
+        B.ns = ns;
+        B.nl = nl;
     }
 }
 
@@ -1466,29 +1587,37 @@ __device__ uint32_t huf_set_max_height(HNode *huffNode, uint32_t lastNonNull, ui
     return maxNbBits;
 }
 
-// HUF_buildCTable_wksp into (nnb, nval); lane 0; returns the max code length
-__device__ uint32_t huf_build(LitSmem &s, uint32_t maxsv, uint32_t maxNbBits) {
-    HNode *const huffNode = s.node + 1;
-    const int STARTNODE = 256;
-    for (int i = 0; i < 2 * 256 + 2; i++) {
+// HUF_buildCTable_wksp's node reset and its stable sort of the symbols by
+// decreasing count (the insertion sort's order: ties keep symbol order), as a
+// rank per symbol -- all lanes
+__device__ void huf_sort(LitSmem &s, uint32_t maxsv) {
+    const int l = lane_id();
+    for (int i = l; i < 2 * 256 + 2; i += 64) {
         s.node[i].count = 0;
         s.node[i].parent = 0;
         s.node[i].byte = 0;
         s.node[i].nbBits = 0;
     }
-    int m = 0;
-    for (uint32_t i = 0; i <= maxsv; i++) {  // stable sort, decreasing count
+    __syncthreads();
+    HNode *const huffNode = s.node + 1;
+    for (uint32_t i = (uint32_t)l; i <= maxsv; i += 64) {
         const uint32_t c = s.tot[i];
-        int pos = m++;
-        while (pos > 0 && c > huffNode[pos - 1].count) {
-            huffNode[pos] = huffNode[pos - 1];
-            pos--;
+        uint32_t r = 0;
+        for (uint32_t j = 0; j <= maxsv; j++) {
+            const uint32_t cj = s.tot[j];
+            r += (cj > c || (cj == c && j < i)) ? 1u : 0u;
         }
-        huffNode[pos].count = c;
-        huffNode[pos].byte = (uint8_t)i;
-        huffNode[pos].parent = 0;
-        huffNode[pos].nbBits = 0;
+        huffNode[r].count = c;
+        huffNode[r].byte = (uint8_t)i;
     }
+    __syncthreads();
+}
+
+// HUF_buildCTable_wksp into (nnb, nval) after huf_sort; lane 0; returns the
+// max code length
+__device__ uint32_t huf_build(LitSmem &s, uint32_t maxsv, uint32_t maxNbBits) {
+    HNode *const huffNode = s.node + 1;
+    const int STARTNODE = 256;
     int nonNullRank = (int)maxsv;
     while (huffNode[nonNullRank].count == 0) nonNullRank--;
     int lowS = nonNullRank, nodeNb = STARTNODE;
@@ -1660,7 +1789,7 @@ __device__ __forceinline__ void put_bytes(g_u8 *dst, int64_t o, uint64_t v, int 
 
 // encode literals lit[a, b) with table (nb, val), last symbol first, into dst
 // at byte o; returns the stream bytes (end mark included)
-__device__ int64_t huf_stream(LitSmem &s, const uint8_t *tnb, const uint16_t *tval, const gc_u8 *lit, int32_t a,
+__device__ int64_t huf_stream(uint32_t *ring, const uint8_t *tnb, const uint16_t *tval, const gc_u8 *lit, int32_t a,
                               int32_t b, g_u8 *dst, int64_t o) {
     const int l = lane_id();
     // ring bit 0 = bit 0 of the dword at (dst + o) & ~3
@@ -1668,7 +1797,7 @@ __device__ int64_t huf_stream(LitSmem &s, const uint8_t *tnb, const uint16_t *tv
     g_u8 *base = (g_u8 *)((uintptr_t)(dst + o) & ~(uintptr_t)3);
     g_u32 *wbase = (g_u32 *)base;
     const int64_t first_byte = (int64_t)(boff >> 3);  // bytes of dword 0 before the stream: keep
-    for (int k = l; k < 256; k += 64) s.ring[k] = 0;
+    for (int k = l; k < 256; k += 64) ring[k] = 0;
     __syncthreads();
     uint64_t bitpos = boff;  // absolute bit position from base
     uint64_t flushed = 0;    // dwords stored
@@ -1685,21 +1814,21 @@ __device__ int64_t huf_stream(LitSmem &s, const uint8_t *tnb, const uint16_t *tv
         if (len) {
             const uint64_t p = bitpos + ex;
             const uint32_t d = (uint32_t)(p >> 5) & 255u, sh = (uint32_t)(p & 31u);
-            atomicOr(&s.ring[d], code << sh);
-            if (sh + len > 32) atomicOr(&s.ring[(d + 1) & 255u], code >> (32 - sh));
+            atomicOr(&ring[d], code << sh);
+            if (sh + len > 32) atomicOr(&ring[(d + 1) & 255u], code >> (32 - sh));
         }
         __syncthreads();
         bitpos += tot;
         // store the complete dwords
         const uint64_t full = bitpos >> 5;
         for (uint64_t dw = flushed + l; dw < full; dw += 64) {
-            const uint32_t v = s.ring[dw & 255u];
+            const uint32_t v = ring[dw & 255u];
             if (dw == 0 && first_byte > 0) {
                 for (int k = (int)first_byte; k < 4; k++) base[k] = (uint8_t)(v >> (8 * k));
             } else {
                 wbase[dw] = v;
             }
-            s.ring[dw & 255u] = 0;
+            ring[dw & 255u] = 0;
         }
         __syncthreads();
         flushed = full;
@@ -1707,14 +1836,14 @@ __device__ int64_t huf_stream(LitSmem &s, const uint8_t *tnb, const uint16_t *tv
     // end mark, last partial dword (bytes up to the end only)
     if (l == 0) {
         const uint32_t d = (uint32_t)(bitpos >> 5) & 255u, sh = (uint32_t)(bitpos & 31u);
-        s.ring[d] |= 1u << sh;
+        ring[d] |= 1u << sh;
     }
     __syncthreads();
     bitpos += 1;
     const uint64_t endbyte = (bitpos + 7) >> 3;  // bytes from base
     const uint64_t lastdw = (endbyte + 3) >> 2;
     for (uint64_t dw = flushed + l; dw < lastdw; dw += 64) {
-        const uint32_t v = s.ring[dw & 255u];
+        const uint32_t v = ring[dw & 255u];
         const int64_t b0 = (int64_t)dw * 4;
         for (int k = 0; k < 4; k++) {
             const int64_t by = b0 + k;
@@ -1725,33 +1854,105 @@ __device__ int64_t huf_stream(LitSmem &s, const uint8_t *tnb, const uint16_t *tv
     return (int64_t)endbyte - first_byte;
 }
 
-__global__ __launch_bounds__(64) void zl1_lit_kernel(FInfo *__restrict__ fi, const int32_t *__restrict__ flist,
-                                                     BInfo *__restrict__ bi, const uint8_t *__restrict__ bytes,
-                                                     const uint32_t *__restrict__ hist, int32_t *__restrict__ ret) {
+// The literal sections and the block bytes, in three launches (the Huffman
+// reuse decision is serial per frame, the heavy work is per block):
+//   zl1_lithuf    one wave per block: histogram totals, and the block's new
+//                 Huffman table + its description (HUF_buildCTable,
+//                 HUF_writeCTable) whenever the block may need one;
+//   zl1_litdec    one wave per frame, block after block: the frame header,
+//                 HUF_compress_internal's choices (repeat check, size
+//                 estimates, exact stream sizes from the segment histograms),
+//                 the raw / RLE / compressed choice and every block's offset;
+//                 a wrong confirmation guess sends the frame back to the parse;
+//   zl1_litwrite  one wave per block: the block written in place.
+struct LitTab {
+    uint8_t nnb[256];   // the block's new table (zl1_lithuf)
+    uint16_t nval[256];
+    uint8_t hdr[160];
+    int32_t hs;         // description bytes (0: impossible), -1: not built
+    int32_t lkind;      // 0 raw, 1 RLE, 2 Huffman new table, 3 Huffman previous table (zl1_litdec)
+    int64_t op;         // block header offset in dst
+    int64_t cS;         // 0 raw block, 1 RLE block, else the compressed block size
+    int64_t clit;       // Huffman streams + description bytes
+    int32_t tsrc;       // block whose new table the streams use
+    int32_t single;     // one stream
+};
+
+__global__ __launch_bounds__(64) void zl1_lithuf_kernel(const FInfo *__restrict__ fi, const int32_t *__restrict__ blist,
+                                                        const BInfo *__restrict__ bi, const uint32_t *__restrict__ hist,
+                                                        LitTab *__restrict__ lt) {
     __shared__ LitSmem s;
+    const int l = lane_id();
+    const int32_t g = blist[blockIdx.x];
+    const BInfo B = bi[g];
+    if (fi[B.frame].status < 0) return;
+    LitTab &T = lt[g];
+    int32_t hs = -1;
+    const int32_t L = B.nl;
+    if (!(B.flags & F_NOCOMP) && L > 63) {
+        for (int i = l; i < 256; i += 64)
+            s.tot[i] = hist[(int64_t)g * 1024 + i] + hist[(int64_t)g * 1024 + 256 + i] +
+                       hist[(int64_t)g * 1024 + 512 + i] + hist[(int64_t)g * 1024 + 768 + i];
+        __syncthreads();
+        uint32_t mx = 0, largest = 0;
+        for (int i = l; i < 256; i += 64) {
+            if (s.tot[i]) mx = umax32(mx, (uint32_t)i);
+            largest = umax32(largest, s.tot[i]);
+        }
+        const uint32_t maxsv = dwave_max(mx);
+        largest = dwave_max(largest);
+        if (largest != (uint32_t)L && largest > (uint32_t)(L >> 7) + 4) {  // (else RLE or raw: no table)
+            const uint32_t hlog0 = fse_opt_tlog(11, (uint32_t)L, maxsv, 1);
+            huf_sort(s, maxsv);
+            if (l == 0) {
+                s.maxbits = (int32_t)huf_build(s, maxsv, hlog0);
+                s.hs = huf_write_ctable(s, maxsv, (uint32_t)s.maxbits);
+            }
+            __syncthreads();
+            hs = s.hs;
+            for (int i = l; i < 256; i += 64) {
+                T.nnb[i] = s.nnb[i];
+                T.nval[i] = s.nval[i];
+            }
+            for (int i = l; i < hs && i < 160; i += 64) T.hdr[i] = s.hdr[i];
+        }
+    }
+    if (l == 0) T.hs = hs;
+}
+
+struct LitDecSmem {
+    uint8_t pnb[256];  // previous (confirmed) Huffman table: code lengths
+    uint8_t nnb[256];  // this block's new table
+    uint32_t cnt[4][256];
+    uint32_t tot[256];
+};
+
+__global__ __launch_bounds__(64) void zl1_litdec_kernel(FInfo *__restrict__ fi, const int32_t *__restrict__ flist,
+                                                        BInfo *__restrict__ bi, const uint32_t *__restrict__ hist,
+                                                        LitTab *__restrict__ lt, int32_t *__restrict__ ret) {
+    __shared__ LitDecSmem s;
     const int l = lane_id();
     const int fidx = flist[blockIdx.x];
     FInfo &FR = fi[fidx];
     const FInfo F = FR;
     if (F.status < 0) return;
     g_u8 *dst = (g_u8 *)F.dst;
-    const Src S = make_src(F.src, F.n);
     // frame header (ZSTD_writeFrameHeader: no checksum, no dictionary, FCS)
     const uint32_t n = (uint32_t)F.n;
-    const bool single = (1u << F.wlog) >= n;
+    const bool single1 = (1u << F.wlog) >= n;
     const uint32_t fcs = (n >= 256) + (n >= 65536 + 256);
     int64_t op = 0;
     {
-        uint64_t hv = 0xFD2FB528ull | ((uint64_t)((single ? 0x20 : 0) | (fcs << 6)) << 32);
+        uint64_t hv = 0xFD2FB528ull | ((uint64_t)((single1 ? 0x20 : 0) | (fcs << 6)) << 32);
         int hn = 5;
-        if (!single) {
+        if (!single1) {
             hv |= (uint64_t)((F.wlog - 10) << 3) << 40;
             hn = 6;
         }
         put_bytes(dst, 0, hv, hn);
         op = hn;
         if (fcs == 0) {
-            if (single) {
+            if (single1) {
                 put_bytes(dst, op, n, 1);
                 op += 1;
             }
@@ -1767,18 +1968,16 @@ __global__ __launch_bounds__(64) void zl1_lit_kernel(FInfo *__restrict__ fi, con
         put_bytes(dst, op, 1, 3);
         op += 3;
     }
-    for (int k = l; k < 256; k += 64) {
-        s.pnb[k] = 0;
-        s.pval[k] = 0;
-    }
-    int prep = 0;  // HUF repeat mode of the previous confirmed table: 0 none, 1 check
+    for (int k = l; k < 256; k += 64) s.pnb[k] = 0;
+    int prep = 0;          // HUF repeat mode of the previous confirmed table: 0 none, 1 check
+    int32_t ptab = -1;     // the block whose new table that is
     __syncthreads();
     for (int32_t k = 0; k < F.nb; k++) {
-        BInfo &B = bi[F.b0 + k];
+        const int32_t g = F.b0 + k;
+        BInfo &B = bi[g];
+        LitTab &T = lt[g];
         const int32_t bs = B.bs, be = B.be, bsz = be - bs, flags = B.flags;
         const bool last = k == F.nb - 1;
-        const uint8_t *lit8 = bytes + B.lit_off;
-        const gc_u8 *lit = (const gc_u8 *)lit8;
         int64_t cS = 0;
         int lkind = 0;  // literal section: 0 raw, 1 RLE, 2 Huffman new table, 3 Huffman previous table
         int64_t litsz = 0, clit = 0;
@@ -1786,7 +1985,7 @@ __global__ __launch_bounds__(64) void zl1_lit_kernel(FInfo *__restrict__ fi, con
         int32_t L = 0;
         if (!(flags & F_NOCOMP)) {
             L = B.nl;
-            for (int i = l; i < 1024; i += 64) (&s.cnt[0][0])[i] = hist[(int64_t)(F.b0 + k) * 1024 + i];
+            for (int i = l; i < 1024; i += 64) (&s.cnt[0][0])[i] = hist[(int64_t)g * 1024 + i];
             __syncthreads();
             for (int i = l; i < 256; i += 64) s.tot[i] = s.cnt[0][i] + s.cnt[1][i] + s.cnt[2][i] + s.cnt[3][i];
             __syncthreads();
@@ -1797,11 +1996,8 @@ __global__ __launch_bounds__(64) void zl1_lit_kernel(FInfo *__restrict__ fi, con
             single = L < 256;
             lkind = 0;
             if (L > 63) {
-                uint32_t mx = 0, largest = 0;
-                for (int i = l; i < 256; i += 64)
-                    if (s.tot[i]) mx = umax32(mx, (uint32_t)i);
+                uint32_t largest = 0;
                 for (int i = l; i < 256; i += 64) largest = umax32(largest, s.tot[i]);
-                const uint32_t maxsv = dwave_max(mx);
                 largest = dwave_max(largest);
                 int repeat = prep;
                 const bool prefer = L <= 1024;
@@ -1841,13 +2037,10 @@ __global__ __launch_bounds__(64) void zl1_lit_kernel(FInfo *__restrict__ fi, con
                         clit = ct_internal(s.pnb, 0);
                         lkind = 3;
                     } else {
-                        const uint32_t hlog0 = fse_opt_tlog(11, (uint32_t)L, maxsv, 1);
-                        if (l == 0) {
-                            s.maxbits = (int32_t)huf_build(s, maxsv, hlog0);
-                            s.hs = huf_write_ctable(s, maxsv, (uint32_t)s.maxbits);
-                        }
+                        // the new table zl1_lithuf built for exactly this case
+                        for (int i = l; i < 256; i += 64) s.nnb[i] = T.nnb[i];
                         __syncthreads();
-                        const int64_t hs = s.hs;
+                        const int64_t hs = T.hs;
                         bool decided = false;
                         if (hs == 0) {
                             clit = 0;
@@ -1902,75 +2095,19 @@ __global__ __launch_bounds__(64) void zl1_lit_kernel(FInfo *__restrict__ fi, con
             }
             return;
         }
-        // ---- write the block
-        if (cS == 0) {
-            put_bytes(dst, op, (uint32_t)(last ? 1 : 0) | ((uint32_t)bsz << 3), 3);
-            wave_copy(dst + op + 3, F.src + bs, bsz);
-            op += 3 + bsz;
-        } else if (cS == 1) {
-            put_bytes(dst, op, (uint32_t)(last ? 1 : 0) | (1u << 1) | ((uint32_t)bsz << 3), 3);
-            const uint32_t rb = ldb(S, bs);
-            if (l == 0) dst[op + 3] = (uint8_t)rb;
-            op += 4;
-        } else {
-            put_bytes(dst, op, (uint32_t)(last ? 1 : 0) | (2u << 1) | ((uint32_t)cS << 3), 3);
-            int64_t o = op + 3;
-            const int64_t fl = 1 + (L > 31) + (L > 4095);
-            if (lkind == 0 || lkind == 1) {
-                const uint32_t t = lkind;
-                const uint64_t hv = fl == 1 ? (t | ((uint64_t)L << 3))
-                                            : fl == 2 ? (t | (1u << 2) | ((uint64_t)L << 4)) : (t | (3u << 2) | ((uint64_t)L << 4));
-                put_bytes(dst, o, hv, (int)fl);
-                o += fl;
-                if (lkind == 0) {
-                    wave_copy(dst + o, lit8, L);
-                    o += L;
-                } else {
-                    if (l == 0) dst[o] = lit[0];
-                    o += 1;
-                }
-            } else {
-                const int lh = 3 + (L >= 1024) + (L >= 16384);
-                const uint64_t ht = lkind == 2 ? 2 : 3;
-                uint64_t hv;
-                if (lh == 3) hv = ht | ((uint64_t)(single ? 0 : 1) << 2) | ((uint64_t)L << 4) | ((uint64_t)clit << 14);
-                else if (lh == 4) hv = ht | (2ull << 2) | ((uint64_t)L << 4) | ((uint64_t)clit << 18);
-                else hv = ht | (3ull << 2) | ((uint64_t)L << 4) | ((uint64_t)clit << 22);
-                put_bytes(dst, o, hv, lh);
-                o += lh;
-                const uint8_t *tnb = lkind == 2 ? s.nnb : s.pnb;
-                const uint16_t *tval = lkind == 2 ? s.nval : s.pval;
-                if (lkind == 2) {
-                    for (int i = l; i < s.hs; i += 64) dst[o + i] = s.hdr[i];
-                    o += s.hs;
-                }
-                if (single) {
-                    o += huf_stream(s, tnb, tval, lit, 0, L, dst, o);
-                } else {
-                    const int32_t sg = (L + 3) / 4;
-                    const int64_t jt = o;
-                    o += 6;
-                    int64_t sz[4];
-                    for (int q = 0; q < 4; q++) {
-                        const int32_t a = q * sg, b = q < 3 ? a + sg : L;
-                        sz[q] = huf_stream(s, tnb, tval, lit, a, b, dst, o);
-                        o += sz[q];
-                    }
-                    put_bytes(dst, jt, (uint64_t)sz[0] | ((uint64_t)sz[1] << 16) | ((uint64_t)sz[2] << 32), 6);
-                }
-            }
-            // the sequences section
-            wave_copy(dst + o, bytes + B.lit_off + bsz, B.secsz);
-            o += B.secsz;
-            op = o;
+        if (l == 0) {
+            T.op = op;
+            T.cS = cS;
+            T.lkind = lkind;
+            T.clit = clit;
+            T.tsrc = lkind == 3 ? ptab : g;
+            T.single = single;
         }
-        __syncthreads();
+        op += cS == 0 ? 3 + bsz : cS == 1 ? 4 : 3 + cS;
         if (confirmed && lkind == 2) {  // this block's new table becomes the previous table
-            for (int i = l; i < 256; i += 64) {
-                s.pnb[i] = s.nnb[i];
-                s.pval[i] = s.nval[i];
-            }
+            for (int i = l; i < 256; i += 64) s.pnb[i] = s.nnb[i];
             prep = 1;
+            ptab = g;
         }
         __syncthreads();
     }
@@ -1978,6 +2115,98 @@ __global__ __launch_bounds__(64) void zl1_lit_kernel(FInfo *__restrict__ fi, con
         ret[fidx] = op <= F.cap ? (int32_t)op : -2;
         FR.status = 0;
     }
+}
+
+struct LitWSmem {
+    uint8_t tnb[256];
+    uint16_t tval[256];
+    uint32_t ring[256];  // Huffman stream staging (8,192 bits)
+};
+
+__global__ __launch_bounds__(64) void zl1_litwrite_kernel(const FInfo *__restrict__ fi, const int32_t *__restrict__ blist,
+                                                          const BInfo *__restrict__ bi, const uint8_t *__restrict__ bytes,
+                                                          const LitTab *__restrict__ lt) {
+    __shared__ LitWSmem s;
+    const int l = lane_id();
+    const int32_t g = blist[blockIdx.x];
+    const BInfo B = bi[g];
+    const FInfo F = fi[B.frame];
+    if (F.status != 0) return;  // (zl1_litdec sent the frame back to the parse)
+    const LitTab &T = lt[g];
+    const int64_t op = T.op, cS = T.cS;
+    const int lkind = T.lkind;
+    const int64_t clit = T.clit;
+    const bool single = T.single != 0;
+    g_u8 *dst = (g_u8 *)F.dst;
+    const Src S = make_src(F.src, F.n);
+    const int32_t bs = B.bs, bsz = B.be - B.bs;
+    const bool last = g - F.b0 == F.nb - 1;
+    const uint8_t *lit8 = bytes + B.lit_off;
+    const gc_u8 *lit = (const gc_u8 *)lit8;
+    if (cS == 0) {
+        put_bytes(dst, op, (uint32_t)(last ? 1 : 0) | ((uint32_t)bsz << 3), 3);
+        wave_copy(dst + op + 3, F.src + bs, bsz);
+        return;
+    }
+    if (cS == 1) {
+        put_bytes(dst, op, (uint32_t)(last ? 1 : 0) | (1u << 1) | ((uint32_t)bsz << 3), 3);
+        const uint32_t rb = ldb(S, bs);
+        if (l == 0) dst[op + 3] = (uint8_t)rb;
+        return;
+    }
+    put_bytes(dst, op, (uint32_t)(last ? 1 : 0) | (2u << 1) | ((uint32_t)cS << 3), 3);
+    int64_t o = op + 3;
+    const int32_t L = B.nl;
+    const int64_t fl = 1 + (L > 31) + (L > 4095);
+    if (lkind == 0 || lkind == 1) {
+        const uint32_t t = lkind;
+        const uint64_t hv = fl == 1 ? (t | ((uint64_t)L << 3))
+                                    : fl == 2 ? (t | (1u << 2) | ((uint64_t)L << 4)) : (t | (3u << 2) | ((uint64_t)L << 4));
+        put_bytes(dst, o, hv, (int)fl);
+        o += fl;
+        if (lkind == 0) {
+            wave_copy(dst + o, lit8, L);
+            o += L;
+        } else {
+            if (l == 0) dst[o] = lit[0];
+            o += 1;
+        }
+    } else {
+        const int lh = 3 + (L >= 1024) + (L >= 16384);
+        const uint64_t ht = lkind == 2 ? 2 : 3;
+        uint64_t hv;
+        if (lh == 3) hv = ht | ((uint64_t)(single ? 0 : 1) << 2) | ((uint64_t)L << 4) | ((uint64_t)clit << 14);
+        else if (lh == 4) hv = ht | (2ull << 2) | ((uint64_t)L << 4) | ((uint64_t)clit << 18);
+        else hv = ht | (3ull << 2) | ((uint64_t)L << 4) | ((uint64_t)clit << 22);
+        put_bytes(dst, o, hv, lh);
+        o += lh;
+        const LitTab &U = lt[T.tsrc];
+        for (int i = l; i < 256; i += 64) {
+            s.tnb[i] = U.nnb[i];
+            s.tval[i] = U.nval[i];
+        }
+        if (lkind == 2) {
+            for (int i = l; i < T.hs; i += 64) dst[o + i] = T.hdr[i];
+            o += T.hs;
+        }
+        __syncthreads();
+        if (single) {
+            o += huf_stream(s.ring, s.tnb, s.tval, lit, 0, L, dst, o);
+        } else {
+            const int32_t sg = (L + 3) / 4;
+            const int64_t jt = o;
+            o += 6;
+            int64_t sz[4];
+            for (int q = 0; q < 4; q++) {
+                const int32_t a = q * sg, b = q < 3 ? a + sg : L;
+                sz[q] = huf_stream(s.ring, s.tnb, s.tval, lit, a, b, dst, o);
+                o += sz[q];
+            }
+            put_bytes(dst, jt, (uint64_t)sz[0] | ((uint64_t)sz[1] << 16) | ((uint64_t)sz[2] << 32), 6);
+        }
+    }
+    // the sequences section
+    wave_copy(dst + o, bytes + B.lit_off + bsz, B.secsz);
 }
 
 }  // namespace zl1
@@ -2021,6 +2250,15 @@ extern "C" int jfs_zpprof_reset() {
 // Small batches take the block-parallel speculative parse (zl1_spec_*) for
 // their multi-block frames: at most JFS_ZL1_SPEC_MAX blocks in all (default
 // 2,048; 0 = never).  Larger batches fill the GPU with frame-serial parses.
+// segments per block of the speculative parse at most (1, 2, 4, 8, 16)
+int spec_segs() {  // (read per launch: the tests sweep it)
+    const char *e = getenv("JFS_ZL1_SEGS");
+    const int p = e ? atoi(e) : 8;
+    int q = 1;
+    while (q * 2 <= p && q < 16) q *= 2;
+    return q;
+}
+
 int spec_max_blocks() {
     static int v = [] {
         const char *e = getenv("JFS_ZL1_SPEC_MAX");
@@ -2078,34 +2316,64 @@ extern "C" int jfs_launch_zstd_encode(const jfs_dev_block *d_blocks, int nblk, i
     const int nbk = (int)bi.size();
     // speculative parse: the multi-block (wide) frames of a small batch, their
     // blocks in slots grouped by hashLog
-    std::vector<int32_t> sf, sslot, sblist;
+    // frames, their blocks in slots grouped by hashLog; a block takes
+    // segsz-byte segments (one slot each) when the batch has few blocks: the
+    // most segments per block (<= JFS_ZL1_SEGS, default 8) that keep the slots
+    // within the ~1,024 waves the GPU holds at once (four per CU by LDS)
+    std::vector<int32_t> sf, sslot, snseg, bfirst;
+    std::vector<SpecB> slots;
     std::vector<std::pair<uint32_t, std::pair<int, int>>> sgrp;  // hashLog -> (first slot, slots)
+    int32_t segsz = BLK;
     {
         int64_t cand = 0;
         for (int f = 0; f < nblk; f++)
             if (fi[f].status == 0 && fi[f].nb >= 2 && fi[f].n >= 65536) cand += fi[f].nb;
         if (cand > 0 && cand <= spec_max_blocks()) {
+            int P = spec_segs();
+            while (P > 1 && cand * P > 1024) P >>= 1;
+            segsz = BLK / P;
             for (uint32_t hl = 6; hl <= 14; hl++) {
-                const int g0 = (int)sblist.size();
+                const int g0 = (int)slots.size();
                 for (int f = 0; f < nblk; f++) {
                     const FInfo &F = fi[f];
                     if (F.status != 0 || F.nb < 2 || F.n < 65536 || F.hlog != hl) continue;
                     sf.push_back(f);
-                    sslot.push_back((int32_t)sblist.size());
-                    for (int k = 0; k < F.nb; k++) sblist.push_back(F.b0 + k);
+                    sslot.push_back((int32_t)slots.size());
+                    for (int k = 0; k < F.nb; k++) {
+                        const BInfo &B = bi[F.b0 + k];
+                        bfirst.push_back((int32_t)slots.size());
+                        for (int32_t q = 0; q == 0 || B.bs + q * segsz < B.be; q++) {
+                            SpecB x;
+                            memset(&x, 0, sizeof(x));
+                            x.blk = F.b0 + k;
+                            x.q = q;
+                            // round 0's guess of the state handed in: the loop
+                            // at the segment start (any valid state will do)
+                            x.in.ip0 = x.in.anchor = B.bs + q * segsz;
+                            x.in.o1 = 1;
+                            x.in.o2 = 4;
+                            slots.push_back(x);
+                        }
+                    }
+                    snseg.push_back((int32_t)slots.size() - sslot.back());
                 }
-                if ((int)sblist.size() > g0) sgrp.push_back({hl, {g0, (int)sblist.size() - g0}});
+                if ((int)slots.size() > g0) sgrp.push_back({hl, {g0, (int)slots.size() - g0}});
             }
+            bfirst.push_back((int32_t)slots.size());
         }
     }
-    const int nsf = (int)sf.size(), nsb = (int)sblist.size();
+    const int nsf = (int)sf.size(), nsb = (int)slots.size(), nspb = bfirst.empty() ? 0 : (int)bfirst.size() - 1;
+    int maxseg = 0;
+    for (int32_t c : snseg) maxseg = std::max(maxseg, c);
+    if (maxseg > SPEC_MAXSEG) return -1;  // (cannot happen: <= 2,048 blocks x 8)
     const size_t fb = a256(sizeof(FInfo) * nblk), bb = a256(sizeof(BInfo) * std::max(nbk, 1)),
                  lb = a256(sizeof(int32_t) * (2 * (size_t)nblk + (size_t)nbk + 16)), sb = a256(sizeof(uint64_t) * (size_t)std::max<int64_t>(seq_total, 1)),
-                 yb = a256((size_t)std::max<int64_t>(byte_total, 1)), hb = a256(sizeof(uint32_t) * 1024 * (size_t)std::max(nbk, 1));
-    const size_t spb = nsb ? a256(sizeof(int32_t) * (2 * (size_t)nsf + nsb + 16)) + a256(sizeof(SpecB) * nsb) +
+                 yb = a256((size_t)std::max<int64_t>(byte_total, 1)), hb = a256(sizeof(uint32_t) * 1024 * (size_t)std::max(nbk, 1)),
+                 tb = a256(sizeof(LitTab) * (size_t)std::max(nbk, 1));
+    const size_t spb = nsb ? a256(sizeof(int32_t) * (3 * (size_t)nsf + nspb + 16)) + a256(sizeof(SpecB) * nsb) +
                                  2 * a256(sizeof(uint32_t) * SPEC_TSZ * (size_t)nsb) + 256
                            : 0;
-    if (!z.grow(fb + bb + lb + sb + yb + hb + spb)) return -1;
+    if (!z.grow(fb + bb + lb + sb + yb + hb + tb + spb)) return -1;
     uint8_t *p = z.d;
     FInfo *d_fi = (FInfo *)p;
     p += fb;
@@ -2119,12 +2387,14 @@ extern "C" int jfs_launch_zstd_encode(const jfs_dev_block *d_blocks, int nblk, i
     p += yb;
     uint32_t *d_hist = (uint32_t *)p;
     p += hb;
+    LitTab *d_lt = (LitTab *)p;
+    p += tb;
     int32_t *d_slists = nullptr, *d_any = nullptr;
     SpecB *d_sp = nullptr;
     uint32_t *d_W = nullptr, *d_I = nullptr;
     if (nsb) {
         d_slists = (int32_t *)p;
-        p += a256(sizeof(int32_t) * (2 * (size_t)nsf + nsb + 16));
+        p += a256(sizeof(int32_t) * (3 * (size_t)nsf + nspb + 16));
         d_sp = (SpecB *)p;
         p += a256(sizeof(SpecB) * nsb);
         d_W = (uint32_t *)p;
@@ -2139,7 +2409,7 @@ extern "C" int jfs_launch_zstd_encode(const jfs_dev_block *d_blocks, int nblk, i
     std::vector<int32_t> todo;
     for (int f = 0; f < nblk; f++)
         if (fi[f].status == 0) todo.push_back(f);
-    // frames that cannot be encoded report -2 now; the others are written by zl1_lit_kernel
+    // frames that cannot be encoded report -2 now; the others are written by zl1_litdec / zl1_litwrite
     for (int f = 0; f < nblk; f++)
         if (fi[f].status < 0) hret[f] = -2;
     if (hipMemcpyAsync(d_ret, hret.data(), sizeof(int32_t) * nblk, hipMemcpyHostToDevice, stream) != hipSuccess) return -1;
@@ -2152,20 +2422,20 @@ extern "C" int jfs_launch_zstd_encode(const jfs_dev_block *d_blocks, int nblk, i
         if (pass == 0 && nsb) {
             std::vector<int32_t> sl(sf);
             sl.insert(sl.end(), sslot.begin(), sslot.end());
-            sl.insert(sl.end(), sblist.begin(), sblist.end());
+            sl.insert(sl.end(), snseg.begin(), snseg.end());
+            sl.insert(sl.end(), bfirst.begin(), bfirst.end());
             if (hipMemcpyAsync(d_slists, sl.data(), sizeof(int32_t) * sl.size(), hipMemcpyHostToDevice, stream) !=
                     hipSuccess ||
-                hipMemsetAsync(d_W, 0, sizeof(uint32_t) * SPEC_TSZ * (size_t)nsb, stream) != hipSuccess ||
-                hipMemsetAsync(d_sp, 0, sizeof(SpecB) * nsb, stream) != hipSuccess)
+                hipMemcpyAsync(d_sp, slots.data(), sizeof(SpecB) * nsb, hipMemcpyHostToDevice, stream) != hipSuccess ||
+                hipMemsetAsync(d_W, 0, sizeof(uint32_t) * SPEC_TSZ * (size_t)nsb, stream) != hipSuccess)
                 return -1;
-            const int32_t *d_sf = d_slists, *d_ss = d_slists + nsf, *d_sb = d_slists + 2 * nsf;
-            int maxnb = 0;
-            for (int f : sf) maxnb = std::max(maxnb, fi[f].nb);
+            const int32_t *d_sf = d_slists, *d_ss = d_slists + nsf, *d_sn = d_slists + 2 * nsf,
+                          *d_bf = d_slists + 3 * nsf;
             bool settled = false;
-            for (int r = 0; r <= maxnb + 1; r++) {
+            for (int r = 0; r <= maxseg + 1; r++) {
                 if (hipMemsetAsync(d_any, 0, sizeof(int32_t), stream) != hipSuccess) return -1;
-                hipLaunchKernelGGL(zl1_spec_merge, dim3(nsf), dim3(256), 0, stream, d_fi, d_sf, d_ss, d_bi, d_W, d_I,
-                                   d_sp, d_any, r == 0 ? 1 : 0);
+                hipLaunchKernelGGL(zl1_spec_merge, dim3(nsf, SPEC_TSZ / 256), dim3(256), 0, stream, d_fi, d_sf, d_ss,
+                                   d_sn, d_bi, d_W, d_I, d_sp, d_any, r == 0 ? 1 : 0);
                 if (hipGetLastError() != hipSuccess) return -1;
                 if (r > 0) {
                     int32_t h_any = 1;
@@ -2178,12 +2448,14 @@ extern "C" int jfs_launch_zstd_encode(const jfs_dev_block *d_blocks, int nblk, i
                     const size_t tsz = (size_t)1 << g.first;
                     const int g0 = g.second.first, cnt = g.second.second;
                     hipLaunchKernelGGL(zl1_spec_parse<true>, dim3(cnt), dim3(64), tsz * 2 + tsz / 2, stream, d_fi,
-                                       d_sb + g0, d_bi, d_seq, d_I + (size_t)g0 * SPEC_TSZ, d_W + (size_t)g0 * SPEC_TSZ,
-                                       d_sp + g0);
+                                       d_bi, d_seq, d_I + (size_t)g0 * SPEC_TSZ, d_W + (size_t)g0 * SPEC_TSZ, d_sp + g0,
+                                       segsz);
                     if (hipGetLastError() != hipSuccess) return -1;
                 }
             }
-            if (!settled) return -1;  // (cannot happen: nb + 1 rounds settle any frame)
+            if (!settled) return -1;  // (cannot happen: segments + 1 rounds settle any frame)
+            hipLaunchKernelGGL(zl1_spec_compact, dim3(nspb), dim3(64), 0, stream, d_bf, d_bi, d_seq, (const SpecB *)d_sp);
+            if (hipGetLastError() != hipSuccess) return -1;
         }
         // parse launches: one per (table width, hashLog) so each gets exactly its LDS
         std::vector<int32_t> lists, blist;
@@ -2240,8 +2512,14 @@ extern "C" int jfs_launch_zstd_encode(const jfs_dev_block *d_blocks, int nblk, i
                                d_list + blist_off, d_bi, d_seq, d_bytes, d_hist);
             if (hipGetLastError() != hipSuccess) return -1;
         }
-        hipLaunchKernelGGL(zl1_lit_kernel, dim3((unsigned)todo.size()), dim3(64), 0, stream, d_fi, d_list + flist_off,
-                           d_bi, d_bytes, d_hist, d_ret);
+        if (!blist.empty())
+            hipLaunchKernelGGL(zl1_lithuf_kernel, dim3((unsigned)blist.size()), dim3(64), 0, stream, d_fi,
+                               d_list + blist_off, d_bi, d_hist, d_lt);
+        hipLaunchKernelGGL(zl1_litdec_kernel, dim3((unsigned)todo.size()), dim3(64), 0, stream, d_fi, d_list + flist_off,
+                           d_bi, d_hist, d_lt, d_ret);
+        if (!blist.empty())
+            hipLaunchKernelGGL(zl1_litwrite_kernel, dim3((unsigned)blist.size()), dim3(64), 0, stream, d_fi,
+                               d_list + blist_off, d_bi, d_bytes, d_lt);
         if (hipGetLastError() != hipSuccess) return -1;
         // frames whose confirmation guess was wrong go again
         std::vector<FInfo> chk(nblk);

@@ -197,6 +197,33 @@ def test_zstd_encode_golden_l1_cases_frame_serial(gpu):
         assert x == c["csize"] and _sha(f) == c["comp_sha"], (c["kind"], c["size"], x, c["csize"])
 
 
+@pytest.mark.parametrize("segs", [1, 2, 4, 8, 16])
+def test_zstd_encode_segment_parse(gpu, oracle, monkeypatch, segs):
+    """The small-batch parse with every block split into `segs` segments (the
+    loop's state handed from segment to segment, JFS_ZL1_SEGS): the golden
+    4 MiB text frame alone (libzstd's sha256), and a small mixed batch --
+    repeat-offset runs across segment starts, long matches that jump whole
+    segments, zeros, random, odd sizes -- identical to the CPU oracle."""
+    import json
+    from tests.zstd_l1_cases import make_case
+    monkeypatch.setenv("JFS_ZL1_SEGS", str(segs))
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "zstd_l1_golden.json")))
+    big = [c for c in g["cases"] if c["kind"] == "T" and c["size"] == 4 << 20][0]
+    r, frames = encode_device([make_case(big["kind"], big["seed"], big["size"])], gpu)
+    assert r[0] == big["csize"] and _sha(frames[0]) == big["comp_sha"], (segs, r[0], big["csize"])
+    rng = np.random.default_rng(900 + segs)
+    pat = rng.integers(0, 256, 11, dtype=np.uint8).tobytes()
+    rep = bytearray((pat * ((1 << 20) // 11 + 2))[:(1 << 20) + 5])
+    for j in range(0, len(rep), 20011):
+        rep[j] ^= 0x33
+    srcs = [bytes(rep), make_case("R", 31, 1 << 20), make_case("Z", 32, 600000), make_case("M", 33, 2 << 20),
+            make_case("T", 34, 262145), make_case("S", 35, 3 * 131072 + 77)]
+    r, frames = encode_device(srcs, gpu, src_mis=2, dst_mis=6)
+    for i, (s, x, f) in enumerate(zip(srcs, r, frames)):
+        want = oracle.zstd_compress_l1(s)
+        assert x == len(want) and f == want, (segs, i, len(s), x, len(want))
+
+
 def test_zstd_encode_matches_oracle_seeded(gpu, oracle):
     """Seeded inputs of every kind and size class (many frames per launch, every
     (table width, hashLog) parse group): identical to the CPU oracle."""
