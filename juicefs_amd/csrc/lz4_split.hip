@@ -339,12 +339,29 @@ __global__ __launch_bounds__(T) void scan_kernel(Scratch sc) {
     }
 }
 
+// the token checks the exact decoder makes (the emit keeps a token only if
+// it would run it the same way)
+__device__ __forceinline__ bool tok_ok(uint32_t tok, const Tok &t, int64_t n, int64_t op, int64_t cap) {
+    // literal-length bytes: liblz4 stops reading them (a "loop error" it
+    // ignores) once its input position reaches iend-15 after a 255 byte;
+    // lenip < iend-14 means the terminator was read before that point
+    bool ok = !t.cut && ((tok >> 4) != 15 || t.lenip < n - 14);
+    if (t.last) {
+        ok = ok && t.lit_end == n && op + t.ll <= cap;
+    } else {
+        ok = ok && t.lit_end <= n - 8 && op + t.ll <= cap - 12 && t.off >= 1 && t.off <= op + t.ll &&
+             ((tok & 15) != 15 || t.mlip < n - 4) && op + t.ll + t.ml <= cap - 5;
+    }
+    return ok;
+}
+
 // One WAVE per segment: the segment's true tokens are parsed wave-uniformly
 // and each token's origin run is written by the whole wave (consecutive
 // entries per lane: coalesced stores).  (One thread per segment wrote ~2 KB
 // of scattered 16-byte stores each: 147 us of a lone 4 MiB block's 426.)
 constexpr int EWV = T / 64;  // segments per workgroup
 constexpr int ESTG = 1024;   // compressed bytes staged per segment (its tokens' fields, mostly)
+constexpr int64_t EMIT_WAVE_MAX = 65536;  // segments (about 4 blocks of 4 MiB text)
 __global__ __launch_bounds__(T) void emit_kernel(int nb, int nseg_all, Scratch sc) {
     __shared__ alignas(16) uint8_t stg[EWV][ESTG];
     const int l = lane_id();
@@ -387,16 +404,7 @@ __global__ __launch_bounds__(T) void emit_kernel(int nb, int nseg_all, Scratch s
     while (x < s1) {
         const uint32_t tok = rd[x];
         const Tok t = parse_rd(rd, n, x, true);
-        // literal-length bytes: liblz4 stops reading them (a "loop error" it
-        // ignores) once its input position reaches iend-15 after a 255 byte;
-        // lenip < iend-14 means the terminator was read before that point
-        bool ok = !t.cut && ((tok >> 4) != 15 || t.lenip < n - 14);
-        if (t.last) {
-            ok = ok && t.lit_end == n && op + t.ll <= cap;
-        } else {
-            ok = ok && t.lit_end <= n - 8 && op + t.ll <= cap - 12 && t.off >= 1 && t.off <= op + t.ll &&
-                 ((tok & 15) != 15 || t.mlip < n - 4) && op + t.ll + t.ml <= cap - 5;
-        }
+        const bool ok = tok_ok(tok, t, n, op, cap);
         if (!ok) {
             if (l == 0) st.bad = 1;
             return;
@@ -415,6 +423,74 @@ __global__ __launch_bounds__(T) void emit_kernel(int nb, int nseg_all, Scratch s
         for (int32_t i = l; i < ml; i += 64) {
             const uint32_t ui = (uint32_t)i;
             org[op + i] = (uint32_t)(base + (ui < off ? ui : ui % off));
+        }
+        op += t.ml;
+        x = t.next;
+    }
+}
+
+// One THREAD per segment (large batches: 64 segments per wave do the most
+// work per instruction; the wave form above wins only while the segments are
+// too few to fill the GPU -- a 16-block chunk ran 20 % slower in it).
+__global__ __launch_bounds__(T) void emit_thread_kernel(int nb, int nseg_all, Scratch sc) {
+    const int g = blockIdx.x * T + threadIdx.x;
+    if (g >= nseg_all) return;
+    const int b = block_of(sc.blk, nb, g);
+    BStat &st = sc.st[b];
+    if (st.fix[FIX_ROUNDS - 1] || st.bad) return;
+    const SBlock B = sc.blk[b];
+    const gc_u8 *s = (const gc_u8 *)B.src;
+    g_u32 *org = (g_u32 *)(sc.org + B.org_off);
+    const int64_t n = B.n, cap = B.cap, k = g - B.seg0;
+    const int64_t s0 = k * SEG, s1 = s0 + SEG < n ? s0 + SEG : n;
+    int64_t x = sc.entry[g], op = sc.cnt[g];
+    while (x < s1) {
+        const uint32_t tok = s[x];
+        const Tok t = parse(s, n, x, true);
+        const bool ok = tok_ok(tok, t, n, op, cap);
+        if (!ok) {
+            st.bad = 1;
+            return;
+        }
+        // origin entries, 16-byte stores where the run is 4-aligned (the
+        // area starts 16-byte aligned: org_off is a multiple of 4 entries)
+        {
+            const uint32_t v0 = (uint32_t)(-(t.lenip) - 1);  // entry i = v0 - i
+            int64_t i = 0;
+            for (; i < t.ll && ((op + i) & 3); i++) org[op + i] = v0 - (uint32_t)i;
+            for (; i + 4 <= t.ll; i += 4) {
+                const uint32_t v = v0 - (uint32_t)i;
+                *(g_u4 *)(org + op + i) = make_uint4(v, v - 1u, v - 2u, v - 3u);
+            }
+            for (; i < t.ll; i++) org[op + i] = v0 - (uint32_t)i;
+        }
+        op += t.ll;
+        if (t.last) {
+            st.last_ok = 1;
+            return;
+        }
+        {
+            const int64_t base = op - t.off;
+            const uint32_t off = (uint32_t)t.off;
+            uint32_t j = 0;  // entry i = base + (i mod off)
+            int64_t i = 0;
+            for (; i < t.ml && ((op + i) & 3); i++) {
+                org[op + i] = (uint32_t)(base + j);
+                j = j + 1 == off ? 0u : j + 1;
+            }
+            for (; i + 4 <= t.ml; i += 4) {
+                uint32_t e[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    e[q] = (uint32_t)(base + j);
+                    j = j + 1 == off ? 0u : j + 1;
+                }
+                *(g_u4 *)(org + op + i) = make_uint4(e[0], e[1], e[2], e[3]);
+            }
+            for (; i < t.ml; i++) {
+                org[op + i] = (uint32_t)(base + j);
+                j = j + 1 == off ? 0u : j + 1;
+            }
         }
         op += t.ml;
         x = t.next;
@@ -569,8 +645,14 @@ extern "C" int jfs_launch_lz4_split(const jfs_dev_block *d_desc, int nb, int32_t
         hipLaunchKernelGGL(count_kernel, dim3(gs), dim3(T), 0, st, nb, (int)nseg_all, sc);
     }
     hipLaunchKernelGGL(scan_kernel, dim3(nb), dim3(T), 0, st, sc);
-    if (nseg_all > 0)
-        hipLaunchKernelGGL(emit_kernel, dim3((unsigned)((nseg_all + EWV - 1) / EWV)), dim3(T), 0, st, nb, (int)nseg_all, sc);
+    if (nseg_all > 0) {
+        // a wave per segment while that leaves the GPU short of waves (a lone
+        // block: ~16 k segments), a thread per segment beyond
+        if (nseg_all <= EMIT_WAVE_MAX)
+            hipLaunchKernelGGL(emit_kernel, dim3((unsigned)((nseg_all + EWV - 1) / EWV)), dim3(T), 0, st, nb, (int)nseg_all, sc);
+        else
+            hipLaunchKernelGGL(emit_thread_kernel, dim3((unsigned)gs), dim3(T), 0, st, nb, (int)nseg_all, sc);
+    }
     // jump grid: about 2,048 workgroups in all (every entry of a 4 MiB block
     // is covered after a few strides), at most one per 1,024 entries
     const unsigned jx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((max_cap / 4 + T) / T, (2048 + nb - 1) / nb));

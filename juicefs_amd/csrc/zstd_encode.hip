@@ -805,13 +805,17 @@ constexpr int SPEC_MAXSEG = 4096;        // segments per frame (the merge's flag
 // offsets in block order and the loop's state from segment to segment; every
 // thread takes one bucket through the frame's segments (prefix maxima of the
 // write sets).  Flags only ever rise (zl1_spec_parse clears its own).
+// any[r]: round r changed something.  The host looks every few rounds; a
+// round after a settled one exits at once (and would change nothing anyway).
 __global__ __launch_bounds__(256) void zl1_spec_merge(const FInfo *__restrict__ fi, const int32_t *__restrict__ sflist,
                                                       const int32_t *__restrict__ sslot, const int32_t *__restrict__ snseg,
                                                       const BInfo *__restrict__ bi, const uint32_t *__restrict__ W,
                                                       uint32_t *__restrict__ I, SpecB *__restrict__ sp,
-                                                      int32_t *__restrict__ any, int first) {
+                                                      int32_t *__restrict__ any, int r) {
     __shared__ uint32_t mark[SPEC_MAXSEG / 32];
     __shared__ int32_t anyc;
+    const int first = r == 0;
+    if (r >= 2 && !any[r - 1]) return;
     const FInfo F = fi[sflist[blockIdx.x]];
     const int32_t s0 = sslot[blockIdx.x], nseg = snseg[blockIdx.x];
     const uint32_t tsize = 1u << F.hlog;
@@ -849,20 +853,30 @@ __global__ __launch_bounds__(256) void zl1_spec_merge(const FInfo *__restrict__ 
     const uint32_t h = blockIdx.y * 256 + t;
     if (h < tsize) {
         uint32_t run = 0;
-        for (int32_t s = 0; s < nseg; s++) {
-            const size_t o = (size_t)(s0 + s) * SPEC_TSZ + h;
-            if (I[o] != run) {
-                I[o] = run;
-                atomicOr(&mark[s >> 5], 1u << (s & 31));
-                anyc = 1;
+        for (int32_t s1 = 0; s1 < nseg; s1 += 8) {  // eight segments' loads in flight
+            uint32_t iv[8], wv[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const size_t o = (size_t)(s0 + s1 + u) * SPEC_TSZ + h;
+                iv[u] = s1 + u < nseg ? I[o] : 0u;
+                wv[u] = s1 + u < nseg ? W[o] : 0u;
             }
-            run = umax32(run, W[o]);
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int32_t s = s1 + u;
+                if (s < nseg && iv[u] != run) {
+                    I[(size_t)(s0 + s) * SPEC_TSZ + h] = run;
+                    atomicOr(&mark[s >> 5], 1u << (s & 31));
+                    anyc = 1;
+                }
+                run = umax32(run, wv[u]);
+            }
         }
     }
     __syncthreads();
     for (int32_t s = t; s < nseg; s += 256)
         if ((mark[s >> 5] >> (s & 31)) & 1u) sp[s0 + s].chg = 1;
-    if (t == 0 && anyc) atomicOr(any, 1);
+    if (t == 0 && anyc) atomicOr(&any[r], 1);
 }
 
 // one wave per segment whose inputs changed
@@ -2233,7 +2247,8 @@ struct ZL1Scratch {
         return true;
     }
 };
-ZL1Scratch g_zl1[16];
+// two per device: the coalescer's two lanes encode at once
+ZL1Scratch g_zl1[16][2];
 inline size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
 }  // namespace
 
@@ -2271,8 +2286,21 @@ extern "C" int jfs_launch_zstd_encode(const jfs_dev_block *d_blocks, int nblk, i
     if (nblk <= 0) return 0;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return -1;
-    ZL1Scratch &z = g_zl1[dev];
-    std::lock_guard<std::mutex> lk(z.mu);
+    // a free scratch of this device (blocking on the first only if both are taken)
+    ZL1Scratch *zp = nullptr;
+    std::unique_lock<std::mutex> lk;
+    for (int i = 0; i < 2 && !zp; i++) {
+        std::unique_lock<std::mutex> t(g_zl1[dev][i].mu, std::try_to_lock);
+        if (t.owns_lock()) {
+            lk = std::move(t);
+            zp = &g_zl1[dev][i];
+        }
+    }
+    if (!zp) {
+        lk = std::unique_lock<std::mutex>(g_zl1[dev][0].mu);
+        zp = &g_zl1[dev][0];
+    }
+    ZL1Scratch &z = *zp;
     // the descriptors may have been written on this stream: read them after it drains
     std::vector<jfs_dev_block> h(nblk);
     if (hipMemcpyAsync(h.data(), d_blocks, sizeof(jfs_dev_block) * nblk, hipMemcpyDeviceToHost, stream) != hipSuccess ||
@@ -2371,7 +2399,7 @@ extern "C" int jfs_launch_zstd_encode(const jfs_dev_block *d_blocks, int nblk, i
                  yb = a256((size_t)std::max<int64_t>(byte_total, 1)), hb = a256(sizeof(uint32_t) * 1024 * (size_t)std::max(nbk, 1)),
                  tb = a256(sizeof(LitTab) * (size_t)std::max(nbk, 1));
     const size_t spb = nsb ? a256(sizeof(int32_t) * (3 * (size_t)nsf + nspb + 16)) + a256(sizeof(SpecB) * nsb) +
-                                 2 * a256(sizeof(uint32_t) * SPEC_TSZ * (size_t)nsb) + 256
+                                 2 * a256(sizeof(uint32_t) * SPEC_TSZ * (size_t)nsb) + a256(sizeof(int32_t) * (maxseg + 3))
                            : 0;
     if (!z.grow(fb + bb + lb + sb + yb + hb + tb + spb)) return -1;
     uint8_t *p = z.d;
@@ -2432,14 +2460,15 @@ extern "C" int jfs_launch_zstd_encode(const jfs_dev_block *d_blocks, int nblk, i
             const int32_t *d_sf = d_slists, *d_ss = d_slists + nsf, *d_sn = d_slists + 2 * nsf,
                           *d_bf = d_slists + 3 * nsf;
             bool settled = false;
-            for (int r = 0; r <= maxseg + 1; r++) {
-                if (hipMemsetAsync(d_any, 0, sizeof(int32_t), stream) != hipSuccess) return -1;
+            const int rmax = maxseg + 2;  // (segments + 1 rounds settle any frame)
+            if (hipMemsetAsync(d_any, 0, sizeof(int32_t) * (rmax + 1), stream) != hipSuccess) return -1;
+            for (int r = 0; r <= rmax; r++) {
                 hipLaunchKernelGGL(zl1_spec_merge, dim3(nsf, SPEC_TSZ / 256), dim3(256), 0, stream, d_fi, d_sf, d_ss,
-                                   d_sn, d_bi, d_W, d_I, d_sp, d_any, r == 0 ? 1 : 0);
+                                   d_sn, d_bi, d_W, d_I, d_sp, d_any, r);
                 if (hipGetLastError() != hipSuccess) return -1;
-                if (r > 0) {
+                if (r > 0 && (r % 4 == 0 || r == rmax)) {  // a look every four rounds
                     int32_t h_any = 1;
-                    if (hipMemcpyAsync(&h_any, d_any, sizeof(int32_t), hipMemcpyDeviceToHost, stream) != hipSuccess ||
+                    if (hipMemcpyAsync(&h_any, d_any + r, sizeof(int32_t), hipMemcpyDeviceToHost, stream) != hipSuccess ||
                         hipStreamSynchronize(stream) != hipSuccess)
                         return -1;
                     if (!h_any) { settled = true; break; }

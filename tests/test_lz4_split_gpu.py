@@ -70,6 +70,20 @@ def test_split_text_blocks_stay_on_the_split_path(gpu, oracle):
     assert done == 2 * len(srcs) and handed == 0, (done, handed)
 
 
+def test_split_many_text_blocks_thread_emit(gpu, oracle):
+    """Eight 4 MiB text blocks in one launch (~130 k segments: past
+    EMIT_WAVE_MAX, the thread-per-segment emit): exact, and on the split path."""
+    srcs = [gen_block("T", 4400 + i, 4 << 20) for i in range(8)]
+    comps = [oracle.lz4_compress(s)[1] for s in srcs]
+    assert sum((len(c) + 127) // 128 for c in comps) > 65536
+    D.lz4_split_counts(reset=True)
+    r, outs = run_small(comps, [len(s) for s in srcs], gpu, mis=3)
+    assert r == [len(s) for s in srcs]
+    assert all(o == s for o, s in zip(outs, srcs))
+    done, handed = D.lz4_split_counts()[:2]
+    assert done == len(srcs) and handed == 0, (done, handed)
+
+
 def test_split_blocks_vs_oracle_all_classes(gpu, oracle):
     cases = [(cls, n) for cls in "TZR" for n in (1, 12, 13, 100, 4096, 65535, 65547, 131072, 1 << 20)] + [
         ("T", 4 << 20), ("Z", 4 << 20), ("R", 4 << 20)]
