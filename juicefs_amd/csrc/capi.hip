@@ -1405,6 +1405,14 @@ int64_t gather_probe_us() {
     return v;
 }
 
+int64_t gather_probe_enc_us() {
+    static const int64_t v = [] {
+        const char *e = getenv("JFS_GATHER_PROBE_ENC_US");
+        return e ? std::max(0ll, atoll(e)) : 300ll;
+    }();
+    return v;
+}
+
 // Work of one block for the dealer: the bytes it stages in and out.
 int64_t block_cost(const jfs_iov &v) { return std::max<int64_t>(v.src_len, 0) + std::max<int64_t>(v.dst_cap, 0) + 4096; }
 
@@ -1542,16 +1550,18 @@ class Coalescer {
                 // has followed it within that probe; under load the calls that
                 // arrive while a batch runs form the next one.  (A burst's first
                 // call alone costs the burst little: the 200-way legs measured
-                // the same with a 40 us probe and without.)  Encode always gathers:
-                // an encode batch lasts about one block's parse whatever its
-                // size -- a lone first call would put the rest of a burst
-                // behind a whole extra batch.
+                // the same with a 40 us probe and without.)  Encode probes
+                // longer (JFS_GATHER_PROBE_ENC_US, default 300): an encode
+                // batch lasts about one block's parse whatever its size, so a
+                // burst's first call sent alone would put the rest behind a
+                // whole extra batch -- a burst's second call comes within the
+                // probe, and a lone upload skips the 2 ms gather.
                 Gather gw = gather_window(dir);
-                if (dir == DECOMPRESS && waiting_batches_ == 0 && queued_like(algo, dir) == 1) {
+                if (waiting_batches_ == 0 && queued_like(algo, dir) == 1) {
                     const uint64_t s0 = arrivals_;
-                    if (gather_probe_us() > 0)
-                        cv_work_.wait_until(lk, std::chrono::steady_clock::now() +
-                                                    std::chrono::microseconds(gather_probe_us()),
+                    const int64_t probe = dir == DECOMPRESS ? gather_probe_us() : gather_probe_enc_us();
+                    if (probe > 0)
+                        cv_work_.wait_until(lk, std::chrono::steady_clock::now() + std::chrono::microseconds(probe),
                                             [&] { return arrivals_ != s0; });
                     if (arrivals_ == s0) gw.gap_us = 0;
                 }

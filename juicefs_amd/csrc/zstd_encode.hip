@@ -801,13 +801,13 @@ struct SpecB {
 constexpr uint32_t SPEC_TSZ = 1u << 14;  // table slots per segment (wide frames: hashLog <= 14)
 constexpr int SPEC_MAXSEG = 4096;        // segments per frame (the merge's flags)
 
-// grid (frame, 256-bucket chunk): chunk 0's thread 0 passes the repeat
-// offsets in block order and the loop's state from segment to segment; every
-// thread takes one bucket through the frame's segments (prefix maxima of the
-// write sets).  Flags only ever rise (zl1_spec_parse clears its own).
+// grid (frame, 64-bucket chunk): chunk 0 hands every segment its inputs
+// (repeat offsets, the loop's state: a thread per segment); every thread
+// takes one bucket through the frame's segments (prefix maxima of the write
+// sets).  Flags only ever rise (zl1_spec_parse clears its own).
 // any[r]: round r changed something.  The host looks every few rounds; a
 // round after a settled one exits at once (and would change nothing anyway).
-__global__ __launch_bounds__(256) void zl1_spec_merge(const FInfo *__restrict__ fi, const int32_t *__restrict__ sflist,
+__global__ __launch_bounds__(64) void zl1_spec_merge(const FInfo *__restrict__ fi, const int32_t *__restrict__ sflist,
                                                       const int32_t *__restrict__ sslot, const int32_t *__restrict__ snseg,
                                                       const BInfo *__restrict__ bi, const uint32_t *__restrict__ W,
                                                       uint32_t *__restrict__ I, SpecB *__restrict__ sp,
@@ -820,15 +820,27 @@ __global__ __launch_bounds__(256) void zl1_spec_merge(const FInfo *__restrict__ 
     const int32_t s0 = sslot[blockIdx.x], nseg = snseg[blockIdx.x];
     const uint32_t tsize = 1u << F.hlog;
     const int t = threadIdx.x;
-    for (int i = t; i < SPEC_MAXSEG / 32; i += 256) mark[i] = 0;
+    for (int i = t; i < SPEC_MAXSEG / 32; i += 64) mark[i] = 0;
     if (t == 0) anyc = 0;
     __syncthreads();
-    if (blockIdx.y == 0 && t == 0) {
-        uint32_t r0 = 1, r1 = 4;  // repStartValue
-        for (int32_t s = 0; s < nseg; s++) {
+    if (blockIdx.y == 0) {
+        // a segment after a block's first takes its predecessor's state; a
+        // block's first takes the repeat offsets of the nearest earlier block
+        // that passes them on (compressed-assumed, >= 7 bytes), else
+        // repStartValue -- independent per segment, one thread each
+        for (int32_t s = t; s < nseg; s += 64) {
             SpecB &x = sp[s0 + s];
             bool c = first != 0;
             if (x.q == 0) {
+                uint32_t r0 = 1, r1 = 4;
+                for (int32_t j = x.blk - 1; j >= F.b0; j--) {
+                    const BInfo &Bj = bi[j];
+                    if (Bj.be - Bj.bs >= 7 && (Bj.flags & F_ASSUMED)) {
+                        r0 = Bj.rout0;
+                        r1 = Bj.rout1;
+                        break;
+                    }
+                }
                 c |= x.rin0 != r0 || x.rin1 != r1;
                 x.rin0 = r0;
                 x.rin1 = r1;
@@ -842,27 +854,21 @@ __global__ __launch_bounds__(256) void zl1_spec_merge(const FInfo *__restrict__ 
                 atomicOr(&mark[s >> 5], 1u << (s & 31));
                 anyc = 1;
             }
-            const bool lastq = s + 1 == nseg || sp[s0 + s + 1].q == 0;
-            const BInfo &B = bi[x.blk];
-            if (lastq && B.be - B.bs >= 7 && (B.flags & F_ASSUMED)) {
-                r0 = B.rout0;
-                r1 = B.rout1;
-            }
         }
     }
-    const uint32_t h = blockIdx.y * 256 + t;
+    const uint32_t h = blockIdx.y * 64 + t;
     if (h < tsize) {
         uint32_t run = 0;
-        for (int32_t s1 = 0; s1 < nseg; s1 += 8) {  // eight segments' loads in flight
-            uint32_t iv[8], wv[8];
+        for (int32_t s1 = 0; s1 < nseg; s1 += 16) {  // sixteen segments' loads in flight
+            uint32_t iv[16], wv[16];
 #pragma unroll
-            for (int u = 0; u < 8; u++) {
+            for (int u = 0; u < 16; u++) {
                 const size_t o = (size_t)(s0 + s1 + u) * SPEC_TSZ + h;
                 iv[u] = s1 + u < nseg ? I[o] : 0u;
                 wv[u] = s1 + u < nseg ? W[o] : 0u;
             }
 #pragma unroll
-            for (int u = 0; u < 8; u++) {
+            for (int u = 0; u < 16; u++) {
                 const int32_t s = s1 + u;
                 if (s < nseg && iv[u] != run) {
                     I[(size_t)(s0 + s) * SPEC_TSZ + h] = run;
@@ -874,7 +880,7 @@ __global__ __launch_bounds__(256) void zl1_spec_merge(const FInfo *__restrict__ 
         }
     }
     __syncthreads();
-    for (int32_t s = t; s < nseg; s += 256)
+    for (int32_t s = t; s < nseg; s += 64)
         if ((mark[s >> 5] >> (s & 31)) & 1u) sp[s0 + s].chg = 1;
     if (t == 0 && anyc) atomicOr(&any[r], 1);
 }
@@ -2265,10 +2271,11 @@ extern "C" int jfs_zpprof_reset() {
 // Small batches take the block-parallel speculative parse (zl1_spec_*) for
 // their multi-block frames: at most JFS_ZL1_SPEC_MAX blocks in all (default
 // 2,048; 0 = never).  Larger batches fill the GPU with frame-serial parses.
-// segments per block of the speculative parse at most (1, 2, 4, 8, 16)
+// segments per block of the speculative parse at most (1, 2, 4, 8, 16;
+// default 16: a lone 4 MiB frame 37.5 ms one-call vs 40.8 at 8, 68 at 4)
 int spec_segs() {  // (read per launch: the tests sweep it)
     const char *e = getenv("JFS_ZL1_SEGS");
-    const int p = e ? atoi(e) : 8;
+    const int p = e ? atoi(e) : 16;
     int q = 1;
     while (q * 2 <= p && q < 16) q *= 2;
     return q;
@@ -2346,7 +2353,7 @@ extern "C" int jfs_launch_zstd_encode(const jfs_dev_block *d_blocks, int nblk, i
     // blocks in slots grouped by hashLog
     // frames, their blocks in slots grouped by hashLog; a block takes
     // segsz-byte segments (one slot each) when the batch has few blocks: the
-    // most segments per block (<= JFS_ZL1_SEGS, default 8) that keep the slots
+    // most segments per block (<= JFS_ZL1_SEGS, default 16) that keep the slots
     // within the ~1,024 waves the GPU holds at once (four per CU by LDS)
     std::vector<int32_t> sf, sslot, snseg, bfirst;
     std::vector<SpecB> slots;
@@ -2393,7 +2400,7 @@ extern "C" int jfs_launch_zstd_encode(const jfs_dev_block *d_blocks, int nblk, i
     const int nsf = (int)sf.size(), nsb = (int)slots.size(), nspb = bfirst.empty() ? 0 : (int)bfirst.size() - 1;
     int maxseg = 0;
     for (int32_t c : snseg) maxseg = std::max(maxseg, c);
-    if (maxseg > SPEC_MAXSEG) return -1;  // (cannot happen: <= 2,048 blocks x 8)
+    if (maxseg > SPEC_MAXSEG) return -1;  // (cannot happen: <= 1,024 slots, or 2,048 blocks x 1)
     const size_t fb = a256(sizeof(FInfo) * nblk), bb = a256(sizeof(BInfo) * std::max(nbk, 1)),
                  lb = a256(sizeof(int32_t) * (2 * (size_t)nblk + (size_t)nbk + 16)), sb = a256(sizeof(uint64_t) * (size_t)std::max<int64_t>(seq_total, 1)),
                  yb = a256((size_t)std::max<int64_t>(byte_total, 1)), hb = a256(sizeof(uint32_t) * 1024 * (size_t)std::max(nbk, 1)),
@@ -2463,7 +2470,7 @@ extern "C" int jfs_launch_zstd_encode(const jfs_dev_block *d_blocks, int nblk, i
             const int rmax = maxseg + 2;  // (segments + 1 rounds settle any frame)
             if (hipMemsetAsync(d_any, 0, sizeof(int32_t) * (rmax + 1), stream) != hipSuccess) return -1;
             for (int r = 0; r <= rmax; r++) {
-                hipLaunchKernelGGL(zl1_spec_merge, dim3(nsf, SPEC_TSZ / 256), dim3(256), 0, stream, d_fi, d_sf, d_ss,
+                hipLaunchKernelGGL(zl1_spec_merge, dim3(nsf, SPEC_TSZ / 64), dim3(64), 0, stream, d_fi, d_sf, d_ss,
                                    d_sn, d_bi, d_W, d_I, d_sp, d_any, r);
                 if (hipGetLastError() != hipSuccess) return -1;
                 if (r > 0 && (r % 4 == 0 || r == rmax)) {  // a look every four rounds
