@@ -1266,7 +1266,74 @@ struct SeqSmem {
     uint8_t hdr[3][128];
     int32_t hsz[3], type[3];
     uint32_t lastc[3];
+    uint32_t ring[256];  // sequence bitstream staging (8,192 bits)
 };
+
+// A wave's bit writer through an LDS ring of 256 dwords: bit 0 of the ring is
+// bit 0 of the dword holding the stream's first byte (dst + o); complete
+// dwords are stored as they fill, the bytes of that first dword before the
+// stream are kept, nothing is written at or past byte `lim` of dst (a stream
+// that does not fit only reports it).
+struct RingW {
+    uint32_t *ring;
+    g_u8 *base;          // dword-aligned
+    int64_t first_byte;  // bytes of dword 0 before the stream
+    int64_t limb;        // byte limit, from base
+    uint64_t bitpos;     // next bit, from base
+    uint64_t flushed;    // dwords stored
+};
+__device__ __forceinline__ void rw_init(RingW &w, uint32_t *ring, g_u8 *dst, int64_t o, int64_t lim) {
+    w.ring = ring;
+    w.base = (g_u8 *)((uintptr_t)(dst + o) & ~(uintptr_t)3);
+    w.first_byte = (int64_t)((uintptr_t)(dst + o) & 3u);
+    w.limb = w.first_byte + (lim - o);
+    w.bitpos = (uint64_t)w.first_byte * 8;
+    w.flushed = 0;
+    for (int k = lane_id(); k < 256; k += 64) ring[k] = 0;
+    __syncthreads();
+}
+// OR n (<= 32) bits of v in at bit p (lanes at once; p from base)
+__device__ __forceinline__ void rw_or(RingW &w, uint64_t p, uint32_t v, uint32_t n) {
+    if (!n) return;
+    v &= (uint32_t)((1ull << n) - 1ull);
+    const uint32_t d = (uint32_t)(p >> 5) & 255u, sh = (uint32_t)(p & 31u);
+    atomicOr(&w.ring[d], v << sh);
+    if (sh + n > 32) atomicOr(&w.ring[(d + 1) & 255u], v >> (32 - sh));
+}
+// store the dwords below bitpos that are complete
+__device__ __forceinline__ void rw_flush(RingW &w) {
+    const int l = lane_id();
+    __syncthreads();
+    const uint64_t full = w.bitpos >> 5;
+    for (uint64_t dw = w.flushed + l; dw < full; dw += 64) {
+        const uint32_t v = w.ring[dw & 255u];
+        if (dw == 0 && w.first_byte > 0) {
+            for (int k = (int)w.first_byte; k < 4; k++)
+                if (k < w.limb) w.base[k] = (uint8_t)(v >> (8 * k));
+        } else if ((int64_t)dw * 4 + 4 <= w.limb) {
+            ((g_u32 *)w.base)[dw] = v;
+        }
+        w.ring[dw & 255u] = 0;
+    }
+    __syncthreads();
+    w.flushed = full;
+}
+// the last partial dword; returns the stream's end (bytes from dst + o)
+__device__ __forceinline__ int64_t rw_close(RingW &w) {
+    const int l = lane_id();
+    rw_flush(w);
+    const uint64_t endbyte = (w.bitpos + 7) >> 3;
+    const uint64_t lastdw = (endbyte + 3) >> 2;
+    for (uint64_t dw = w.flushed + l; dw < lastdw; dw += 64) {
+        const uint32_t v = w.ring[dw & 255u];
+        for (int k = 0; k < 4; k++) {
+            const int64_t by = (int64_t)dw * 4 + k;
+            if (by >= w.first_byte && by < (int64_t)endbyte && by < w.limb) w.base[by] = (uint8_t)(v >> (8 * k));
+        }
+    }
+    __syncthreads();
+    return (int64_t)endbyte - w.first_byte;
+}
 
 __global__ __launch_bounds__(64) void zl1_seq_kernel(const FInfo *__restrict__ fi, const int32_t *__restrict__ blist,
                                                      BInfo *__restrict__ bi, const uint64_t *__restrict__ seqs,
@@ -1440,16 +1507,13 @@ __global__ __launch_bounds__(64) void zl1_seq_kernel(const FInfo *__restrict__ f
         for (int k = l; k < s.hsz[t]; k += 64) sec[o + k] = s.hdr[t][k];
         o += s.hsz[t];
     }
-    // ZSTD_encodeSequences: last sequence first; per 64 sequences the lanes
-    // look up everything that does not depend on the states, the serial loop
-    // steps the three states and packs the bits
-    BitW w;
-    w.dst = sec;
-    w.wp = o;
-    w.lim = cap;
-    w.bc = 0;
-    w.bp = 0;
-    w.ovf = false;
+    // ZSTD_encodeSequences: last sequence first, 64 at a time.  A scalar
+    // state pass steps the three states and leaves each sequence's state bits
+    // (OF, ML, LL) in its lane; then every lane ORs its sequence's bits --
+    // state bits, LL, ML and OF extra bits -- into the LDS bit ring at a
+    // prefix-summed position (the serial writer's bits in its order).
+    RingW w;
+    rw_init(w, s.ring, sec, o, cap);
     uint32_t sML = 0, sOF = 0, sLL = 0;
     for (int64_t c0 = ns - 1; c0 >= 0; c0 -= 64) {
         const int64_t i = c0 - l;
@@ -1463,15 +1527,13 @@ __global__ __launch_bounds__(64) void zl1_seq_kernel(const FInfo *__restrict__ f
         const uint32_t lc = ll_code(ll), mc = ml_code(mlb), oc = hbit(ofv);
         const int32_t dO = s.tOF.dnb[oc], dM = s.tML.dnb[mc], dL = s.tLL.dnb[lc];
         const int32_t fO = s.tOF.dfs[oc], fM = s.tML.dfs[mc], fL = s.tLL.dfs[lc];
-        const uint32_t nbits = (uint32_t)LL_BITS[lc] | ((uint32_t)ML_BITS[mc] << 8) | (oc << 16);
         const int nj = c0 + 1 < 64 ? (int)(c0 + 1) : 64;
+        uint32_t stv = 0, stn = 0;  // lane jj: sequence c0 - jj's state bits and their count
         for (int jj = 0; jj < nj; ++jj) {
             const int32_t jdO = (int32_t)readlane((uint32_t)dO, jj), jdM = (int32_t)readlane((uint32_t)dM, jj),
                           jdL = (int32_t)readlane((uint32_t)dL, jj);
             const int32_t jfO = (int32_t)readlane((uint32_t)fO, jj), jfM = (int32_t)readlane((uint32_t)fM, jj),
                           jfL = (int32_t)readlane((uint32_t)fL, jj);
-            const uint32_t jnb = readlane(nbits, jj);
-            const uint32_t jll = readlane(ll, jj), jml = readlane(mlb, jj), jof = readlane(ofv, jj);
             if (c0 == ns - 1 && jj == 0) {  // FSE_initCState2 with the last sequence
                 const uint32_t nM = (uint32_t)((jdM + (1 << 15)) >> 16), nO = (uint32_t)((jdO + (1 << 15)) >> 16),
                                nL = (uint32_t)((jdL + (1 << 15)) >> 16);
@@ -1481,41 +1543,53 @@ __global__ __launch_bounds__(64) void zl1_seq_kernel(const FInfo *__restrict__ f
             } else {
                 const uint32_t nO = (uint32_t)(((int32_t)sOF + jdO) >> 16), nM = (uint32_t)(((int32_t)sML + jdM) >> 16),
                                nL = (uint32_t)(((int32_t)sLL + jdL) >> 16);
-                bw_add(w, sOF, (int)nO);
-                bw_add(w, sML, (int)nM);
-                bw_add(w, sLL, (int)nL);
+                const uint32_t v = (sOF & ((1u << nO) - 1u)) | ((sML & ((1u << nM) - 1u)) << nO) |
+                                   ((sLL & ((1u << nL) - 1u)) << (nO + nM));
+                if (l == jj) {
+                    stv = v;
+                    stn = nO + nM + nL;
+                }
                 const uint32_t tO = s.tOF.st[(sOF >> nO) + (uint32_t)jfO], tM = s.tML.st[(sML >> nM) + (uint32_t)jfM],
                                tL = s.tLL.st[(sLL >> nL) + (uint32_t)jfL];
                 sOF = tO;
                 sML = tM;
                 sLL = tL;
-                bw_flush(w);
             }
-            bw_add(w, jll, (int)(jnb & 0xFFu));
-            bw_add(w, jml, (int)((jnb >> 8) & 0xFFu));
-            bw_flush(w);
-            bw_add(w, jof, (int)(jnb >> 16));
-            bw_flush(w);
         }
+        // the lanes' bits: state bits, then LL, ML, OF extra bits
+        const uint32_t nll = l < nj ? (uint32_t)LL_BITS[lc] : 0u, nml = l < nj ? (uint32_t)ML_BITS[mc] : 0u,
+                       nof = l < nj ? oc : 0u;
+        const uint32_t tot = stn + nll + nml + nof;
+        uint32_t sum = 0;
+        const uint32_t ex = wave_scan_excl(tot, &sum);
+        uint64_t p = w.bitpos + ex;
+        rw_or(w, p, stv, stn);
+        p += stn;
+        rw_or(w, p, ll, nll);
+        p += nll;
+        rw_or(w, p, mlb, nml);
+        p += nml;
+        rw_or(w, p, ofv, nof);
+        w.bitpos += sum;
+        rw_flush(w);
     }
-    bw_add(w, sML, s.tML.tlog);
-    bw_flush(w);
-    bw_add(w, sOF, s.tOF.tlog);
-    bw_flush(w);
-    bw_add(w, sLL, s.tLL.tlog);
-    bw_flush(w);
-    bw_add(w, 1, 1);  // end mark
-    bw_flush(w);
-    if (w.bp > 0) {
-        if (w.wp + 1 > w.lim) w.ovf = true;
-        if (!w.ovf && l == 0) w.dst[w.wp] = (uint8_t)w.bc;
-        w.wp++;
+    if (l == 0) {  // the final states (ML, OF, LL) and the end mark
+        uint64_t p = w.bitpos;
+        rw_or(w, p, sML, (uint32_t)s.tML.tlog);
+        p += (uint32_t)s.tML.tlog;
+        rw_or(w, p, sOF, (uint32_t)s.tOF.tlog);
+        p += (uint32_t)s.tOF.tlog;
+        rw_or(w, p, sLL, (uint32_t)s.tLL.tlog);
+        p += (uint32_t)s.tLL.tlog;
+        rw_or(w, p, 1u, 1u);
     }
+    w.bitpos += (uint64_t)(s.tML.tlog + s.tOF.tlog + s.tLL.tlog + 1);
+    const int64_t wp = o + rw_close(w);
     if (l == 0) {
-        B.secsz = w.ovf ? -1 : (int32_t)w.wp;
+        B.secsz = wp > cap ? -1 : (int32_t)wp;
         // zstd <= 1.3.4 decoder workaround: a last FSE_Compressed table
         // description closer than 4 bytes to the end -> raw block
-        B.flags = (lastnc >= 0 && w.wp - lastnc < 4) ? (flags | F_LASTNC) : (flags & ~F_LASTNC);
+        B.flags = (lastnc >= 0 && wp - lastnc < 4) ? (flags | F_LASTNC) : (flags & ~F_LASTNC);
     }
 }
 
