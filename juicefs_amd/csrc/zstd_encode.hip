@@ -2355,6 +2355,15 @@ int spec_segs() {  // (read per launch: the tests sweep it)
     return q;
 }
 
+// slots (segments) a small batch may take at most (JFS_ZL1_SLOTS; default
+// 4,096: 20 concurrent 4 MiB frames take 4 segments per block, 187 ms a burst
+// vs 198 with whole blocks and 228 with 2 -- the late rounds, with few
+// changed segments, are the cheap ones; 128 KiB of scratch per slot)
+int spec_slots() {
+    const char *e = getenv("JFS_ZL1_SLOTS");
+    return e ? std::max(1, atoi(e)) : 4096;
+}
+
 int spec_max_blocks() {
     static int v = [] {
         const char *e = getenv("JFS_ZL1_SPEC_MAX");
@@ -2434,12 +2443,15 @@ extern "C" int jfs_launch_zstd_encode(const jfs_dev_block *d_blocks, int nblk, i
     std::vector<std::pair<uint32_t, std::pair<int, int>>> sgrp;  // hashLog -> (first slot, slots)
     int32_t segsz = BLK;
     {
-        int64_t cand = 0;
+        int64_t cand = 0, fmax = 0;
         for (int f = 0; f < nblk; f++)
-            if (fi[f].status == 0 && fi[f].nb >= 2 && fi[f].n >= 65536) cand += fi[f].nb;
+            if (fi[f].status == 0 && fi[f].nb >= 2 && fi[f].n >= 65536) {
+                cand += fi[f].nb;
+                fmax = std::max<int64_t>(fmax, fi[f].nb);
+            }
         if (cand > 0 && cand <= spec_max_blocks()) {
             int P = spec_segs();
-            while (P > 1 && cand * P > 1024) P >>= 1;
+            while (P > 1 && (cand * P > spec_slots() || fmax * P > SPEC_MAXSEG)) P >>= 1;
             segsz = BLK / P;
             for (uint32_t hl = 6; hl <= 14; hl++) {
                 const int g0 = (int)slots.size();
@@ -2474,7 +2486,7 @@ extern "C" int jfs_launch_zstd_encode(const jfs_dev_block *d_blocks, int nblk, i
     const int nsf = (int)sf.size(), nsb = (int)slots.size(), nspb = bfirst.empty() ? 0 : (int)bfirst.size() - 1;
     int maxseg = 0;
     for (int32_t c : snseg) maxseg = std::max(maxseg, c);
-    if (maxseg > SPEC_MAXSEG) return -1;  // (cannot happen: <= 1,024 slots, or 2,048 blocks x 1)
+    if (maxseg > SPEC_MAXSEG) return -1;  // (cannot happen: P keeps every frame within it)
     const size_t fb = a256(sizeof(FInfo) * nblk), bb = a256(sizeof(BInfo) * std::max(nbk, 1)),
                  lb = a256(sizeof(int32_t) * (2 * (size_t)nblk + (size_t)nbk + 16)), sb = a256(sizeof(uint64_t) * (size_t)std::max<int64_t>(seq_total, 1)),
                  yb = a256((size_t)std::max<int64_t>(byte_total, 1)), hb = a256(sizeof(uint32_t) * 1024 * (size_t)std::max(nbk, 1)),
