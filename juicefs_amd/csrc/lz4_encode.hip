@@ -1198,15 +1198,17 @@ int64_t eseg_warm() {
     return v;
 }
 // Segment length: about 2,048 segments over the batch (8 waves per CU), at
-// least 64 KiB (JFS_LZ4E_SEG_MIN_KB).  A difference between two rounds travels
+// least 32 KiB (JFS_LZ4E_SEG_MIN_KB).  A difference between two rounds travels
 // about one segment per round, and some persist for tens of KiB of input
 // (hash-table entries live until overwritten), so shorter segments need more
-// rounds: on 4 MiB text blocks 16 KiB did not settle in 8 rounds, 32 KiB took
-// 7, 64 KiB 4-6 (scripts/eseg_timing.py).
+// rounds (scripts/eseg_timing.py, 4 MiB text, round 6): 64 KiB settles in 4-6
+// rounds (1 block 37.1 ms, 8 blocks 53.3), 32 KiB in 6-9 (34.7, 45.6), 16 KiB
+// in 9-13 (30.9, 42.2) -- too close to the 16-round cap past which a block
+// takes the serial parse.
 int64_t eseg_len(int nblk, const int32_t *lens) {
     static int64_t lmin = [] {
         const char *e = getenv("JFS_LZ4E_SEG_MIN_KB");
-        return (int64_t)(e ? atoi(e) : 64) << 10;
+        return (int64_t)(e ? atoi(e) : 32) << 10;
     }();
     int64_t tot = 0;
     for (int b = 0; b < nblk; ++b) tot += lens[b] > 0 ? lens[b] : 0;
