@@ -2619,7 +2619,7 @@ int launch_split(const jfs_dev_block *d_blocks, int nblk, int32_t *d_ret, jfs::z
                            sc);
     hipLaunchKernelGGL(zsfix_kernel, dim3(nblk), dim3(64), 0, st, d_blocks, nblk, d_info, d_items, sc);
     if (nbk > 0)
-        hipLaunchKernelGGL(zsemit_kernel, dim3((unsigned)nbk), dim3(ST), 0, st, nblk, (const ZInfo *)d_info,
+        hipLaunchKernelGGL(zsemit_kernel, dim3((unsigned)nbk, ZSE_PARTS), dim3(ST), 0, st, nblk, (const ZInfo *)d_info,
                            (const uint4 *)d_items, sc);
     const unsigned jx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((max_cap / 4 + ST) / ST, (2048 + nblk - 1) / nblk));
     // Rounds: after round r every entry points >= SJ_HOPS^r steps up its chain
