@@ -1497,6 +1497,8 @@ class Coalescer {
         std::vector<DevCtx *> &ds = devices();
         if (ds.empty()) return JFS_ERR_NO_DEVICE;
         start(ds);
+        int64_t res = 0;
+        if (dir == DECOMPRESS && inline_lone() && run_inline(ds, algo, dir, iov, &res)) return res;
         Pending p{algo, dir, iov, 0, false, {}};
         std::unique_lock<std::mutex> lk(mu_);
         q_.push_back(&p);
@@ -1526,6 +1528,55 @@ class Coalescer {
             for (DevCtx *d : ds)
                 for (int k = 0; k < NLANE; k++) std::thread([this, d, k] { worker(d, d->lane[k]); }).detach();
         });
+    }
+    // A decode that finds nothing queued and no batch waiting on the devices
+    // (a lone cache miss) runs on the calling thread when a lane is free: no
+    // hand-off to a worker and back (JFS_INLINE_LONE=0: always hand off).  It
+    // counts as a waiting batch, so calls arriving meanwhile gather.
+    static bool inline_lone() {
+        static const bool v = [] {
+            const char *e = getenv("JFS_INLINE_LONE");
+            return !e || atoi(e) != 0;
+        }();
+        return v;
+    }
+    bool run_inline(std::vector<DevCtx *> &ds, int algo, int dir, const jfs_iov &iov, int64_t *res) {
+        DevCtx *dev = nullptr;
+        Lane *ln = nullptr;
+        std::unique_lock<std::mutex> lane_lk;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            if (!q_.empty() || gathering_ || waiting_batches_ != 0) return false;
+            for (DevCtx *d : ds) {  // (lanes are only ever try-locked here)
+                for (int k = 0; k < NLANE && !ln; k++) {
+                    std::unique_lock<std::mutex> t(d->lane[k].mu, std::try_to_lock);
+                    if (t.owns_lock()) {
+                        lane_lk = std::move(t);
+                        dev = d;
+                        ln = &d->lane[k];
+                    }
+                }
+                if (ln) break;
+            }
+            if (!ln) return false;
+            waiting_batches_++;
+        }
+        const double t0 = host_trace() ? now_ms() : 0.0;
+        jfs_iov v = iov;
+        int64_t out = 0;
+        if (run_batch(dev, *ln, algo, dir, 1, &v, &out, nullptr, nullptr, 0, nullptr) != JFS_OK)
+            run_isolated(dev, *ln, algo, dir, 1, &v, &out);
+        lane_lk.unlock();
+        if (host_trace())
+            fprintf(stderr, "[jfs coalescer] t=%.2f dev %d lane %d algo %d dir %d: 1 call inline, ran %.2f ms\n",
+                    now_ms(), dev->id, (int)(ln - dev->lane), algo, dir, now_ms() - t0);
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            waiting_batches_--;
+        }
+        cv_work_.notify_all();  // calls that queued meanwhile
+        *res = out;
+        return true;
     }
     int queued_like(int algo, int dir) const {
         int n = 0;
