@@ -188,6 +188,60 @@ def test_mixed_codecs_and_errors_in_one_burst(gpu, lib, blocks, oracle):
     assert not bad, [(t, res[t]) for t in bad[:5]]
 
 
+def test_lone_and_overlapping_calls(gpu, lib, blocks, oracle):
+    """A call that finds its device idle runs on the calling thread (capi.hip
+    run_inline, JFS_INLINE_LONE); calls that arrive while it runs queue for the
+    worker lanes.  A lone call is one device batch; then six threads with
+    jittered starts mix LZ4 / Zstd decodes and LZ4 compresses (so inline and
+    queued calls overlap): every result is exactly its own block's."""
+    import random
+    import time
+    from juicefs_amd import compress as C
+    raws, comps = blocks
+    zs = C.ZStandard()
+    zfr = []
+    for r in raws[:2]:
+        d = bytearray(zs.CompressBound(U))
+        k, e = zs.Compress(d, r)
+        assert e is None
+        zfr.append(bytes(d[:k]))
+    src0 = ctypes.create_string_buffer(comps[0], len(comps[0]))
+    dst0 = ctypes.create_string_buffer(U)
+    lib.jfs_decompress(L.ALGO_LZ4, dst0, U, src0, len(comps[0]))  # warm
+    lib.jfs_stats_reset()
+    assert lib.jfs_decompress(L.ALGO_LZ4, dst0, U, src0, len(comps[0])) == U and dst0.raw == raws[0]
+    st = _stats(lib)[L.ALGO_LZ4 * 2 + 1]
+    assert st.calls == 1 and st.blocks == 1 and st.batches == 1 and st.errors == 0
+    bound = lib.jfs_compress_bound(L.ALGO_LZ4, U)
+    nt, k = 6, 10
+    bad = []
+
+    def work(t):
+        rng = random.Random(t)
+        dst = ctypes.create_string_buffer(max(U, bound))
+        for r in range(k):
+            time.sleep(rng.random() * 0.004)
+            kind = (t + r) % 3
+            i = (t * k + r) % 8
+            if kind == 0:
+                s = ctypes.create_string_buffer(comps[i], len(comps[i]))
+                ok = lib.jfs_decompress(L.ALGO_LZ4, dst, U, s, len(comps[i])) == U and dst.raw[:U] == raws[i]
+            elif kind == 1:
+                z = zfr[i % 2]
+                s = ctypes.create_string_buffer(z, len(z))
+                ok = lib.jfs_decompress(L.ALGO_ZSTD, dst, U, s, len(z)) == U and dst.raw[:U] == raws[i % 2]
+            else:
+                s = ctypes.create_string_buffer(raws[i], U)
+                n = lib.jfs_compress(L.ALGO_LZ4, dst, bound, s, U)
+                ok = n == len(comps[i]) and dst.raw[:n] == comps[i]
+            if not ok:
+                bad.append((t, r, kind))
+    th = [threading.Thread(target=work, args=(t,)) for t in range(nt)]
+    [x.start() for x in th]
+    [x.join() for x in th]
+    assert not bad, bad[:5]
+
+
 CHILD_ZSTD_FIRST = r'''
 import sys, numpy as np, torch
 sys.path.insert(0, sys.argv[1])
