@@ -420,9 +420,13 @@ __global__ __launch_bounds__(T) void emit_kernel(int nb, int nseg_all, Scratch s
         // match entry i = op - off + (i mod off): overlapped matches point before the match
         const int64_t base = op - t.off;
         const uint32_t off = (uint32_t)t.off;
-        for (int32_t i = l; i < ml; i += 64) {
-            const uint32_t ui = (uint32_t)i;
-            org[op + i] = (uint32_t)(base + (ui < off ? ui : ui % off));
+        if (off >= (uint32_t)ml) {  // no overlap (most matches): no modulo
+            for (int32_t i = l; i < ml; i += 64) org[op + i] = (uint32_t)(base + i);
+        } else {
+            for (int32_t i = l; i < ml; i += 64) {
+                const uint32_t ui = (uint32_t)i;
+                org[op + i] = (uint32_t)(base + (ui < off ? ui : ui % off));
+            }
         }
         op += t.ml;
         x = t.next;
