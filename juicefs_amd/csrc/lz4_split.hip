@@ -81,26 +81,34 @@ struct Scratch {
 
 // one token at x (x < n): next token position, output bytes, and the fields
 // the acceptance conditions need.  A token whose literals reach n is the last.
+// 32-bit positions and lengths (the plan sends blocks with n or cap >= 2^30 to
+// the exact kernel): the wave-per-segment emit parses in scalar registers, and
+// 64-bit fields cost it two scalar ops per add and a VALU round trip per
+// compare.  A length field stops growing at 2^30: such a token ends past n
+// (or its match past cap) either way, so it is rejected as before.
+constexpr int32_t LEN_CAP = 1 << 30;
 struct Tok {
-    int64_t lenip;   // input position after the literal-length bytes
-    int64_t ll;      // literal length
-    int64_t lit_end; // lenip + ll
-    int64_t next;    // next token (n for the last token)
-    int64_t mlip;    // input position after the match-length bytes
-    int64_t ml;      // match length (0 for the last token)
+    uint32_t tok;    // the token byte
+    int32_t lenip;   // input position after the literal-length bytes
+    int32_t ll;      // literal length
+    int32_t lit_end; // lenip + ll
+    int32_t next;    // next token (n for the last token)
+    int32_t mlip;    // input position after the match-length bytes
+    int32_t ml;      // match length (0 for the last token)
     int32_t off;
     bool last, cut;  // cut: the stream ends inside the token's header fields
 };
 
 template <class RD>
-__device__ __forceinline__ Tok parse_rd(RD s, int64_t n, int64_t x, bool want_off) {
+__device__ __forceinline__ Tok parse_rd(RD s, int32_t n, int32_t x, bool want_off) {
     Tok t;
     t.cut = false;
     t.off = 0;
     t.ml = 0;
     const uint32_t tok = s[x];
-    int64_t ip = x + 1;
-    int64_t ll = tok >> 4;
+    t.tok = tok;
+    int32_t ip = x + 1;
+    int32_t ll = (int32_t)(tok >> 4);
     if (ll == 15) {
         uint32_t b;
         do {
@@ -109,8 +117,8 @@ __device__ __forceinline__ Tok parse_rd(RD s, int64_t n, int64_t x, bool want_of
                 break;
             }
             b = s[ip++];
-            ll += b;
-        } while (b == 255 && ll < (1ll << 31));
+            ll += (int32_t)b;
+        } while (b == 255 && ll < LEN_CAP);
     }
     t.lenip = ip;
     t.ll = ll;
@@ -122,7 +130,7 @@ __device__ __forceinline__ Tok parse_rd(RD s, int64_t n, int64_t x, bool want_of
         return t;
     }
     t.last = false;
-    int64_t q = t.lit_end;
+    int32_t q = t.lit_end;
     if (q + 2 > n) {
         t.cut = true;
         t.next = n;
@@ -130,7 +138,7 @@ __device__ __forceinline__ Tok parse_rd(RD s, int64_t n, int64_t x, bool want_of
     }
     if (want_off) t.off = (int32_t)s[q] | ((int32_t)s[q + 1] << 8);
     q += 2;
-    int64_t ml = tok & 15;
+    int32_t ml = (int32_t)(tok & 15);
     if (ml == 15) {
         uint32_t b;
         do {
@@ -139,15 +147,15 @@ __device__ __forceinline__ Tok parse_rd(RD s, int64_t n, int64_t x, bool want_of
                 break;
             }
             b = s[q++];
-            ml += b;
-        } while (b == 255 && ml < (1ll << 31));
+            ml += (int32_t)b;
+        } while (b == 255 && ml < LEN_CAP);
     }
     t.mlip = q;
     t.ml = ml + 4;
     t.next = q;
     return t;
 }
-__device__ __forceinline__ Tok parse(const gc_u8 *s, int64_t n, int64_t x, bool want_off) {
+__device__ __forceinline__ Tok parse(const gc_u8 *s, int32_t n, int32_t x, bool want_off) {
     return parse_rd(s, n, x, want_off);
 }
 
@@ -183,7 +191,7 @@ __global__ void plan_kernel(const jfs_dev_block *__restrict__ desc, int nb, Scra
             s.n = d.src_len > 0 ? d.src_len : 0;
             s.cap = d.dst_cap > 0 ? d.dst_cap : 0;
             const int64_t ns = (s.n + SEG - 1) / SEG, no = ((int64_t)s.cap + 3) & ~3ll;
-            if (s.cap > max_cap || seg + ns > nseg_all || org + no > norg_all) {
+            if (s.cap > max_cap || seg + ns > nseg_all || org + no > norg_all || s.n >= LEN_CAP || s.cap >= LEN_CAP) {
                 s.n = 0;
                 s.cap = 0;
                 sc.st[b].bad = 1;
@@ -205,12 +213,12 @@ __global__ __launch_bounds__(T) void spec_kernel(int nb, int nseg_all, Scratch s
     const int b = block_of(sc.blk, nb, g);
     const SBlock B = sc.blk[b];
     const gc_u8 *s = (const gc_u8 *)B.src;
-    const int64_t n = B.n, k = g - B.seg0;
-    const int64_t s0 = k * SEG, s1 = s0 + SEG < n ? s0 + SEG : n;
+    const int32_t n = B.n, k = g - B.seg0;
+    const int32_t s0 = k * SEG, s1 = s0 + SEG < n ? s0 + SEG : n;
     uint32_t m[SEG / 32];
 #pragma unroll
     for (int w = 0; w < SEG / 32; w++) m[w] = 0;
-    int64_t x = s0;
+    int32_t x = s0;
     while (x < s1) {
         const uint32_t rel = (uint32_t)(x - s0), w = rel >> 5, bit = 1u << (rel & 31);
 #pragma unroll
@@ -220,7 +228,7 @@ __global__ __launch_bounds__(T) void spec_kernel(int nb, int nseg_all, Scratch s
     g_u32 *bits = (g_u32 *)(sc.bits + B.bits_off + k * (SEG / 32));
 #pragma unroll
     for (int i = 0; i < SEG / 32; i++) bits[i] = m[i];
-    const int32_t ex = (int32_t)(x < n ? x : n);
+    const int32_t ex = x < n ? x : n;
     sc.spec_exit[g] = ex;
     if (k + 1 < B.nseg) sc.entry[g + 1] = ex;
     if (k == 0) sc.entry[g] = 0;
@@ -228,14 +236,14 @@ __global__ __launch_bounds__(T) void spec_kernel(int nb, int nseg_all, Scratch s
 
 // exit of segment (s0, s1) entered at x: walk until the chain meets a marked
 // position (then it is the speculative chain, whose exit is known) or leaves
-__device__ __forceinline__ int32_t seg_exit(const gc_u8 *s, int64_t n, int64_t s0, int64_t s1, int64_t x,
+__device__ __forceinline__ int32_t seg_exit(const gc_u8 *s, int32_t n, int32_t s0, int32_t s1, int32_t x,
                                            const gc_u32 *bits, int32_t spec_ex) {
     while (x < s1) {
         const uint32_t rel = (uint32_t)(x - s0);
         if ((bits[rel >> 5] >> (rel & 31)) & 1u) return spec_ex;
         x = parse(s, n, x, false).next;
     }
-    return (int32_t)(x < n ? x : n);
+    return x < n ? x : n;
 }
 
 // One fix-up round.  Inside a workgroup the segments' entries live in LDS and
@@ -251,7 +259,7 @@ __global__ __launch_bounds__(T) void fix_kernel(int nb, int nseg_all, Scratch sc
     const bool valid = g < nseg_all;
     int b = 0;
     SBlock B{};
-    int64_t k = 0;
+    int32_t k = 0;
     bool active = false;
     if (valid) {
         b = block_of(sc.blk, nb, g);
@@ -262,7 +270,7 @@ __global__ __launch_bounds__(T) void fix_kernel(int nb, int nseg_all, Scratch sc
     const int32_t e0 = valid ? sc.entry[g] : 0;
     ent[t] = e0;
     const gc_u8 *s = (const gc_u8 *)B.src;
-    const int64_t n = B.n, s0 = k * SEG, s1 = s0 + SEG < n ? s0 + SEG : n;
+    const int32_t n = B.n, s0 = k * SEG, s1 = s0 + SEG < n ? s0 + SEG : n;
     const gc_u32 *bits = (const gc_u32 *)(sc.bits + B.bits_off + k * (SEG / 32));
     const int32_t spec_ex = active ? sc.spec_exit[g] : 0;
     int32_t last_in = -1, ex = -1;
@@ -296,12 +304,13 @@ __global__ __launch_bounds__(T) void count_kernel(int nb, int nseg_all, Scratch 
     if (sc.st[b].fix[FIX_ROUNDS - 1]) return;  // did not converge: exact path
     const SBlock B = sc.blk[b];
     const gc_u8 *s = (const gc_u8 *)B.src;
-    const int64_t n = B.n, k = g - B.seg0;
-    const int64_t s0 = k * SEG, s1 = s0 + SEG < n ? s0 + SEG : n;
-    int64_t x = sc.entry[g], c = 0;
+    const int32_t n = B.n, k = g - B.seg0;
+    const int32_t s0 = k * SEG, s1 = s0 + SEG < n ? s0 + SEG : n;
+    int32_t x = sc.entry[g];
+    int64_t c = 0;
     while (x < s1) {
         const Tok t = parse(s, n, x, false);
-        c += t.ll + t.ml;
+        c += (int64_t)t.ll + t.ml;
         if (c > B.cap) break;
         x = t.next;
     }
@@ -341,7 +350,9 @@ __global__ __launch_bounds__(T) void scan_kernel(Scratch sc) {
 
 // the token checks the exact decoder makes (the emit keeps a token only if
 // it would run it the same way)
-__device__ __forceinline__ bool tok_ok(uint32_t tok, const Tok &t, int64_t n, int64_t op, int64_t cap) {
+__device__ __forceinline__ bool tok_ok(uint32_t tok, const Tok &t, int32_t n, int32_t op, int32_t cap) {
+    // (op <= cap < 2^30 and every length < 2^30 + 2^8: no sum below overflows;
+    // the last is evaluated only once op + ll <= cap - 12 holds)
     // literal-length bytes: liblz4 stops reading them (a "loop error" it
     // ignores) once its input position reaches iend-15 after a 255 byte;
     // lenip < iend-14 means the terminator was read before that point
@@ -374,10 +385,10 @@ __global__ __launch_bounds__(T) void emit_kernel(int nb, int nseg_all, Scratch s
     const gc_u8 *s = (const gc_u8 *)(((uint64_t)uniform((uint32_t)((uint64_t)(uintptr_t)B.src >> 32)) << 32) |
                                      uniform((uint32_t)(uintptr_t)B.src));
     g_u32 *org = (g_u32 *)(sc.org + B.org_off);
-    const int64_t n = (int32_t)uniform((uint32_t)B.n), cap = (int32_t)uniform((uint32_t)B.cap),
+    const int32_t n = (int32_t)uniform((uint32_t)B.n), cap = (int32_t)uniform((uint32_t)B.cap),
                   k = g - (int32_t)uniform((uint32_t)B.seg0);
-    const int64_t s0 = k * SEG, s1 = s0 + SEG < n ? s0 + SEG : n;
-    int64_t x = (int32_t)uniform((uint32_t)sc.entry[g]), op = (int32_t)uniform((uint32_t)sc.cnt[g]);
+    const int32_t s0 = k * SEG, s1 = s0 + SEG < n ? s0 + SEG : n;
+    int32_t x = (int32_t)uniform((uint32_t)sc.entry[g]), op = (int32_t)uniform((uint32_t)sc.cnt[g]);
     // the parse reads the segment's bytes from LDS (one wave-uniform LDS round
     // trip per field instead of an L2 one); bytes past the staging from HBM
     uint8_t *buf = stg[threadIdx.x >> 6];
@@ -392,25 +403,24 @@ __global__ __launch_bounds__(T) void emit_kernel(int nb, int nseg_all, Scratch s
     struct Rd {
         const gc_u8 *s;
         const uint8_t *buf;
-        uintptr_t a0;
-        __device__ uint32_t operator[](int64_t p) const {  // (p wave-uniform: scalar branch)
-            const uint32_t r = (uint32_t)uniform((uint32_t)((uintptr_t)(s + p) - a0));
+        int32_t A;  // stream position of buf[0] (a0 - s: s0 less its misalignment)
+        __device__ uint32_t operator[](int32_t p) const {  // (p wave-uniform: scalar branch)
+            const uint32_t r = (uint32_t)(p - A);
             uint32_t v;
-            if ((uintptr_t)(s + p) - a0 < (uintptr_t)ESTG) v = buf[r];
+            if (r < (uint32_t)ESTG) v = buf[r];
             else v = s[p];
             return uniform(v);
         }
-    } rd{s, buf, a0};
+    } rd{s, buf, s0 - (int32_t)((uintptr_t)(s + s0) & 15u)};
     while (x < s1) {
-        const uint32_t tok = rd[x];
         const Tok t = parse_rd(rd, n, x, true);
-        const bool ok = tok_ok(tok, t, n, op, cap);
+        const bool ok = tok_ok(t.tok, t, n, op, cap);
         if (!ok) {
             if (l == 0) st.bad = 1;
             return;
         }
         const uint32_t v0 = (uint32_t)(-(t.lenip) - 1);  // literal entry i = v0 - i
-        const int32_t ll = (int32_t)t.ll, ml = (int32_t)t.ml;
+        const int32_t ll = t.ll, ml = t.ml;
         for (int32_t i = l; i < ll; i += 64) org[op + i] = v0 - (uint32_t)i;
         op += t.ll;
         if (t.last) {
@@ -418,7 +428,7 @@ __global__ __launch_bounds__(T) void emit_kernel(int nb, int nseg_all, Scratch s
             return;
         }
         // match entry i = op - off + (i mod off): overlapped matches point before the match
-        const int64_t base = op - t.off;
+        const int32_t base = op - t.off;
         const uint32_t off = (uint32_t)t.off;
         if (off >= (uint32_t)ml) {  // no overlap (most matches): no modulo
             for (int32_t i = l; i < ml; i += 64) org[op + i] = (uint32_t)(base + i);
@@ -445,13 +455,12 @@ __global__ __launch_bounds__(T) void emit_thread_kernel(int nb, int nseg_all, Sc
     const SBlock B = sc.blk[b];
     const gc_u8 *s = (const gc_u8 *)B.src;
     g_u32 *org = (g_u32 *)(sc.org + B.org_off);
-    const int64_t n = B.n, cap = B.cap, k = g - B.seg0;
-    const int64_t s0 = k * SEG, s1 = s0 + SEG < n ? s0 + SEG : n;
-    int64_t x = sc.entry[g], op = sc.cnt[g];
+    const int32_t n = B.n, cap = B.cap, k = g - B.seg0;
+    const int32_t s0 = k * SEG, s1 = s0 + SEG < n ? s0 + SEG : n;
+    int32_t x = sc.entry[g], op = sc.cnt[g];
     while (x < s1) {
-        const uint32_t tok = s[x];
         const Tok t = parse(s, n, x, true);
-        const bool ok = tok_ok(tok, t, n, op, cap);
+        const bool ok = tok_ok(t.tok, t, n, op, cap);
         if (!ok) {
             st.bad = 1;
             return;
@@ -460,7 +469,7 @@ __global__ __launch_bounds__(T) void emit_thread_kernel(int nb, int nseg_all, Sc
         // area starts 16-byte aligned: org_off is a multiple of 4 entries)
         {
             const uint32_t v0 = (uint32_t)(-(t.lenip) - 1);  // entry i = v0 - i
-            int64_t i = 0;
+            int32_t i = 0;
             for (; i < t.ll && ((op + i) & 3); i++) org[op + i] = v0 - (uint32_t)i;
             for (; i + 4 <= t.ll; i += 4) {
                 const uint32_t v = v0 - (uint32_t)i;
@@ -474,10 +483,10 @@ __global__ __launch_bounds__(T) void emit_thread_kernel(int nb, int nseg_all, Sc
             return;
         }
         {
-            const int64_t base = op - t.off;
+            const int32_t base = op - t.off;
             const uint32_t off = (uint32_t)t.off;
             uint32_t j = 0;  // entry i = base + (i mod off)
-            int64_t i = 0;
+            int32_t i = 0;
             for (; i < t.ml && ((op + i) & 3); i++) {
                 org[op + i] = (uint32_t)(base + j);
                 j = j + 1 == off ? 0u : j + 1;
