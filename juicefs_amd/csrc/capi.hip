@@ -96,6 +96,21 @@ int64_t staging_max_bytes() {
 #define JFS_NPIECE 4
 #endif
 constexpr int NPIECE = JFS_NPIECE;
+
+// Output pieces of a one-block chunk (a lone cache miss): its output D2H goes
+// in NPIECE byte ranges and the caller copies each out as soon as it lands,
+// spinning on the piece's event (a blocking wait per piece cost more than the
+// overlap saved).  Lone 4 MiB one-call decode: LZ4 0.77-0.81 -> 0.71-0.74 ms,
+// Zstd 2.35-2.37 -> 2.28-2.30 ms (scripts/r6_bpiece.sh).  JFS_BYTE_PIECES=n
+// overrides (0 or 1 = whole).
+int byte_npiece() {
+    static int v = [] {
+        const char *e = getenv("JFS_BYTE_PIECES");
+        return e ? std::min(NPIECE, std::max(0, atoi(e))) : NPIECE;
+    }();
+    return v;
+}
+
 static_assert(NPIECE >= 1, "at least one output piece per chunk (finish() waits on ev_p[npiece - 1])");
 struct Slot {
     hipEvent_t ev_in = nullptr, ev_k = nullptr, ev = nullptr;  // H2D done, kernel done, D2H done
@@ -800,21 +815,19 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
     // aead extras per block: descriptor, second result, 64 bytes of key (32) + nonce (12)
     const int64_t aeb = ae ? (int64_t)sizeof(jfs_aead_block) + 4 + 64 : 0;
     // output pieces of a chunk (see NPIECE): large chunks in block ranges
-    // [piece_b(c, p), piece_b(c, p + 1)); small chunks with a large output (a
-    // lone 4 MiB cache miss) in byte ranges of the output area, so that the
+    // [piece_b(c, p), piece_b(c, p + 1)); a one-block chunk (a lone cache
+    // miss) in byte ranges of the output area (byte_npiece), so that the
     // copy-out of one piece overlaps the D2H of the next; other small chunks
     // (the coalescer's 16-block ones) stay whole: a piece's host copy is a
     // thread-pool round of its own.  piece_o(c, p) = the piece's first byte.
-    // (byte pieces were measured for a lone 4 MiB decode: each piece's copy-out
-    // is a thread-pool round of its own, 0.51 vs 0.14 ms for the whole output)
-    auto byte_pieces = [&](const Chunk &c) { return false && c.e - c.s < 64; };
+    auto byte_pieces = [&](const Chunk &c) { return byte_npiece() > 1 && c.e - c.s == 1; };
     // input staging pieces: block ranges of large chunks only
     auto in_npiece = [&](const Chunk &c) { return c.e - c.s >= 64 ? std::min(NPIECE, c.e - c.s) : 1; };
     auto in_piece_b = [&](const Chunk &c, int p) {
         return c.s + (int)((int64_t)(c.e - c.s) * p / in_npiece(c));
     };
     auto npiece = [&](const Chunk &c) {
-        return c.e - c.s >= 64 ? std::min(NPIECE, c.e - c.s) : byte_pieces(c) ? NPIECE : 1;
+        return c.e - c.s >= 64 ? std::min(NPIECE, c.e - c.s) : byte_pieces(c) ? byte_npiece() : 1;
     };
     auto piece_b = [&](const Chunk &c, int p) {
         return byte_pieces(c) ? c.s : c.s + (int)((int64_t)(c.e - c.s) * p / npiece(c));
@@ -1224,7 +1237,14 @@ int64_t run_batch(DevCtx *dev, Lane &ln, int algo, int dir, int nblk, const jfs_
         } else {
             for (int i = c.s; i < c.e; i++) out[i] = finish_result(algo, dir, h_ret[i - c.s]);
             for (int p = 0; p < npiece(c); p++) {  // each piece's copy-out as soon as it landed
-                if (p > 0 && hipEventSynchronize(sl.ev_p[p]) != hipSuccess) return JFS_ERR_HIP;
+                if (p > 0 && byte_pieces(c)) {  // (a piece of a lone block: spin, it lands within microseconds)
+                    hipError_t q;
+                    while ((q = hipEventQuery(sl.ev_p[p])) == hipErrorNotReady) {
+                    }
+                    if (q != hipSuccess) return JFS_ERR_HIP;
+                } else if (p > 0 && hipEventSynchronize(sl.ev_p[p]) != hipSuccess) {
+                    return JFS_ERR_HIP;
+                }
                 std::vector<CopyJob> pj;
                 const int64_t p0 = piece_o(c, p), p1 = piece_o(c, p + 1);
                 const int i0 = byte_pieces(c) ? c.s : piece_b(c, p), i1 = byte_pieces(c) ? c.e : piece_b(c, p + 1);
