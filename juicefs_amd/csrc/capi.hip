@@ -97,17 +97,16 @@ int64_t staging_max_bytes() {
 #endif
 constexpr int NPIECE = JFS_NPIECE;
 
-// Output pieces of a one-block chunk (a lone cache miss), opt-in:
-// JFS_BYTE_PIECES=n (<= NPIECE) sends its output D2H in n byte ranges and the
-// caller copies each out as soon as it lands, spinning on the piece's event.
-// Standalone (scripts/r6_bpiece.sh) that took a lone 4 MiB decode LZ4
-// 0.77-0.81 -> 0.71-0.74 ms and Zstd 2.35-2.37 -> 2.28-2.30 ms, but inside the
-// bench process the LZ4 lone leg read 1.35 ms with it: off by
-// default.
+// Output pieces of a one-block chunk (a lone cache miss): its output D2H goes
+// in NPIECE byte ranges and the caller copies each out as soon as it lands,
+// spinning on the piece's event (a blocking wait per piece cost more than the
+// overlap saved).  Lone 4 MiB one-call decode in the full bench: LZ4 0.81 ->
+// 0.70 ms, Zstd 2.34 -> 2.23 ms (scripts/r6_bpiece3.sh).
+// JFS_BYTE_PIECES=n overrides (0 or 1 = whole output).
 int byte_npiece() {
     static int v = [] {
         const char *e = getenv("JFS_BYTE_PIECES");
-        return e ? std::min(NPIECE, std::max(0, atoi(e))) : 0;
+        return e ? std::min(NPIECE, std::max(0, atoi(e))) : NPIECE;
     }();
     return v;
 }
